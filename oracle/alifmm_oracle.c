@@ -1,0 +1,1480 @@
+/*
+ * oracle/alifmm_oracle.c — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement (plain C, double precision, no FMA contraction) of the reference's
+ * ALI-FMM hot path in /root/reference/Anis_TTF_rays.py.  It is the parity checker for the
+ * MI355X product (ali-fmm-and-ray-tracing_amd/), used only by tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg.  Nothing in the product links, loads or calls it.
+ *
+ * Semantics pinned to the reference (each function cites the lines it follows):
+ *   - Python float '%' (sign of divisor), round() = round-half-even (numba: llvm.rint),
+ *     math.floor -> int, math.degrees/radians = x*(180/pi) / x*(pi/180) (numba mathimpl).
+ *   - finer_grid_n quantisation: orientations -> int32 (truncation), vel_map -> float32
+ *     (Anis_TTF_rays.py:26-56, call sites :1527-1529, :2156-2158).
+ *   - The heap parent is round(t/2) with half-even rounding (:123,:135,:160,:172, SURVEY B-D3).
+ *   - travel() stage 1 passes nnz=nnx1 when updating close x-neighbours (:1645, SURVEY B-D2);
+ *     rows past the stage-1 array are read as nsts=-1 / ttn=0 ("padded" semantics).
+ * Parity is pinned by tests/golden/ *.npz, produced by oracle/gen_golden.py from the reference
+ * itself (numba 0.54 under /opt/conda python3.9, padded AST patch).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <pthread.h>
+
+#define DEG2RAD (M_PI / 180.0)
+#define RAD2DEG (180.0 / M_PI)
+
+static inline double pymod(double a, double b) {
+    /* CPython float_divmod / numba real_divmod_func_body */
+    double m = fmod(a, b);
+    if (m != 0.0) {
+        if ((b < 0) != (m < 0)) m += b;
+    } else {
+        m = copysign(0.0, b);
+    }
+    return m;
+}
+static inline long pyround(double x) { return (long)nearbyint(x); }
+static inline long imax(long a, long b) { return a > b ? a : b; }
+static inline long imin(long a, long b) { return a < b ? a : b; }
+
+/* ------------------------------------------------------------------------------------------ */
+/* Material view: a logical (nnz x nnx) grid whose cells read the caller's base arrays through
+ * per-axis index maps (window + nearest-neighbour refinement, finer_grid_n :26-91).           */
+typedef struct {
+    int nnz, nnx;
+    const int32_t *zmap, *xmap; /* logical index -> base index */
+    int nx0;                    /* base row stride */
+    const double *veln;
+    const int64_t *velpn;
+    const double *vel_map;
+    const int64_t *stif;        /* base (nz0, nx0, 5) or NULL (= Python None) */
+    int quant;                  /* finer_grid_n: veln -> int32, vel_map -> float32 */
+} mat_t;
+
+static inline size_t mat_base(const mat_t *m, int iz, int ix) {
+    return (size_t)m->zmap[iz] * (size_t)m->nx0 + (size_t)m->xmap[ix];
+}
+static inline double mat_veln(const mat_t *m, int iz, int ix) {
+    double v = m->veln[mat_base(m, iz, ix)];
+    return m->quant ? (double)(int32_t)v : v;
+}
+static inline long mat_velpn(const mat_t *m, int iz, int ix) { return (long)m->velpn[mat_base(m, iz, ix)]; }
+static inline double mat_velmap(const mat_t *m, int iz, int ix) {
+    double v = m->vel_map[mat_base(m, iz, ix)];
+    return m->quant ? (double)(float)v : v;
+}
+static inline const int64_t *mat_stif(const mat_t *m, int iz, int ix) {
+    return m->stif ? m->stif + 5 * mat_base(m, iz, ix) : NULL;
+}
+
+typedef struct { const double *tab; int ncol; } table_t; /* (361, ncol) row-major */
+
+/* Table lookup, linear in 1-degree bins (:288-291, :1372-1375, :2951-2954). */
+static inline double table_vel(const table_t *t, double eff, long col, double vm) {
+    long a1 = (long)floor(eff);
+    long a2 = (a1 + 1) % 180;
+    double rem = eff - (double)a1;
+    return vm * ((1 - rem) * t->tab[a1 * t->ncol + col] + rem * t->tab[a2 * t->ncol + col]);
+}
+
+/* Closed-form 2D orthotropic Christoffel GROUP velocity (:294-315; same formula :1566-1587,
+ * :2242-2263, :2957-2978, group_vel :3542-3558).  int64 arithmetic where the reference has it. */
+static double christoffel_group(const int64_t *s, double eff, double vm) {
+    int64_t sigma = s[4];
+    double e90 = pymod(eff, 90);
+    if (e90 < 0.01 || e90 > 90 - 0.01) {
+        int64_t lam = (fabs(pymod(eff, 180) - 90) < 1) ? s[2] : s[0];
+        return 1000 * vm * sqrt((double)lam / (double)sigma);
+    }
+    int64_t c22 = s[0], c23 = s[1], c33 = s[2], c44 = s[3];
+    double tan_ang = tan(eff * DEG2RAD);
+    int64_t A = c22 + c33 - 2 * c44;
+    double B = (double)(c23 + c44) * (tan_ang - 1 / tan_ang);
+    int64_t C = c22 - c33;
+    double disc = B * B + (double)(A * A) - (double)(C * C);
+    double pa;
+    if (eff < 90)
+        pa = pymod(atan((-B - sqrt(disc)) / (double)(C - A)), M_PI);
+    else
+        pa = pymod(atan((-B + sqrt(disc)) / (double)(C - A)), M_PI);
+    double lam = 0.5 * (cos(2 * pa) * (double)(c22 - c44) + sin(2 * pa) * (double)(c23 + c44) * tan_ang +
+                        (double)c22 + (double)c44);
+    return 1000 * vm * sqrt(lam / (double)sigma) / cos(eff * DEG2RAD - pa);
+}
+
+/* Christoffel PHASE velocity used by update() (:1400-1406). */
+static double christoffel_phase(const int64_t *s, double eff, double vm) {
+    double ca = cos(eff * DEG2RAD);
+    double sa = sin(eff * DEG2RAD);
+    double A = ca * ca * (double)s[0] + sa * sa * (double)s[3];
+    double B = ca * sa * (double)(s[1] + s[3]);
+    double C = ca * ca * (double)s[3] + sa * sa * (double)s[2];
+    return 1000 * vm * sqrt((A + C + sqrt((A - C) * (A - C) + 4 * (B * B))) / (double)(2 * s[4]));
+}
+
+/* group velocity with the fouds18_A / time_between_points selector
+ * 'velpn != 0 or stif_den == None' (:287, :2950) */
+static inline double group_vel_cell(const mat_t *m, const table_t *av, int iz, int ix, double eff) {
+    long p = mat_velpn(m, iz, ix);
+    const int64_t *s = mat_stif(m, iz, ix);
+    double vm = mat_velmap(m, iz, ix);
+    if (p != 0 || s == NULL) return table_vel(av, eff, p, vm);
+    return christoffel_group(s, eff, vm);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Field state of one FMM grid (ttn, nsts) with the stage-1 "padded" read semantics.         */
+typedef struct {
+    int nnz, nnx;      /* actual array dims */
+    double *ttn;
+    int32_t *nsts;
+    int32_t *btg;      /* heap: btg[2*k] = iz, btg[2*k+1] = ix, k >= 1 */
+    long ntr;
+    long maxbt;
+} fstate_t;
+
+static inline int32_t ST(const fstate_t *f, long z, long x) {
+    if (z >= f->nnz) return -1; /* padded rows: invalid */
+    return f->nsts[z * f->nnx + x];
+}
+static inline double TT(const fstate_t *f, long z, long x) {
+    if (z >= f->nnz) return 0.0;
+    return f->ttn[z * f->nnx + x];
+}
+
+/* heap :94-237 */
+static inline long hparent(long t) { return pyround((double)t / 2.0); }
+
+static int addtree(fstate_t *f, long iz, long ix) {
+    long nnx = f->nnx;
+    f->ntr += 1;
+    if (f->ntr >= f->maxbt) return -1;
+    f->nsts[iz * nnx + ix] = (int32_t)f->ntr;
+    f->btg[2 * f->ntr + 1] = (int32_t)ix;
+    f->btg[2 * f->ntr] = (int32_t)iz;
+    long tpc = f->ntr;
+    long tpp = hparent(tpc);
+    double tv = f->ttn[iz * nnx + ix];
+    while (tpp > 0) {
+        long aa = f->btg[2 * tpp], bb = f->btg[2 * tpp + 1];
+        if (tv < f->ttn[aa * nnx + bb]) {
+            f->nsts[iz * nnx + ix] = (int32_t)tpp;
+            f->nsts[(long)f->btg[2 * tpp] * nnx + f->btg[2 * tpp + 1]] = (int32_t)tpc;
+            int32_t e0 = f->btg[2 * tpc], e1 = f->btg[2 * tpc + 1];
+            f->btg[2 * tpc] = f->btg[2 * tpp];
+            f->btg[2 * tpc + 1] = f->btg[2 * tpp + 1];
+            f->btg[2 * tpp] = e0;
+            f->btg[2 * tpp + 1] = e1;
+            tpc = tpp;
+            tpp = hparent(tpc);
+        } else {
+            tpp = 0;
+        }
+    }
+    return 0;
+}
+
+static void updtree(fstate_t *f, long iz, long ix) {
+    long nnx = f->nnx;
+    long tpc = f->nsts[iz * nnx + ix];
+    long tpp = hparent(tpc);
+    double tv = f->ttn[iz * nnx + ix];
+    while (tpp > 0) {
+        if (tv < f->ttn[(long)f->btg[2 * tpp] * nnx + f->btg[2 * tpp + 1]]) {
+            f->nsts[iz * nnx + ix] = (int32_t)tpp;
+            f->nsts[(long)f->btg[2 * tpp] * nnx + f->btg[2 * tpp + 1]] = (int32_t)tpc;
+            int32_t e0 = f->btg[2 * tpc], e1 = f->btg[2 * tpc + 1];
+            f->btg[2 * tpc] = f->btg[2 * tpp];
+            f->btg[2 * tpc + 1] = f->btg[2 * tpp + 1];
+            f->btg[2 * tpp] = e0;
+            f->btg[2 * tpp + 1] = e1;
+            tpc = tpp;
+            tpp = hparent(tpc);
+        } else {
+            tpp = 0;
+        }
+    }
+}
+
+static inline double TB(const fstate_t *f, long k) {
+    return f->ttn[(long)f->btg[2 * k] * f->nnx + f->btg[2 * k + 1]];
+}
+static inline void hswap(fstate_t *f, long a, long b) {
+    int32_t e0 = f->btg[2 * a], e1 = f->btg[2 * a + 1];
+    f->btg[2 * a] = f->btg[2 * b];
+    f->btg[2 * a + 1] = f->btg[2 * b + 1];
+    f->btg[2 * b] = e0;
+    f->btg[2 * b + 1] = e1;
+}
+
+static void downtree(fstate_t *f) {
+    long nnx = f->nnx;
+    if (f->ntr == 1) { f->ntr -= 1; return; }
+    long ntr = f->ntr;
+    f->nsts[(long)f->btg[2 * ntr] * nnx + f->btg[2 * ntr + 1]] = 1;
+    f->btg[2] = f->btg[2 * ntr];
+    f->btg[3] = f->btg[2 * ntr + 1];
+    ntr = ntr - 1;
+    f->ntr = ntr;
+    long tpp = 1, tpc = 2 * tpp;
+    while (tpc < ntr) {
+        double rd1 = TB(f, tpc), rd2 = TB(f, tpc + 1);
+        if (rd1 > rd2) tpc = tpc + 1;
+        rd1 = TB(f, tpc);
+        rd2 = TB(f, tpp);
+        if (rd1 < rd2) {
+            f->nsts[(long)f->btg[2 * tpp] * nnx + f->btg[2 * tpp + 1]] = (int32_t)tpc;
+            f->nsts[(long)f->btg[2 * tpc] * nnx + f->btg[2 * tpc + 1]] = (int32_t)tpp;
+            hswap(f, tpc, tpp);
+            tpp = tpc;
+            tpc = 2 * tpp;
+        } else {
+            tpc = ntr + 1;
+        }
+    }
+    if (tpc == ntr) {
+        double rd1 = TB(f, tpc), rd2 = TB(f, tpp);
+        if (rd1 < rd2) {
+            f->nsts[(long)f->btg[2 * tpp] * nnx + f->btg[2 * tpp + 1]] = (int32_t)tpc;
+            f->nsts[(long)f->btg[2 * tpc] * nnx + f->btg[2 * tpc + 1]] = (int32_t)tpp;
+            hswap(f, tpc, tpp);
+        }
+    }
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* fouds18_A :240-901 — multi-stencil quadratic fallback with GROUP velocity.                 */
+static double slowness_at(const mat_t *m, const table_t *av, int iz, int ix, double eff) {
+    return 1.0 / group_vel_cell(m, av, iz, ix, eff);
+}
+
+double oref_fouds18_f(const fstate_t *f, const mat_t *m, const table_t *av, long iz, long ix, double dnx, double dnz,
+                      long nnx, long nnz) {
+#define N_(z, x) ST(f, (z), (x))
+#define T_(z, x) TT(f, (z), (x))
+    double veln = mat_veln(m, (int)iz, (int)ix);
+    /* ---- 0 deg stencil (:281-459) ---- */
+    int tsw1 = 0;
+    double travm = 0;
+    double eff = pymod(0 - veln, 180);
+    double slown = slowness_at(m, av, (int)iz, (int)ix, eff);
+    long jl[2] = {ix - 1, ix + 1};
+    for (int jj_ = 0; jj_ < 2; jj_++) {
+        long j = jl[jj_];
+        if (0 <= j && j <= nnx - 1) {
+            int swj = -1;
+            long j2;
+            if (j == ix - 1) {
+                j2 = j - 1;
+                if (j2 >= 0 && N_(iz, j2) == 0) swj = 0;
+            } else {
+                j2 = j + 1;
+                if (j2 <= nnx - 1 && N_(iz, j2) == 0) swj = 0;
+            }
+            if (N_(iz, j) == 0 && swj == 0) {
+                swj = -1;
+                if (T_(iz, j) >= T_(iz, j2)) swj = 0;
+            } else {
+                swj = -1;
+            }
+            long kl[2] = {iz - 1, iz + 1};
+            for (int kk_ = 0; kk_ < 2; kk_++) {
+                long k = kl[kk_];
+                if (0 <= k && k <= nnz - 1) {
+                    int swk = -1;
+                    long k2;
+                    if (k == iz - 1) {
+                        k2 = k - 1;
+                        if (k2 >= 0 && N_(k2, ix) == 0) swk = 0;
+                    } else {
+                        k2 = k + 1;
+                        if (k2 <= nnz - 1 && N_(k2, ix) == 0) swk = 0;
+                    }
+                    if (N_(k, ix) == 0 && swk == 0) {
+                        swk = -1;
+                        if (T_(k, ix) >= T_(k2, ix)) swk = 0;
+                    } else {
+                        swk = -1;
+                    }
+                    int swsol = 0;
+                    double a = 0, b = 0, c = 0, tref = 0, tdiv = 1, u, v;
+                    (void)v;
+                    if (swj == 0) {
+                        swsol = 1;
+                        if (swk == 0) {
+                            u = 2.0 * dnx;
+                            a = 18;
+                            b = -6 * (4.0 * T_(iz, j) - T_(iz, j2) + 4.0 * T_(k, ix) - T_(k2, ix));
+                            double p = 4.0 * T_(iz, j) - T_(iz, j2), q = 4.0 * T_(k, ix) - T_(k2, ix);
+                            c = p * p + q * q - 4 * (u * u) * (slown * slown);
+                            tref = 0.0; tdiv = 1.0;
+                        } else if (N_(k, ix) == 0) {
+                            u = dnz; v = 2.0 * dnx;
+                            a = 18;
+                            b = -6.0 * (3.0 * T_(k, ix) + 4.0 * T_(iz, j) - T_(iz, j2));
+                            double p = 3.0 * T_(k, ix), q = 4.0 * T_(iz, j) - T_(iz, j2);
+                            c = p * p + q * q - 4 * (v * v) * (slown * slown);
+                            tref = 0.0; tdiv = 1.0;
+                        } else {
+                            u = 2.0 * dnx;
+                            a = 1.0; b = 0.0;
+                            c = -(u * u) * (slown * slown);
+                            tref = 4.0 * T_(iz, j) - T_(iz, j2);
+                            tdiv = 1.0; /* tdiv=3.0 is overwritten by tdiv=1.0 (:389,:395) */
+                        }
+                    } else if (N_(iz, j) == 0) {
+                        swsol = 1;
+                        if (swk == 0) {
+                            u = dnx;
+                            double em = 3.0 * T_(iz, j) + 4.0 * T_(k, ix) - T_(k2, ix);
+                            a = 18; b = -6.0 * em;
+                            double p = 3.0 * T_(iz, j), q = 4.0 * T_(k, ix) - T_(k2, ix);
+                            c = p * p + q * q - 3 * 4 * (u * u) * (slown * slown);
+                            tref = 0.0; tdiv = 1.0;
+                        } else if (N_(k, ix) == 0) {
+                            u = dnx; v = dnz;
+                            a = 2;
+                            b = -2 * (T_(k, ix) + T_(iz, j));
+                            double w = u * slown;
+                            c = T_(k, ix) * T_(k, ix) + T_(iz, j) * T_(iz, j) - w * w;
+                            tref = 0.0; tdiv = 1.0;
+                        } else {
+                            a = 1.0; b = 0.0;
+                            double w = T_(iz, j) + slown * dnx;
+                            c = -(w * w);
+                            tref = 0.0; tdiv = 1.0;
+                        }
+                    } else {
+                        if (swk == 0) {
+                            swsol = 1;
+                            u = 2.0 * dnz;
+                            a = 1.0; b = 0.0;
+                            c = -(u * u) * (slown * slown);
+                            tref = 4.0 * T_(k, ix) - T_(k2, ix);
+                            tdiv = 3.0;
+                        } else if (N_(k, ix) == 0) {
+                            swsol = 1;
+                            a = 1.0; b = 0.0;
+                            double w = T_(k, ix) + slown * dnz;
+                            c = -(w * w);
+                            tref = 0.0; tdiv = 1.0;
+                        }
+                    }
+                    if (swsol == 1) {
+                        double rd1 = b * b - 4.0 * a * c;
+                        if (rd1 < 0) rd1 = 0;
+                        double tdsh = (-b + sqrt(rd1)) / (2.0 * a);
+                        double trav = (tref + tdsh) / tdiv;
+                        if (tsw1 == 1) travm = (travm < trav) ? travm : trav;
+                        else { travm = trav; tsw1 = 1; }
+                    }
+                }
+            }
+        }
+    }
+    /* ---- 45 deg stencil (:467-696) ---- */
+    int tsw2 = 0;
+    double travmd = 0;
+    eff = (double)pyround(pymod(45 - veln, 180));
+    slown = 1.0 / group_vel_cell(m, av, (int)iz, (int)ix, eff);
+    double mf2 = sqrt(2.0);
+    for (int jj_ = 0; jj_ < 2; jj_++) {
+        long j = (jj_ == 0) ? ix - 1 : ix + 1;
+        long k = (j == ix - 1) ? iz + 1 : iz - 1;
+        if (0 <= j && j <= nnx - 1 && 0 <= k && k <= nnz - 1) {
+            int swdiag = -1;
+            long j2 = 0, k2 = 0;
+            if (j == ix - 1) {
+                j2 = j - 1; k2 = k + 1;
+                if (j2 >= 0 && k2 <= nnz - 1 && N_(k2, j2) == 0) swdiag = 0;
+            } else {
+                j2 = j + 1; k2 = k - 1;
+                if (j2 <= nnx - 1 && k2 >= 0 && N_(k2, j2) == 0) swdiag = 0;
+            }
+            if (N_(k, j) == 0 && swdiag == 0) {
+                swdiag = -1;
+                if (T_(k, j) >= T_(k2, j2)) swdiag = 0;
+            } else {
+                swdiag = -1;
+            }
+            for (int q_ = 0; q_ < 2; q_++) {
+                long jj = (q_ == 0) ? ix - 1 : ix + 1;
+                long kk = (jj == ix - 1) ? iz - 1 : iz + 1;
+                if (0 <= jj && jj <= nnx - 1 && 0 <= kk && kk <= nnz - 1) {
+                    int swskew = -1;
+                    long jj2, kk2;
+                    if (jj == ix - 1) {
+                        jj2 = jj - 1; kk2 = kk - 1;
+                        if (jj2 >= 0 && kk2 >= 0 && N_(kk2, jj2) == 0) swskew = 0;
+                    } else {
+                        jj2 = jj + 1; kk2 = kk + 1;
+                        if (jj2 <= nnx - 1 && kk2 <= nnz - 1 && N_(kk2, jj2) == 0) swskew = 0;
+                    }
+                    if (N_(kk, jj) == 0 && swskew == 0) {
+                        swskew = -1;
+                        if (T_(kk, jj) >= T_(kk2, jj2)) swskew = 0;
+                    } else {
+                        swskew = -1;
+                    }
+                    int swsol = 0;
+                    double a = 0, b = 0, c = 0, tref = 0, tdiv = 1, u, v;
+                    (void)v;
+                    if (swdiag == 0) {
+                        swsol = 1;
+                        if (swskew == 0) {
+                            u = 2.0 * mf2 * dnx;
+                            a = 18.0;
+                            b = -6.0 * (4.0 * T_(k, j) - T_(k2, j2) + 4.0 * T_(kk, jj) - T_(kk2, jj2));
+                            double p = 4.0 * T_(k, j) - T_(k2, j2), q = 4.0 * T_(kk, jj) - T_(kk2, jj2);
+                            c = p * p + q * q - 4 * (u * u) * (slown * slown);
+                            tref = 0; tdiv = 1.0;
+                        } else if (N_(kk, jj) == 0) {
+                            u = mf2 * dnz; v = 2.0 * mf2 * dnx;
+                            a = 18;
+                            b = -6.0 * (3.0 * T_(kk, jj) + 4.0 * T_(k, j) - T_(k2, j2));
+                            double p = 3.0 * T_(kk, jj), q = 4.0 * T_(k, j) - T_(k2, j2);
+                            c = p * p + q * q - 4 * (v * v) * (slown * slown);
+                            tref = 0.0; tdiv = 1.0;
+                        } else {
+                            u = mf2 * 2.0 * dnx;
+                            a = 1.0; b = 0.0;
+                            double w = u * slown;
+                            c = -1.0 * (w * w);
+                            tref = 4.0 * T_(k, j) - T_(k2, j2);
+                            tdiv = 3.0;
+                        }
+                    } else if (N_(k, j) == 0) {
+                        swsol = 1;
+                        if (swskew == 0) {
+                            u = mf2 * dnx; v = mf2 * 2.0 * dnz;
+                            double em = 3.0 * T_(k, j) + 4.0 * T_(kk, jj) - T_(kk2, jj2);
+                            a = 18; b = -6.0 * em;
+                            double p = 3.0 * T_(k, j), q = 4.0 * T_(kk, jj) - T_(kk2, jj2);
+                            c = p * p + q * q - 3 * 4 * (u * u) * (slown * slown);
+                            tref = 0.0; tdiv = 1.0;
+                        } else if (N_(kk, jj) == 0) {
+                            u = mf2 * dnx; v = mf2 * dnz;
+                            a = 2;
+                            b = -2 * (T_(kk, jj) + T_(k, j));
+                            double w = u * slown;
+                            c = T_(kk, jj) * T_(kk, jj) + T_(k, j) * T_(k, j) - 4.0 / 9.0 * (w * w);
+                            tref = 0.0; tdiv = 1.0;
+                        } else {
+                            u = mf2 * dnx;
+                            a = 1.0; b = 0.0;
+                            double w = T_(k, j) + slown * u;
+                            c = -(w * w);
+                            tref = 0; tdiv = 1.0;
+                        }
+                    } else {
+                        if (swskew == 0) {
+                            swsol = 1;
+                            u = 2.0 * mf2 * dnz;
+                            a = 1.0; b = 0.0;
+                            c = -(u * u) * (slown * slown);
+                            tref = 4.0 * T_(kk, jj) - T_(kk2, jj2);
+                            tdiv = 3.0;
+                        } else if (N_(kk, jj) == 0) {
+                            swsol = 1;
+                            u = mf2 * dnx;
+                            a = 1.0; b = 0.0;
+                            c = -(slown * slown) * (u * u);
+                            tref = T_(kk, jj);
+                            tdiv = 1.0;
+                        }
+                    }
+                    if (swsol == 1) {
+                        double rd1 = b * b - 4.0 * a * c;
+                        if (rd1 > 0) {
+                            double tdsh = (-b + sqrt(rd1)) / (2.0 * a);
+                            double trav = (tref + tdsh) / tdiv;
+                            if (tsw2 == 1) travmd = (travmd < trav) ? travmd : trav;
+                            else { travmd = trav; tsw2 = 1; }
+                        }
+                    }
+                }
+            }
+        }
+    }
+    if (travmd != 0) travmd = (travm < travmd) ? travm : travmd;
+    else travmd = travm;
+
+    /* ---- atan(1/2) stencils (:698-897) ---- */
+    const double wave_ang = 27.0; /* round(degrees(atan(0.5))) */
+    double travmt = 0, travms = 0;
+    for (int pass = 0; pass < 2; pass++) {
+        double e = (pass == 0) ? pymod(-wave_ang - veln, 180) : pymod(wave_ang - veln, 180);
+        slown = 1.0 / group_vel_cell(m, av, (int)iz, (int)ix, e);
+        double m5 = sqrt(5.0);
+        long jv0[5] = {ix - 1, ix + 2, ix + 1, ix - 2, ix - 1};
+        long kv0[5] = {iz - 2, iz - 1, iz + 2, iz + 1, iz - 2};
+        long jv1[5] = {ix + 1, ix + 2, ix - 1, ix - 2, ix + 1};
+        long kv1[5] = {iz - 2, iz + 1, iz + 2, iz - 1, iz - 2};
+        const long *jv = pass == 0 ? jv0 : jv1;
+        const long *kv = pass == 0 ? kv0 : kv1;
+        int tsw = 0;
+        double tm = 0;
+        for (int lp = 0; lp < 4; lp++) {
+            long j = jv[lp], k = kv[lp], jj = jv[lp + 1], kk = kv[lp + 1];
+            if (0 <= j && j <= nnx - 1 && 0 <= k && k <= nnz - 1 && 0 <= jj && jj <= nnx - 1 && 0 <= kk &&
+                kk <= nnz - 1) {
+                int swsol = 0;
+                double a = 0, b = 0, c = 0, tref = 0, u;
+                if (N_(k, j) == 0) {
+                    swsol = 1;
+                    if (N_(kk, jj) == 0) {
+                        u = m5 * dnx;
+                        a = 2;
+                        b = -2 * (T_(kk, jj) + T_(k, j));
+                        double w = u * slown;
+                        c = T_(kk, jj) * T_(kk, jj) + T_(k, j) * T_(k, j) - 2 * (w * w);
+                        tref = 0.0;
+                    } else {
+                        u = m5 * dnx;
+                        a = 1; b = 0;
+                        double w = slown * u;
+                        c = -(w * w);
+                        tref = T_(k, j);
+                    }
+                } else if (N_(kk, jj) == 0) {
+                    swsol = 1;
+                    u = m5 * dnx;
+                    a = 1; b = 0;
+                    double w = slown * u;
+                    c = -(w * w);
+                    tref = T_(kk, jj);
+                }
+                if (swsol == 1) {
+                    double rd1 = b * b - 4 * a * c;
+                    if (rd1 < 0) rd1 = 0;
+                    double tdsh = (-b + sqrt(rd1)) / (2.0 * a);
+                    double trav = tref + tdsh;
+                    if (tsw == 1) tm = (trav < tm) ? trav : tm;
+                    else { tm = trav; tsw = 1; }
+                }
+            }
+        }
+        if (pass == 0) {
+            travmt = tm;
+            if (travmt != 0) travmt = (travmt < travmd) ? travmt : travmd;
+            else travmt = travmd;
+        } else {
+            travms = tm;
+            if (travms != 0) travms = (travmt < travms) ? travmt : travms;
+            else travms = travmt;
+        }
+    }
+    double cur = f->ttn[iz * f->nnx + ix];
+    if (cur != 0) travms = (travms < cur) ? travms : cur;
+    return travms;
+#undef N_
+#undef T_
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* wavefront_angle_dist :1413-1460 */
+static void wad(long ix, long iz, long x1, long x2, long x3, long z1, long z2, long z3, double y1, double y2,
+                double y3, double *angle, double *dist) {
+    double a;
+    if (y3 != y1) {
+        a = (y2 - y1) / (y3 - y1);
+    } else {
+        *angle = 0.0;
+        *dist = -1.0;
+        return;
+    }
+    double xpos = (1 - a) * (double)x1 + a * (double)x3;
+    double zpos = (1 - a) * (double)z1 + a * (double)z3;
+    double dx = (double)x2 - xpos;
+    double dz = (double)z2 - zpos;
+    if (dx == 0) *angle = 0.0;
+    else *angle = pymod(atan(dz / dx) * RAD2DEG + 90, 180);
+    *dist = fabs(dz * (double)(x2 - ix) - dx * (double)(z2 - iz)) / sqrt(dx * dx + dz * dz);
+}
+
+/* update :904-1410 — the ALI local solve.  nnz/nnx are the reference's ARGUMENTS (stage-1
+ * quirk passes nnz=nnx1); reads beyond the actual rows follow the padded semantics.        */
+double oref_update_f(const fstate_t *f, const mat_t *m, const table_t *ph, long iz, long ix, double dnx, long nnz,
+                     long nnx) {
+#define N_(z, x) ST(f, (z), (x))
+#define T_(z, x) TT(f, (z), (x))
+    int sp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (ix > 1) { if (N_(iz, ix - 2) >= 0) sp[3]++; }
+    if (ix > 0) {
+        if (N_(iz, ix - 1) >= 0) { sp[4]++; sp[7]++; }
+        if (iz > 0) { if (N_(iz - 1, ix - 1) >= 0) { sp[0]++; sp[3]++; sp[4]++; } }
+        if (iz < nnz - 1) { if (N_(iz + 1, ix - 1) >= 0) { sp[2]++; sp[3]++; sp[7]++; } }
+    }
+    if (ix < nnx - 2) { if (N_(iz, ix + 2) >= 0) sp[1]++; }
+    if (ix < nnx - 1) {
+        if (N_(iz, ix + 1) >= 0) { sp[5]++; sp[6]++; }
+        if (iz > 0) { if (N_(iz - 1, ix + 1) >= 0) { sp[0]++; sp[1]++; sp[5]++; } }
+        if (iz < nnz - 1) { if (N_(iz + 1, ix + 1) >= 0) { sp[1]++; sp[2]++; sp[6]++; } }
+    }
+    if (iz > 1) { if (N_(iz - 2, ix) >= 0) sp[0]++; }
+    if (iz > 0) { if (N_(iz - 1, ix) >= 0) { sp[4]++; sp[5]++; } }
+    if (iz < nnz - 2) { if (N_(iz + 2, ix) >= 0) sp[2]++; }
+    if (iz < nnz - 1) { if (N_(iz + 1, ix) >= 0) { sp[6]++; sp[7]++; } }
+
+    int sno = -1;
+    double min_diff = 1000000.0, diff;
+    if (sp[0] == 3) { diff = fabs(T_(iz - 1, ix - 1) - T_(iz - 1, ix + 1)); if (diff < min_diff) { sno = 0; min_diff = diff; } }
+    if (sp[1] == 3) { diff = fabs(T_(iz - 1, ix + 1) - T_(iz + 1, ix + 1)); if (diff < min_diff) { sno = 1; min_diff = diff; } }
+    if (sp[2] == 3) { diff = fabs(T_(iz + 1, ix - 1) - T_(iz + 1, ix + 1)); if (diff < min_diff) { sno = 2; min_diff = diff; } }
+    if (sp[3] == 3) { diff = fabs(T_(iz - 1, ix - 1) - T_(iz + 1, ix - 1)); if (diff < min_diff) { sno = 3; min_diff = diff; } }
+    if (sp[4] == 3) { diff = fabs(T_(iz, ix - 1) - T_(iz - 1, ix)); if (diff < min_diff) { sno = 4; min_diff = diff; } }
+    if (sp[5] == 3) { diff = fabs(T_(iz - 1, ix) - T_(iz, ix + 1)); if (diff < min_diff) { sno = 5; min_diff = diff; } }
+    if (sp[6] == 3) { diff = fabs(T_(iz + 1, ix) - T_(iz, ix + 1)); if (diff < min_diff) { sno = 6; min_diff = diff; } }
+    if (sp[7] == 3) { diff = fabs(T_(iz, ix - 1) - T_(iz + 1, ix)); if (diff < min_diff) { sno = 7; min_diff = diff; } }
+
+    double angle = 0.0, dist = -1.0, wt = 0.0;
+    if (sno != -1) {
+        /* square stencils :1039-1143 (both nsts sub-branches of stencils 0-3 are identical) */
+        switch (sno) {
+        case 0:
+            if (T_(iz - 1, ix - 1) < T_(iz - 1, ix + 1)) {
+                wad(ix, iz, ix, ix - 1, ix + 1, iz - 2, iz - 1, iz - 1, T_(iz - 2, ix), T_(iz - 1, ix - 1), T_(iz - 1, ix + 1), &angle, &dist);
+                wt = T_(iz - 1, ix - 1);
+            } else {
+                wad(ix, iz, ix, ix + 1, ix - 1, iz - 2, iz - 1, iz - 1, T_(iz - 2, ix), T_(iz - 1, ix + 1), T_(iz - 1, ix - 1), &angle, &dist);
+                wt = T_(iz - 1, ix + 1);
+            }
+            break;
+        case 1:
+            if (T_(iz - 1, ix + 1) < T_(iz + 1, ix + 1)) {
+                wad(ix, iz, ix + 2, ix + 1, ix + 1, iz, iz - 1, iz + 1, T_(iz, ix + 2), T_(iz - 1, ix + 1), T_(iz + 1, ix + 1), &angle, &dist);
+                wt = T_(iz - 1, ix + 1);
+            } else {
+                wad(ix, iz, ix + 2, ix + 1, ix + 1, iz, iz + 1, iz - 1, T_(iz, ix + 2), T_(iz + 1, ix + 1), T_(iz - 1, ix + 1), &angle, &dist);
+                wt = T_(iz + 1, ix + 1);
+            }
+            break;
+        case 2:
+            if (T_(iz + 1, ix - 1) < T_(iz + 1, ix + 1)) {
+                wad(ix, iz, ix, ix - 1, ix + 1, iz + 2, iz + 1, iz + 1, T_(iz + 2, ix), T_(iz + 1, ix - 1), T_(iz + 1, ix + 1), &angle, &dist);
+                wt = T_(iz + 1, ix - 1);
+            } else {
+                wad(ix, iz, ix, ix + 1, ix - 1, iz + 2, iz + 1, iz + 1, T_(iz + 2, ix), T_(iz + 1, ix + 1), T_(iz + 1, ix - 1), &angle, &dist);
+                wt = T_(iz + 1, ix + 1);
+            }
+            break;
+        case 3:
+            if (T_(iz - 1, ix - 1) < T_(iz + 1, ix - 1)) {
+                wad(ix, iz, ix - 2, ix - 1, ix - 1, iz, iz - 1, iz + 1, T_(iz, ix - 2), T_(iz - 1, ix - 1), T_(iz + 1, ix - 1), &angle, &dist);
+                wt = T_(iz - 1, ix - 1);
+            } else {
+                wad(ix, iz, ix - 2, ix - 1, ix - 1, iz, iz + 1, iz - 1, T_(iz, ix - 2), T_(iz + 1, ix - 1), T_(iz - 1, ix - 1), &angle, &dist);
+                wt = T_(iz + 1, ix - 1);
+            }
+            break;
+        case 4:
+            if (T_(iz, ix - 1) < T_(iz - 1, ix)) {
+                wad(ix, iz, ix - 1, ix - 1, ix, iz - 1, iz, iz - 1, T_(iz - 1, ix - 1), T_(iz, ix - 1), T_(iz - 1, ix), &angle, &dist);
+                wt = T_(iz, ix - 1);
+            } else {
+                wad(ix, iz, ix - 1, ix, ix - 1, iz - 1, iz - 1, iz, T_(iz - 1, ix - 1), T_(iz - 1, ix), T_(iz, ix - 1), &angle, &dist);
+                wt = T_(iz - 1, ix);
+            }
+            break;
+        case 5:
+            if (T_(iz - 1, ix) < T_(iz, ix + 1)) {
+                wad(ix, iz, ix + 1, ix, ix + 1, iz - 1, iz - 1, iz, T_(iz - 1, ix + 1), T_(iz - 1, ix), T_(iz, ix + 1), &angle, &dist);
+                wt = T_(iz - 1, ix);
+            } else {
+                wad(ix, iz, ix + 1, ix + 1, ix, iz - 1, iz, iz - 1, T_(iz - 1, ix + 1), T_(iz, ix + 1), T_(iz - 1, ix), &angle, &dist);
+                wt = T_(iz, ix + 1);
+            }
+            break;
+        case 6:
+            if (T_(iz + 1, ix) < T_(iz, ix + 1)) {
+                wad(ix, iz, ix + 1, ix, ix + 1, iz + 1, iz + 1, iz, T_(iz + 1, ix + 1), T_(iz + 1, ix), T_(iz, ix + 1), &angle, &dist);
+                wt = T_(iz + 1, ix);
+            } else {
+                wad(ix, iz, ix + 1, ix + 1, ix, iz + 1, iz, iz + 1, T_(iz + 1, ix + 1), T_(iz, ix + 1), T_(iz + 1, ix), &angle, &dist);
+                wt = T_(iz, ix + 1);
+            }
+            break;
+        case 7:
+            if (T_(iz, ix - 1) < T_(iz + 1, ix)) {
+                wad(ix, iz, ix - 1, ix - 1, ix, iz + 1, iz, iz + 1, T_(iz + 1, ix - 1), T_(iz, ix - 1), T_(iz + 1, ix), &angle, &dist);
+                wt = T_(iz, ix - 1);
+            } else {
+                wad(ix, iz, ix - 1, ix, ix - 1, iz + 1, iz + 1, iz, T_(iz + 1, ix - 1), T_(iz + 1, ix), T_(iz, ix - 1), &angle, &dist);
+                wt = T_(iz + 1, ix);
+            }
+            break;
+        }
+    }
+
+    if (sno == -1 || ix == 0 || ix == nnx - 1 || iz == 0 || iz == nnz - 1) {
+        /* triangular stencils :1146-1366 */
+        int tp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (ix > 1) { if (N_(iz, ix - 2) >= 0) { tp[4]++; tp[7]++; } }
+        if (ix > 0) {
+            if (N_(iz, ix - 1) >= 0) { tp[4]++; tp[7]++; }
+            if (iz > 0) { if (N_(iz - 1, ix - 1) >= 0) { tp[2]++; tp[7]++; } }
+            if (iz < nnz - 1) { if (N_(iz + 1, ix - 1) >= 0) { tp[3]++; tp[4]++; } }
+        }
+        if (ix < nnx - 2) { if (N_(iz, ix + 2) >= 0) { tp[5]++; tp[6]++; } }
+        if (ix < nnx - 1) {
+            if (N_(iz, ix + 1) >= 0) { tp[5]++; tp[6]++; }
+            if (iz > 0) { if (N_(iz - 1, ix + 1) >= 0) { tp[1]++; tp[6]++; } }
+            if (iz < nnz - 1) { if (N_(iz + 1, ix + 1) >= 0) { tp[0]++; tp[5]++; } }
+        }
+        if (iz > 1) { if (N_(iz - 2, ix) >= 0) { tp[1]++; tp[2]++; } }
+        if (iz > 0) { if (N_(iz - 1, ix) >= 0) { tp[1]++; tp[2]++; } }
+        if (iz < nnz - 2) { if (N_(iz + 2, ix) >= 0) { tp[0]++; tp[3]++; } }
+        if (iz < nnz - 1) { if (N_(iz + 1, ix) >= 0) { tp[0]++; tp[3]++; } }
+
+        if (sno == -1) min_diff = 1000000.0;
+        sno = -2;
+        const double s2m1 = sqrt(2.0) - 1, tms2 = 2 - sqrt(2.0);
+#define TRI(id, ca, cb, cc)                                                                   \
+    if (tp[id] == 3) {                                                                        \
+        double A_ = (ca), B_ = (cb), C_ = (cc);                                               \
+        if (A_ < ((B_ < C_) ? B_ : C_)) {                                                     \
+            diff = fabs(s2m1 * A_ + tms2 * B_ - C_);                                          \
+            if (diff < min_diff) { sno = id; min_diff = diff; }                               \
+        }                                                                                     \
+    }
+        TRI(0, T_(iz + 2, ix), T_(iz + 1, ix), T_(iz + 1, ix + 1))
+        TRI(1, T_(iz - 2, ix), T_(iz - 1, ix), T_(iz - 1, ix + 1))
+        TRI(2, T_(iz - 2, ix), T_(iz - 1, ix), T_(iz - 1, ix - 1))
+        TRI(3, T_(iz + 2, ix), T_(iz + 1, ix), T_(iz + 1, ix - 1))
+        TRI(4, T_(iz, ix - 2), T_(iz, ix - 1), T_(iz + 1, ix - 1))
+        TRI(5, T_(iz, ix + 2), T_(iz, ix + 1), T_(iz + 1, ix + 1))
+        TRI(6, T_(iz, ix + 2), T_(iz, ix + 1), T_(iz - 1, ix + 1))
+        TRI(7, T_(iz, ix - 2), T_(iz, ix - 1), T_(iz - 1, ix - 1))
+#undef TRI
+        /* NOTE: the reference's min(b, c) for the guard: numba min(b,c) -> b if not (c < b) */
+        if (sno != -2) {
+            switch (sno) {
+            case 0:
+                if (T_(iz + 1, ix) < T_(iz + 1, ix + 1)) {
+                    if (ix == 0) { angle = 90.; dist = 1.; }
+                    else wad(ix, iz, ix, ix, ix + 1, iz + 2, iz + 1, iz + 1, T_(iz + 2, ix), T_(iz + 1, ix), T_(iz + 1, ix + 1), &angle, &dist);
+                } else {
+                    wad(ix, iz, ix, ix + 1, ix, iz + 2, iz + 1, iz + 1, T_(iz + 2, ix), T_(iz + 1, ix + 1), T_(iz + 1, ix), &angle, &dist);
+                }
+                wt = T_(iz + 1, ix + 1); /* SURVEY B-D15 */
+                break;
+            case 1:
+                if (T_(iz - 1, ix) < T_(iz - 1, ix + 1)) {
+                    if (ix == 0) { angle = 90.; dist = 1.; }
+                    else wad(ix, iz, ix, ix, ix + 1, iz - 2, iz - 1, iz - 1, T_(iz - 2, ix), T_(iz - 1, ix), T_(iz - 1, ix + 1), &angle, &dist);
+                    wt = T_(iz - 1, ix);
+                } else {
+                    wad(ix, iz, ix, ix + 1, ix, iz - 2, iz - 1, iz - 1, T_(iz - 2, ix), T_(iz - 1, ix + 1), T_(iz - 1, ix), &angle, &dist);
+                    wt = T_(iz - 1, ix + 1);
+                }
+                break;
+            case 2:
+                if (T_(iz - 1, ix) < T_(iz - 1, ix - 1)) {
+                    if (ix == nnx - 1) { angle = 90.; dist = 1.; }
+                    else wad(ix, iz, ix, ix, ix - 1, iz - 2, iz - 1, iz - 1, T_(iz - 2, ix), T_(iz - 1, ix), T_(iz - 1, ix - 1), &angle, &dist);
+                    wt = T_(iz - 1, ix);
+                } else {
+                    wad(ix, iz, ix, ix - 1, ix, iz - 2, iz - 1, iz - 1, T_(iz - 2, ix), T_(iz - 1, ix - 1), T_(iz - 1, ix), &angle, &dist);
+                    wt = T_(iz - 1, ix - 1);
+                }
+                break;
+            case 3:
+                if (T_(iz + 1, ix) < T_(iz + 1, ix - 1)) {
+                    if (ix == nnx - 1) { angle = 90.; dist = 1.; }
+                    else wad(ix, iz, ix, ix, ix - 1, iz + 2, iz + 1, iz + 1, T_(iz + 2, ix), T_(iz + 1, ix), T_(iz + 1, ix - 1), &angle, &dist);
+                    wt = T_(iz + 1, ix);
+                } else {
+                    wad(ix, iz, ix, ix - 1, ix, iz + 2, iz + 1, iz + 1, T_(iz + 2, ix), T_(iz + 1, ix - 1), T_(iz + 1, ix), &angle, &dist);
+                    wt = T_(iz + 1, ix - 1);
+                }
+                break;
+            case 4:
+                if (T_(iz, ix - 1) < T_(iz + 1, ix - 1)) {
+                    if (iz == 0) { angle = 0.; dist = 1.; }
+                    else wad(ix, iz, ix - 2, ix - 1, ix - 1, iz, iz, iz + 1, T_(iz, ix - 2), T_(iz, ix - 1), T_(iz + 1, ix - 1), &angle, &dist);
+                    wt = T_(iz, ix - 1);
+                } else {
+                    wad(ix, iz, ix - 2, ix - 1, ix - 1, iz, iz + 1, iz, T_(iz, ix - 2), T_(iz + 1, ix - 1), T_(iz, ix - 1), &angle, &dist);
+                    wt = T_(iz + 1, ix - 1);
+                }
+                break;
+            case 5:
+                if (T_(iz, ix + 1) < T_(iz + 1, ix + 1)) {
+                    if (iz == 0) { angle = 0.; dist = 1.; }
+                    else wad(ix, iz, ix + 2, ix + 1, ix + 1, iz, iz, iz + 1, T_(iz, ix + 2), T_(iz, ix + 1), T_(iz + 1, ix + 1), &angle, &dist);
+                    wt = T_(iz, ix + 1);
+                } else {
+                    wad(ix, iz, ix + 2, ix + 1, ix + 1, iz, iz + 1, iz, T_(iz, ix + 2), T_(iz + 1, ix + 1), T_(iz, ix + 1), &angle, &dist);
+                    wt = T_(iz + 1, ix + 1);
+                }
+                break;
+            case 6:
+                if (T_(iz, ix + 1) < T_(iz - 1, ix + 1)) {
+                    if (iz == nnz - 1) { angle = 0.; dist = 1.; }
+                    else wad(ix, iz, ix + 2, ix + 1, ix + 1, iz, iz, iz - 1, T_(iz, ix + 2), T_(iz, ix + 1), T_(iz - 1, ix + 1), &angle, &dist);
+                    wt = T_(iz, ix + 1);
+                } else {
+                    wad(ix, iz, ix + 2, ix + 1, ix + 1, iz, iz - 1, iz, T_(iz, ix + 2), T_(iz - 1, ix + 1), T_(iz, ix + 1), &angle, &dist);
+                    wt = T_(iz - 1, ix + 1);
+                }
+                break;
+            case 7:
+                if (T_(iz, ix - 1) < T_(iz - 1, ix - 1)) {
+                    if (iz == nnz - 1) { angle = 0.; dist = 1.; }
+                    else wad(ix, iz, ix - 2, ix - 1, ix - 1, iz, iz, iz - 1, T_(iz, ix - 2), T_(iz, ix - 1), T_(iz - 1, ix - 1), &angle, &dist);
+                    wt = T_(iz, ix - 1);
+                } else {
+                    wad(ix, iz, ix - 2, ix - 1, ix - 1, iz, iz - 1, iz, T_(iz, ix - 2), T_(iz - 1, ix - 1), T_(iz, ix - 1), &angle, &dist);
+                    wt = T_(iz - 1, ix - 1);
+                }
+                break;
+            }
+            sno += 8;
+        }
+    }
+    if (dist != -1.0) {
+        double effa = pymod(mat_veln(m, (int)iz, (int)ix) - angle, 180);
+        long p = mat_velpn(m, (int)iz, (int)ix);
+        const int64_t *s = mat_stif(m, (int)iz, (int)ix);
+        double vm = mat_velmap(m, (int)iz, (int)ix);
+        double velocity;
+        if (p != 0 || s == NULL) velocity = table_vel(ph, effa, p, vm);
+        else velocity = christoffel_phase(s, effa, vm);
+        return wt + (dist * dnx / velocity);
+    }
+    return -1.0;
+#undef N_
+#undef T_
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* One heap-FMM loop on a grid (main loop :2055-2102; stage loops :1621-1674, :1787-1844,
+ * :1937-1993, :2292-2346, :2460-2504).  stage != 0 enables the window-edge finish test;
+ * quirk_nnz != 0 passes nnz=nnx to update() for close x-neighbours (:1645).                 */
+typedef struct {
+    const table_t *av, *ph;
+    double dnx, dnz_fouds;
+    int stage, isx_s, isz_s, max_dist, quirk_nnz;
+} loopcfg_t;
+
+static void relax(fstate_t *f, const mat_t *m, const loopcfg_t *c, long iz, long ix, int is_xclose_quirk) {
+    long nnzu = is_xclose_quirk ? f->nnx : f->nnz;
+    double v = oref_update_f(f, m, c->ph, iz, ix, c->dnx, nnzu, f->nnx);
+    if (v == -1.0) v = oref_fouds18_f(f, m, c->av, iz, ix, c->dnx, c->dnz_fouds, f->nnx, f->nnz);
+    f->ttn[iz * f->nnx + ix] = v;
+}
+
+static int fmm_loop(fstate_t *f, const mat_t *m, const loopcfg_t *c) {
+    int finished = 0;
+    long nnx = f->nnx, nnz = f->nnz;
+    while (f->ntr > 0 && !finished) {
+        long ix = f->btg[3], iz = f->btg[2];
+        f->nsts[iz * nnx + ix] = 0;
+        downtree(f);
+        for (int s = 0; s < 2; s++) {
+            long i = s == 0 ? ix - 1 : ix + 1;
+            if (0 <= i && i <= nnx - 1) {
+                int32_t st = f->nsts[iz * nnx + i];
+                if (st == -1) {
+                    relax(f, m, c, iz, i, 0);
+                    if (addtree(f, iz, i)) return -1;
+                } else if (st > 0) {
+                    relax(f, m, c, iz, i, c->quirk_nnz);
+                    updtree(f, iz, i);
+                }
+            } else if (c->stage && labs(c->isx_s - i) == c->max_dist + 1) {
+                finished = 1;
+            }
+        }
+        for (int s = 0; s < 2; s++) {
+            long i = s == 0 ? iz - 1 : iz + 1;
+            if (0 <= i && i <= nnz - 1) {
+                int32_t st = f->nsts[i * nnx + ix];
+                if (st == -1) {
+                    relax(f, m, c, i, ix, 0);
+                    if (addtree(f, i, ix)) return -1;
+                } else if (st > 0) {
+                    relax(f, m, c, i, ix, 0);
+                    updtree(f, i, ix);
+                }
+            } else if (c->stage && labs(c->isz_s - i) == c->max_dist + 1) {
+                finished = 1;
+            }
+        }
+    }
+    return 0;
+}
+
+static int fstate_alloc(fstate_t *f, int nnz, int nnx, long maxbt, double *ttn_ext) {
+    f->nnz = nnz;
+    f->nnx = nnx;
+    size_t n = (size_t)nnz * nnx;
+    f->ttn = ttn_ext ? ttn_ext : (double *)calloc(n, sizeof(double));
+    f->nsts = (int32_t *)malloc(n * sizeof(int32_t));
+    if (maxbt < (long)n + 2) maxbt = (long)n + 2; /* never overflow (reference sizes are 0.25-0.5 n) */
+    f->maxbt = maxbt;
+    f->btg = (int32_t *)calloc((size_t)maxbt * 2, sizeof(int32_t));
+    f->ntr = 0;
+    if (!f->ttn || !f->nsts || !f->btg) return -1;
+    for (size_t i = 0; i < n; i++) f->nsts[i] = -1;
+    return 0;
+}
+static void fstate_free(fstate_t *f, int own_ttn) {
+    if (own_ttn) free(f->ttn);
+    free(f->nsts);
+    free(f->btg);
+}
+
+/* Hand-over from a finer stage grid (every 3rd node) to the next grid (:1719-1753,
+ * :1887-1921, :2006-2040, :2391-2425, :2725-2759). */
+static int handover(const fstate_t *s, long isz_s, long isx_s, fstate_t *d, long isz_d, long isx_d) {
+    for (long i = 0; i < s->nnz + 1; i += 3) {
+        for (long j = 0; j < s->nnx + 1; j += 3) {
+            long pz = isz_d + (i - isz_s) / 3;
+            long px = isx_d + (j - isx_s) / 3;
+            d->ttn[pz * d->nnx + px] = s->ttn[i * s->nnx + j];
+            int32_t st = s->nsts[i * s->nnx + j];
+            if (st == 0) {
+                d->nsts[pz * d->nnx + px] = 0;
+                int outer = 0;
+                if (i - 3 >= 0) { if (s->nsts[(i - 3) * s->nnx + j] == -1) outer = 1; } else outer = 1;
+                if (i + 3 <= s->nnz - 1) { if (s->nsts[(i + 3) * s->nnx + j] == -1) outer = 1; } else outer = 1;
+                if (j - 3 >= 0) { if (s->nsts[i * s->nnx + j - 3] == -1) outer = 1; } else outer = 1;
+                if (j + 3 <= s->nnx - 1) { if (s->nsts[i * s->nnx + j + 3] == -1) outer = 1; } else outer = 1;
+                if (outer) { if (addtree(d, pz, px)) return -1; }
+            }
+            if (st > 0) { if (addtree(d, pz, px)) return -1; }
+        }
+    }
+    return 0;
+}
+
+/* Build a refined window view of a parent view: rows [lo_z, hi_z], cols [lo_x, hi_x] of the
+ * parent, refined by 'scale' (finer_grid_n :26-56), quantised. */
+typedef struct { mat_t m; int32_t *zm, *xm; } view_t;
+static int make_view(view_t *v, const mat_t *parent, long lo_z, long hi_z, long lo_x, long hi_x, long scale) {
+    long side = (scale - 1) / 2;
+    long nz = scale * (hi_z - lo_z) + 1, nx = scale * (hi_x - lo_x) + 1;
+    v->zm = (int32_t *)malloc(nz * sizeof(int32_t));
+    v->xm = (int32_t *)malloc(nx * sizeof(int32_t));
+    if (!v->zm || !v->xm) return -1;
+    for (long a = 0; a < nz; a++) v->zm[a] = parent->zmap[lo_z + (a + side) / scale];
+    for (long b = 0; b < nx; b++) v->xm[b] = parent->xmap[lo_x + (b + side) / scale];
+    v->m = *parent;
+    v->m.nnz = (int)nz;
+    v->m.nnx = (int)nx;
+    v->m.zmap = v->zm;
+    v->m.xmap = v->xm;
+    v->m.quant = 1;
+    return 0;
+}
+static void free_view(view_t *v) { free(v->zm); free(v->xm); }
+
+/* Straight-ray travel times inside the source cell footprint (:1546-1590, :2223-2267).
+ * 'plus' selects the travel_finer_grid sign (veln + angle, SURVEY B-D5). */
+static void straight_rays(fstate_t *f, long isz1, long isx1, long side1, double dnx1, const mat_t *src_m, int sz,
+                          int sx, const table_t *av, int plus) {
+    double vsrc = mat_veln(src_m, sz, sx);
+    long p = mat_velpn(src_m, sz, sx);
+    const int64_t *s = mat_stif(src_m, sz, sx);
+    double vm = mat_velmap(src_m, sz, sx);
+    for (long i = -side1; i <= side1; i++) {
+        if (0 <= isz1 + i && isz1 + i <= f->nnz - 1) {
+            for (long j = -side1; j <= side1; j++) {
+                if (0 <= isx1 + j && isx1 + j <= f->nnx - 1) {
+                    double angle = (j == 0) ? 90.0 : atan((double)i / (double)j) * RAD2DEG;
+                    double eff = plus ? pymod(vsrc + angle, 180) : pymod(vsrc - angle, 180);
+                    double velocity;
+                    if (p != 0) velocity = table_vel(av, eff, p, vm);
+                    else velocity = christoffel_group(s, eff, vm);
+                    double length = dnx1 * sqrt((double)(i * i + j * j));
+                    f->ttn[(isz1 + i) * f->nnx + isx1 + j] = length / velocity;
+                    f->nsts[(isz1 + i) * f->nnx + isx1 + j] = 0;
+                }
+            }
+        }
+    }
+}
+
+static void add_edges(fstate_t *f, long isz1, long isx1, long side1) {
+    long nnz1 = f->nnz, nnx1 = f->nnx;
+    if (isz1 - side1 >= 0)
+        for (long i = imax(0, isx1 - side1); i <= imin(nnx1 - 1, isx1 + side1); i++) addtree(f, isz1 - side1, i);
+    if (isz1 + side1 <= nnz1 - 1)
+        for (long i = imax(0, isx1 - side1); i <= imin(nnx1 - 1, isx1 + side1); i++) addtree(f, isz1 + side1, i);
+    if (isx1 - side1 >= 0)
+        for (long i = imax(0, isz1 - side1); i <= imin(nnz1 - 1, isz1 + side1); i++) addtree(f, i, isx1 - side1);
+    if (isx1 + side1 <= nnx1 - 1)
+        for (long i = imax(0, isz1 - side1); i <= imin(nnz1 - 1, isz1 + side1); i++) addtree(f, i, isx1 + side1);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* travel :1463-2117 (subgrid 1).  ttn (nnz x nnx) must be zeroed by the caller; it is filled. */
+static int travel_impl(double scx, double scz, const mat_t *base, const table_t *av, const table_t *ph, double gox,
+                       double goz, double dnx, double dnz, double *ttn) {
+    long nnx = base->nnx, nnz = base->nnz;
+    long isx = pyround((scx - gox) / dnx);
+    long isz = pyround((scz - goz) / dnz);
+    if (isx < 0 || isx >= nnx || isz < 0 || isz >= nnz) return -2;
+    int rc = 0;
+
+    /* ---- stage 1: 5x5 coarse window x27 ---- */
+    long size1 = 2, sg1 = 27, side1 = (sg1 - 1) / 2;
+    long left = imax(0, isx - size1), right = imin(nnx - 1, isx + size1);
+    long bottom = imax(0, isz - size1), top = imin(nnz - 1, isz + size1);
+    view_t v1;
+    if (make_view(&v1, base, bottom, top, left, right, sg1)) return -1;
+    fstate_t f1;
+    if (fstate_alloc(&f1, v1.m.nnz, v1.m.nnx, 0, NULL)) return -1;
+    long isx_1 = sg1 * (isx - left), isz_1 = sg1 * (isz - bottom);
+    double dnx1 = dnx / sg1;
+    long max_dist1 = sg1 * size1;
+    straight_rays(&f1, isz_1, isx_1, side1, dnx1, base, (int)isz, (int)isx, av, 0);
+    add_edges(&f1, isz_1, isx_1, side1);
+    loopcfg_t c1 = {av, ph, dnx1, dnx1, 1, (int)isx_1, (int)isz_1, (int)max_dist1, 1};
+    if (fmm_loop(&f1, &v1.m, &c1)) rc = -1;
+
+    /* ---- stage 2: 13x13 coarse window x9 ---- */
+    long size2 = 6, sg2 = 9;
+    left = imax(0, isx - size2); right = imin(nnx - 1, isx + size2);
+    bottom = imax(0, isz - size2); top = imin(nnz - 1, isz + size2);
+    view_t v2;
+    if (make_view(&v2, base, bottom, top, left, right, sg2)) return -1;
+    fstate_t f2;
+    if (fstate_alloc(&f2, v2.m.nnz, v2.m.nnx, 0, NULL)) return -1;
+    long isx_2 = sg2 * (isx - left), isz_2 = sg2 * (isz - bottom);
+    double dnx2 = dnx / sg2;
+    if (!rc && handover(&f1, isz_1, isx_1, &f2, isz_2, isx_2)) rc = -1;
+    loopcfg_t c2 = {av, ph, dnx2, dnx2, 1, (int)isx_2, (int)isz_2, (int)(sg2 * size2), 0};
+    if (!rc && fmm_loop(&f2, &v2.m, &c2)) rc = -1;
+    fstate_free(&f1, 1);
+    free_view(&v1);
+
+    /* ---- stage 3: 27x27 coarse window x3 ---- */
+    long size3 = 13, sg3 = 3;
+    left = imax(0, isx - size3); right = imin(nnx - 1, isx + size3);
+    bottom = imax(0, isz - size3); top = imin(nnz - 1, isz + size3);
+    view_t v3;
+    if (make_view(&v3, base, bottom, top, left, right, sg3)) return -1;
+    fstate_t f3;
+    if (fstate_alloc(&f3, v3.m.nnz, v3.m.nnx, 0, NULL)) return -1;
+    long isx_3 = sg3 * (isx - left), isz_3 = sg3 * (isz - bottom);
+    double dnx3 = dnx / sg3;
+    if (!rc && handover(&f2, isz_2, isx_2, &f3, isz_3, isx_3)) rc = -1;
+    loopcfg_t c3 = {av, ph, dnx3, dnx3, 1, (int)isx_3, (int)isz_3, (int)(sg3 * size3), 0};
+    if (!rc && fmm_loop(&f3, &v3.m, &c3)) rc = -1;
+    fstate_free(&f2, 1);
+    free_view(&v2);
+
+    /* ---- main grid ---- */
+    fstate_t f;
+    if (fstate_alloc(&f, (int)nnz, (int)nnx, 0, ttn)) return -1;
+    if (!rc && handover(&f3, isz_3, isx_3, &f, isz, isx)) rc = -1;
+    fstate_free(&f3, 1);
+    free_view(&v3);
+    loopcfg_t c = {av, ph, dnx, dnz, 0, 0, 0, 0, 0};
+    if (!rc && fmm_loop(&f, base, &c)) rc = -1;
+    fstate_free(&f, 0);
+    return rc;
+}
+
+/* travel_finer_grid :2120-2832.  out: (sg*(nz0-1)+1) x (sg*(nx0-1)+1), already divided by sg. */
+static int travel_finer_impl(double scx, double scz, const mat_t *coarse, long sg, const table_t *av,
+                             const table_t *ph, double gox, double goz, double dnx, double dnz, double *out) {
+    view_t vf;
+    if (make_view(&vf, coarse, 0, coarse->nnz - 1, 0, coarse->nnx - 1, sg)) return -1;
+    int64_t *zero_stif = NULL;
+    if (coarse->stif == NULL) {
+        /* stif_den0 is None -> zeros (:2159-2160) */
+        zero_stif = (int64_t *)calloc((size_t)coarse->nnz * coarse->nnx * 5, sizeof(int64_t));
+        vf.m.stif = zero_stif;
+    }
+    const mat_t *fine = &vf.m;
+    long nnz = fine->nnz, nnx = fine->nnx;
+    long isx = sg * pyround((scx - gox) / dnx);
+    long isz = sg * pyround((scz - goz) / dnz);
+    if (isx < 0 || isx >= nnx || isz < 0 || isz >= nnz) { free_view(&vf); free(zero_stif); return -2; }
+    int rc = 0;
+
+    long size1 = 2 * sg + (sg - 1) / 2, s1 = 9;
+    long side1 = (s1 - 1) / 2 + s1 * ((sg - 1) / 2);
+    long left = imax(0, isx - size1), right = imin(nnx - 1, isx + size1);
+    long bottom = imax(0, isz - size1), top = imin(nnz - 1, isz + size1);
+    view_t v1;
+    if (make_view(&v1, fine, bottom, top, left, right, s1)) return -1;
+    fstate_t f1;
+    if (fstate_alloc(&f1, v1.m.nnz, v1.m.nnx, 0, NULL)) return -1;
+    long isx_1 = s1 * (isx - left), isz_1 = s1 * (isz - bottom);
+    double dnx1 = dnx / s1;
+    straight_rays(&f1, isz_1, isx_1, side1, dnx1, fine, (int)isz, (int)isx, av, 1);
+    add_edges(&f1, isz_1, isx_1, side1);
+    loopcfg_t c1 = {av, ph, dnx1, dnx1, 1, (int)isx_1, (int)isz_1, (int)(s1 * size1), 0};
+    if (fmm_loop(&f1, &v1.m, &c1)) rc = -1;
+
+    long size2 = size1 + 3 * sg, s2 = 3;
+    left = imax(0, isx - size2); right = imin(nnx - 1, isx + size2);
+    bottom = imax(0, isz - size2); top = imin(nnz - 1, isz + size2);
+    view_t v2;
+    if (make_view(&v2, fine, bottom, top, left, right, s2)) return -1;
+    fstate_t f2;
+    if (fstate_alloc(&f2, v2.m.nnz, v2.m.nnx, 0, NULL)) return -1;
+    long isx_2 = s2 * (isx - left), isz_2 = s2 * (isz - bottom);
+    double dnx2 = dnx / s2;
+    if (!rc && handover(&f1, isz_1, isx_1, &f2, isz_2, isx_2)) rc = -1;
+    loopcfg_t c2 = {av, ph, dnx2, dnx2, 1, (int)isx_2, (int)isz_2, (int)(s2 * size2), 0};
+    if (!rc && fmm_loop(&f2, &v2.m, &c2)) rc = -1;
+    fstate_free(&f1, 1);
+    free_view(&v1);
+
+    fstate_t f;
+    memset(out, 0, (size_t)nnz * nnx * sizeof(double));
+    if (fstate_alloc(&f, (int)nnz, (int)nnx, 0, out)) return -1;
+    if (!rc && handover(&f2, isz_2, isx_2, &f, isz, isx)) rc = -1;
+    fstate_free(&f2, 1);
+    free_view(&v2);
+    loopcfg_t c = {av, ph, dnx, dnz, 0, 0, 0, 0, 0};
+    if (!rc && fmm_loop(&f, fine, &c)) rc = -1;
+    fstate_free(&f, 0);
+    size_t n = (size_t)nnz * nnx;
+    for (size_t i = 0; i < n; i++) out[i] = out[i] / (double)sg;
+    free_view(&vf);
+    free(zero_stif);
+    return rc;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* time_between_points :2835-2989 — straight-segment DDA over coarse cells.                  */
+static double tbp_impl(double x1, double x2, double y1, double y2, double dnx, long sg, const table_t *vd,
+                       const mat_t *m) {
+    x1 = x1 / (double)sg; x2 = x2 / (double)sg; y1 = y1 / (double)sg; y2 = y2 / (double)sg;
+    double section_time = 0.0;
+    double start_x = x1, end_x = x2, start_y = y1, end_y = y2, prev_x = x1, prev_y = y1;
+    double angle = (x1 == x2) ? 0.0 : atan((y2 - y1) / (x2 - x1)) * RAD2DEG;
+    double mm = 0, cc = 0;
+    if (end_x != start_x) { mm = (end_y - start_y) / (end_x - start_x); cc = start_y - mm * start_x; }
+    int fin_x = 0, fin_y = 0;
+    int dir_x = (start_x < end_x) ? 1 : -1;
+    int dir_y = (start_y < end_y) ? 1 : -1;
+    double next_x = (double)pyround(start_x) + dir_x * 0.5;
+    double next_y = (double)pyround(start_y) + dir_y * 0.5;
+    while (!(fin_x && fin_y)) {
+        if (((next_x > end_x && dir_x == 1) || (next_x < end_x && dir_x == -1)) && !fin_x) { fin_x = 1; next_x = end_x; }
+        if (((next_y > end_y && dir_y == 1) || (next_y < end_y && dir_y == -1)) && !fin_y) { fin_y = 1; next_y = end_y; }
+        double nxv, nyv;
+        if (end_x == start_x) {
+            nxv = start_x; nyv = next_y; next_y += dir_y;
+        } else {
+            double next_x_yval = mm * next_x + cc;
+            if (mm != 0) {
+                double next_y_xval = (next_y - cc) / mm;
+                double d1x = start_x - next_x, d1y = start_y - next_x_yval;
+                double d2x = start_x - next_y_xval, d2y = start_y - next_y;
+                if (d1x * d1x + d1y * d1y < d2x * d2x + d2y * d2y) {
+                    nxv = next_x; nyv = next_x_yval; next_x += dir_x;
+                } else {
+                    nxv = next_y_xval; nyv = next_y; next_y += dir_y;
+                }
+            } else {
+                nxv = next_x; nyv = next_x_yval; next_x += dir_x;
+            }
+        }
+        long x_pos = pyround((prev_x + nxv) / 2);
+        long y_pos = pyround((prev_y + nyv) / 2);
+        /* numba wraps negative indices */
+        if (x_pos < 0) x_pos += m->nnx;
+        if (y_pos < 0) y_pos += m->nnz;
+        double eff = pymod(mat_veln(m, (int)y_pos, (int)x_pos) - angle, 180);
+        double ddx = prev_x - nxv, ddy = prev_y - nyv;
+        double distance = dnx * sqrt(ddx * ddx + ddy * ddy);
+        double velocity = group_vel_cell(m, vd, (int)y_pos, (int)x_pos, eff);
+        double slown = 1.0 / velocity;
+        section_time += distance * slown;
+        prev_x = nxv; prev_y = nyv;
+    }
+    return section_time;
+}
+
+/* find_ray :3104-3465.  Returns number of points (>=2) or <0 on error. */
+static long find_ray_impl(double dnx, const table_t *vd, double srcx, double srcy, double recx, double recy,
+                          const double *ttf, long fnz, long fnx, const mat_t *m, long sg, double *rx, double *ry,
+                          long max_pts, double *time_out, int *early) {
+    long plane_dist = 3;
+    long sd = plane_dist * sg + 1;
+    long sd2 = (plane_dist - 1) * sg + 1;
+    long cap = 5 * (long)(m->nnz + m->nnx);
+    if (cap > max_pts) cap = max_pts;
+    rx[0] = srcx; ry[0] = srcy;
+    double last_x = srcx, last_y = srcy;
+    long ray_len = 1;
+    double lvx = recx - srcx, lvy = recy - srcy;
+    long nnx = fnz; /* reference naming: nnx = rec_TTF.shape[0] (rows) */
+    long nnz = fnx; /*                   nnz = rec_TTF.shape[1] (cols) */
+    double *TT = (double *)malloc(sizeof(double) * (size_t)(2 * sd + 8 + 2 * sd2 + 8));
+    *early = 0;
+#define RT(r, c) ttf[(long)(r) * fnx + (long)(c)]
+    while ((last_x - recx) * (last_x - recx) + (last_y - recy) * (last_y - recy) > (1.6 * sg) * (1.6 * sg)) {
+        if ((last_x - recx) * (last_x - recx) + (last_y - recy) * (last_y - recy) < (double)(4 * sg) * (4 * sg)) {
+            lvx = recx - last_x;
+            lvy = recy - last_y;
+        }
+        if (ray_len + 1 >= cap) { free(TT); return -3; }
+        double cand[4] = {fabs(lvx), fabs(lvx + lvy) / sqrt(2.0), fabs(lvy), fabs(lvx - lvy) / sqrt(2.0)};
+        int dir = 0;
+        for (int q = 1; q < 4; q++) if (cand[q] > cand[dir]) dir = q;
+        long n = 0, base0 = 0, c_value;
+        long rlx = pyround(last_x), rly = pyround(last_y);
+        if (dir == 0) {
+            c_value = rlx;
+            if (lvx > 0) c_value += sg; else c_value -= sg;
+            if (c_value < 0 || c_value >= nnz) break;
+            long min_val = imax(0, rly - sd), max_val = imin(nnx - 1, rly + sd);
+            n = max_val - min_val + 1; base0 = min_val;
+            for (long i = 0; i < n; i++) {
+                long xv = i + min_val;
+                TT[i] = RT(xv, c_value) + tbp_impl(last_x, (double)c_value, last_y, (double)xv, dnx, sg, vd, m);
+            }
+        } else if (dir == 1) {
+            c_value = rlx + rly;
+            long min_x, max_x;
+            if (lvx > 0) {
+                c_value += sg;
+                min_x = imax(imax(0, c_value - (nnx - 1)), rlx - sd2);
+                max_x = imin(imin(nnz - 1, c_value), c_value - rly + sd2);
+            } else {
+                c_value -= sg;
+                min_x = imax(imax(0, c_value - (nnx - 1)), c_value - rly - sd2);
+                max_x = imin(imin(nnz - 1, c_value), rlx + sd2);
+            }
+            n = max_x - min_x + 1; base0 = min_x;
+            for (long i = 0; i < n; i++) {
+                long xc = min_x + i, yc = -xc + c_value;
+                TT[i] = RT(yc, xc) + tbp_impl(last_x, (double)xc, last_y, (double)yc, dnx, sg, vd, m);
+            }
+        } else if (dir == 2) {
+            c_value = rly;
+            if (lvy > 0) c_value += sg; else c_value -= sg;
+            if (c_value < 0 || c_value >= nnx) break;
+            long min_val = imax(0, rlx - sd), max_val = imin(nnz - 1, rlx + sd);
+            n = max_val - min_val + 1; base0 = min_val;
+            for (long i = 0; i < n; i++) {
+                long yv = i + min_val;
+                TT[i] = RT(c_value, yv) + tbp_impl(last_x, (double)yv, last_y, (double)c_value, dnx, sg, vd, m);
+            }
+        } else {
+            c_value = rly - rlx;
+            long min_x, max_x;
+            if (lvx < 0) {
+                c_value += sg;
+                min_x = imax(imax(0, -c_value), rly - c_value - sd2);
+                max_x = imin(imin(nnz - 1, (nnx - 1) - c_value), rlx + sd2);
+            } else {
+                c_value -= sg;
+                min_x = imax(imax(0, -c_value), rlx - sd2);
+                max_x = imin(imin(nnz - 1, (nnx - 1) - c_value), rly - c_value + sd2);
+            }
+            n = max_x - min_x + 1; base0 = min_x;
+            for (long i = 0; i < n; i++) {
+                long xc = min_x + i, yc = xc + c_value;
+                TT[i] = RT(yc, xc) + tbp_impl(last_x, (double)xc, last_y, (double)yc, dnx, sg, vd, m);
+            }
+        }
+        if (n <= 0) { free(TT); return -4; } /* SURVEY B-D11: empty candidate set */
+        double minimum, min_i;
+        if (TT[0] < TT[n - 1]) { minimum = TT[0]; min_i = 0; }
+        else { minimum = TT[n - 1]; min_i = (double)(n - 1); }
+        for (long j = 1; j < n - 1; j++) {
+            double t1 = TT[j - 1], t2 = TT[j], t3 = TT[j + 1];
+            if (t1 >= t2 && t2 <= t3) {
+                double a = (t1 + t3 - 2 * t2) / 2;
+                double b = (t3 - t1) / 2;
+                double c = t2;
+                double pos, lmv;
+                if (a != 0) {
+                    pos = -b / (2 * a);
+                    lmv = a * (pos * pos) + b * pos + c;
+                    pos += (double)j;
+                } else {
+                    pos = (double)j;
+                    lmv = t2;
+                }
+                if (lmv < minimum) { min_i = pos; minimum = lmv; }
+            }
+        }
+        if (dir == 0) { rx[ray_len] = (double)c_value; ry[ray_len] = min_i + (double)base0; }
+        else if (dir == 1) { rx[ray_len] = (double)base0 + min_i; ry[ray_len] = (double)c_value - rx[ray_len]; }
+        else if (dir == 2) { rx[ray_len] = min_i + (double)base0; ry[ray_len] = (double)c_value; }
+        else { rx[ray_len] = (double)base0 + min_i; ry[ray_len] = rx[ray_len] + (double)c_value; }
+        if (RT(pyround(last_y), pyround(last_x)) < RT(pyround(ry[ray_len]), pyround(rx[ray_len]))) {
+            *early = 1; /* "Travel time to receiver increasing: Finishing ray early" (:3406-3407) */
+            break;
+        }
+        lvx = rx[ray_len] - last_x;
+        last_x = rx[ray_len];
+        lvy = ry[ray_len] - last_y;
+        last_y = ry[ray_len];
+        ray_len += 1;
+    }
+#undef RT
+    free(TT);
+    rx[ray_len] = recx;
+    ry[ray_len] = recy;
+    long npts = ray_len + 1;
+    double tt = 0.0;
+    for (long i = 0; i < npts - 1; i++) tt += tbp_impl(rx[i], rx[i + 1], ry[i], ry[i + 1], dnx, sg, vd, m);
+    *time_out = tt;
+    return npts;
+}
+
+/* ========================================================================================== */
+/* C-ABI of the oracle (ctypes, tests only).                                                  */
+typedef struct {
+    mat_t m;
+    int32_t *zm, *xm;
+} base_t;
+
+static int make_base(base_t *b, int nnz, int nnx, const double *veln, const int64_t *velpn, const double *vel_map,
+                     const int64_t *stif) {
+    b->zm = (int32_t *)malloc(sizeof(int32_t) * nnz);
+    b->xm = (int32_t *)malloc(sizeof(int32_t) * nnx);
+    if (!b->zm || !b->xm) return -1;
+    for (int i = 0; i < nnz; i++) b->zm[i] = i;
+    for (int i = 0; i < nnx; i++) b->xm[i] = i;
+    b->m.nnz = nnz; b->m.nnx = nnx; b->m.zmap = b->zm; b->m.xmap = b->xm; b->m.nx0 = nnx;
+    b->m.veln = veln; b->m.velpn = velpn; b->m.vel_map = vel_map; b->m.stif = stif; b->m.quant = 0;
+    return 0;
+}
+static void free_base(base_t *b) { free(b->zm); free(b->xm); }
+
+int oref_travel(double scx, double scz, int nnz, int nnx, const double *veln, const int64_t *velpn,
+                const double *vel_map, const int64_t *stif, const double *av, const double *ph, int ncol, double gox,
+                double goz, double dnx, double dnz, double *ttn) {
+    base_t b;
+    if (make_base(&b, nnz, nnx, veln, velpn, vel_map, stif)) return -1;
+    table_t tav = {av, ncol}, tph = {ph, ncol};
+    memset(ttn, 0, sizeof(double) * (size_t)nnz * nnx);
+    int rc = travel_impl(scx, scz, &b.m, &tav, &tph, gox, goz, dnx, dnz, ttn);
+    free_base(&b);
+    return rc;
+}
+
+int oref_travel_finer_grid(double scx, double scz, int nnz, int nnx, const double *veln, const int64_t *velpn,
+                           const double *vel_map, const int64_t *stif, int sg, const double *av, const double *ph,
+                           int ncol, double gox, double goz, double dnx, double dnz, double *out) {
+    base_t b;
+    if (make_base(&b, nnz, nnx, veln, velpn, vel_map, stif)) return -1;
+    table_t tav = {av, ncol}, tph = {ph, ncol};
+    int rc = travel_finer_impl(scx, scz, &b.m, sg, &tav, &tph, gox, goz, dnx, dnz, out);
+    free_base(&b);
+    return rc;
+}
+
+double oref_time_between_points(double x1, double x2, double y1, double y2, double dnx, int sg, const double *vd,
+                                int ncol, int nnz, int nnx, const double *veln, const int64_t *velpn,
+                                const double *vel_map, const int64_t *stif) {
+    base_t b;
+    if (make_base(&b, nnz, nnx, veln, velpn, vel_map, stif)) return NAN;
+    table_t t = {vd, ncol};
+    double r = tbp_impl(x1, x2, y1, y2, dnx, sg, &t, &b.m);
+    free_base(&b);
+    return r;
+}
+
+long oref_find_ray(double dnx, const double *vd, int ncol, double srcx, double srcy, double recx, double recy,
+                   const double *ttf, int fnz, int fnx, int nnz, int nnx, const double *veln, const int64_t *velpn,
+                   const double *vel_map, const int64_t *stif, int sg, double *rx, double *ry, long max_pts,
+                   double *time_out, int *early) {
+    base_t b;
+    if (make_base(&b, nnz, nnx, veln, velpn, vel_map, stif)) return -1;
+    table_t t = {vd, ncol};
+    long r = find_ray_impl(dnx, &t, srcx, srcy, recx, recy, ttf, fnz, fnx, &b.m, sg, rx, ry, max_pts, time_out, early);
+    free_base(&b);
+    return r;
+}
+
+/* Local operators on caller-provided (ttn, nsts) arrays, for the unit known-answer tests. */
+double oref_update(int nnz_arr, int nnx_arr, const double *ttn, const int32_t *nsts, int iz, int ix, double dnx,
+                   int nnz_arg, int nnx_arg, const double *veln, const int64_t *velpn, const double *vel_map,
+                   const int64_t *stif, const double *ph, int ncol) {
+    base_t b;
+    if (make_base(&b, nnz_arr, nnx_arr, veln, velpn, vel_map, stif)) return NAN;
+    fstate_t f = {nnz_arr, nnx_arr, (double *)ttn, (int32_t *)nsts, NULL, 0, 0};
+    table_t t = {ph, ncol};
+    double r = oref_update_f(&f, &b.m, &t, iz, ix, dnx, nnz_arg, nnx_arg);
+    free_base(&b);
+    return r;
+}
+double oref_fouds18(int nnz, int nnx, const double *ttn, const int32_t *nsts, int iz, int ix, double dnx, double dnz,
+                    const double *veln, const int64_t *velpn, const double *vel_map, const int64_t *stif,
+                    const double *av, int ncol) {
+    base_t b;
+    if (make_base(&b, nnz, nnx, veln, velpn, vel_map, stif)) return NAN;
+    fstate_t f = {nnz, nnx, (double *)ttn, (int32_t *)nsts, NULL, 0, 0};
+    table_t t = {av, ncol};
+    double r = oref_fouds18_f(&f, &b.m, &t, iz, ix, dnx, dnz, nnx, nnz);
+    free_base(&b);
+    return r;
+}
+double oref_group_vel(double angle, long c22, long c23, long c33, long c44, long sigma, double vel_scale) {
+    int64_t s[5] = {c22, c23, c33, c44, sigma};
+    return christoffel_group(s, angle, vel_scale);
+}
+
+/* ---- multithreaded batch (CPU baseline: one source per thread, like update_parallel) ---- */
+typedef struct {
+    const double *scx, *scz;
+    int nsrc, nnz, nnx, sg, ncol;
+    const double *veln, *vel_map, *av, *ph;
+    const int64_t *velpn, *stif;
+    double gox, goz, dnx, dnz;
+    double *out;
+    size_t out_stride;
+    int next;
+    pthread_mutex_t mu;
+    int rc;
+} batch_t;
+
+static void *batch_worker(void *arg) {
+    batch_t *bt = (batch_t *)arg;
+    for (;;) {
+        pthread_mutex_lock(&bt->mu);
+        int i = bt->next++;
+        pthread_mutex_unlock(&bt->mu);
+        if (i >= bt->nsrc) break;
+        int rc;
+        if (bt->sg <= 1)
+            rc = oref_travel(bt->scx[i], bt->scz[i], bt->nnz, bt->nnx, bt->veln, bt->velpn, bt->vel_map, bt->stif,
+                             bt->av, bt->ph, bt->ncol, bt->gox, bt->goz, bt->dnx, bt->dnz,
+                             bt->out + (size_t)i * bt->out_stride);
+        else
+            rc = oref_travel_finer_grid(bt->scx[i], bt->scz[i], bt->nnz, bt->nnx, bt->veln, bt->velpn, bt->vel_map,
+                                        bt->stif, bt->sg, bt->av, bt->ph, bt->ncol, bt->gox, bt->goz, bt->dnx,
+                                        bt->dnz, bt->out + (size_t)i * bt->out_stride);
+        if (rc) bt->rc = rc;
+    }
+    return NULL;
+}
+
+int oref_travel_batch(int nsrc, const double *scx, const double *scz, int nnz, int nnx, const double *veln,
+                      const int64_t *velpn, const double *vel_map, const int64_t *stif, int sg, const double *av,
+                      const double *ph, int ncol, double gox, double goz, double dnx, double dnz, double *out,
+                      int nthreads) {
+    batch_t bt;
+    memset(&bt, 0, sizeof bt);
+    bt.scx = scx; bt.scz = scz; bt.nsrc = nsrc; bt.nnz = nnz; bt.nnx = nnx; bt.sg = sg; bt.ncol = ncol;
+    bt.veln = veln; bt.vel_map = vel_map; bt.av = av; bt.ph = ph; bt.velpn = velpn; bt.stif = stif;
+    bt.gox = gox; bt.goz = goz; bt.dnx = dnx; bt.dnz = dnz; bt.out = out;
+    long fz = sg <= 1 ? nnz : (long)sg * (nnz - 1) + 1, fx = sg <= 1 ? nnx : (long)sg * (nnx - 1) + 1;
+    bt.out_stride = (size_t)fz * fx;
+    pthread_mutex_init(&bt.mu, NULL);
+    if (nthreads < 1) nthreads = 1;
+    pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * nthreads);
+    for (int t = 0; t < nthreads; t++) pthread_create(&th[t], NULL, batch_worker, &bt);
+    for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+    free(th);
+    pthread_mutex_destroy(&bt.mu);
+    return bt.rc;
+}

@@ -1,0 +1,220 @@
+/*
+ * oracle/band_model.c — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU model of the MI355X formulation (band-synchronous "Delta-stepping" FMM):
+ * every step accepts ALL close cells with T <= Tmin + delta, then re-evaluates the reference's
+ * local operator (update(), fouds18_A() fallback) for their non-known 4-neighbours Jacobi-style
+ * against the post-acceptance state, exactly as csrc/fmm_band.hip does.  It reuses the oracle's
+ * restated local operators, so GPU-vs-model differences isolate device arithmetic, and
+ * model-vs-oracle differences isolate the reformulation.  Used by tests/ only.
+ */
+#include "alifmm_oracle.c"
+
+/* status codes shared with the device kernel */
+enum { S_FAR = -1, S_FARC = -3, S_KNOWN = 0, S_CLOSE = 1, S_CLOSEC = 2 };
+
+typedef struct {
+    fstate_t f;        /* ttn + nsts (nsts holds the status codes above) */
+    int32_t *L, *L2, *A, *C;
+    int32_t *accstep;  /* step at which a cell was accepted (stage-1 quirk test) */
+    double *V;
+    long nL;
+} bstate_t;
+
+static int bstate_alloc(bstate_t *b, int nz, int nx, double *ttn_ext) {
+    if (fstate_alloc(&b->f, nz, nx, 4, ttn_ext)) return -1;
+    size_t n = (size_t)nz * nx;
+    b->L = (int32_t *)malloc(n * 4);
+    b->L2 = (int32_t *)malloc(n * 4);
+    b->A = (int32_t *)malloc(n * 4);
+    b->C = (int32_t *)malloc(n * 4);
+    b->accstep = (int32_t *)malloc(n * 4);
+    b->V = (double *)malloc(n * 8);
+    b->nL = 0;
+    if (!b->L || !b->L2 || !b->A || !b->C || !b->accstep || !b->V) return -1;
+    for (size_t i = 0; i < n; i++) b->accstep[i] = -1;
+    return 0;
+}
+static void bstate_free(bstate_t *b, int own) {
+    fstate_free(&b->f, own);
+    free(b->L); free(b->L2); free(b->A); free(b->C); free(b->accstep); free(b->V);
+}
+static inline void push_close(bstate_t *b, long idx) {
+    /* the heap's "addtree": status close + list entry (duplicates are harmless: see dedupe) */
+    if (b->f.nsts[idx] != S_CLOSE) { b->f.nsts[idx] = S_CLOSE; b->L[b->nL++] = (int32_t)idx; }
+}
+
+/* one band run on a grid until the close list drains (main) or the window edge is hit (stages) */
+static long band_run(bstate_t *b, const mat_t *m, const loopcfg_t *c, double delta, int sweeps, double t0) {
+    fstate_t *f = &b->f;
+    long nx = f->nnx, nz = f->nnz;
+    long steps = 0;
+    int finished = 0;
+    while (b->nL > 0 && !finished) {
+        double tmin = INFINITY;
+        for (long e = 0; e < b->nL; e++) { double t = f->ttn[b->L[e]]; if (t < tmin) tmin = t; }
+        /* near-source schedule: the band narrows in proportion to Tmin while Tmin < t0 */
+        double dl = delta;
+        if (t0 > 0 && tmin < t0) dl = delta * (tmin / t0);
+        double thr = tmin + dl;
+        long nA = 0, nL2 = 0;
+        for (long e = 0; e < b->nL; e++) {
+            long idx = b->L[e];
+            if (f->ttn[idx] <= thr) {
+                f->nsts[idx] = S_KNOWN;
+                b->accstep[idx] = (int32_t)steps;
+                b->A[nA++] = (int32_t)idx;
+            } else {
+                b->L2[nL2++] = (int32_t)idx;
+            }
+        }
+        /* claim candidates (dedupe); window-edge finish test (reference :1651-1652, :1673-1674) */
+        long nC = 0;
+        for (long a = 0; a < nA; a++) {
+            long idx = b->A[a], iz = idx / nx, ix = idx % nx;
+            long nb[4][2] = {{iz, ix - 1}, {iz, ix + 1}, {iz - 1, ix}, {iz + 1, ix}};
+            for (int q = 0; q < 4; q++) {
+                long z = nb[q][0], x = nb[q][1];
+                if (z < 0 || z >= nz || x < 0 || x >= nx) {
+                    if (c->stage) {
+                        if (q < 2 && labs(c->isx_s - x) == c->max_dist + 1) finished = 1;
+                        if (q >= 2 && labs(c->isz_s - z) == c->max_dist + 1) finished = 1;
+                    }
+                    continue;
+                }
+                long r = z * nx + x;
+                int32_t s = f->nsts[r];
+                if (s == S_FAR) { f->nsts[r] = S_FARC; b->C[nC++] = (int32_t)r; }
+                else if (s == S_CLOSE) { f->nsts[r] = S_CLOSEC; b->C[nC++] = (int32_t)r; }
+            }
+        }
+        for (int sw = 0; sw < sweeps; sw++) {
+            for (long k = 0; k < nC; k++) {
+                long r = b->C[k], iz = r / nx, ix = r % nx;
+                int quirk = 0;
+                if (c->quirk_nnz && (sw == 0 ? f->nsts[r] == S_CLOSEC : 1)) {
+                    /* stage-1 quirk (:1645): a close cell re-evaluated because an x-neighbour was popped */
+                    if ((ix > 0 && b->accstep[r - 1] == steps) || (ix < nx - 1 && b->accstep[r + 1] == steps)) quirk = 1;
+                }
+                double v = oref_update_f(f, m, c->ph, iz, ix, c->dnx, quirk ? nx : nz, nx);
+                if (v == -1.0) v = oref_fouds18_f(f, m, c->av, iz, ix, c->dnx, c->dnz_fouds, nx, nz);
+                b->V[k] = v;
+            }
+            if (sw + 1 < sweeps) {
+                /* Gauss-Seidel-like second sweep: candidates see each other's first-sweep values */
+                for (long k = 0; k < nC; k++) { long r = b->C[k]; f->ttn[r] = b->V[k]; f->nsts[r] = S_CLOSEC; }
+            }
+        }
+        for (long k = 0; k < nC; k++) {
+            long r = b->C[k];
+            f->ttn[r] = b->V[k];
+            if (f->nsts[r] == S_FARC) b->L2[nL2++] = (int32_t)r;
+            f->nsts[r] = S_CLOSE;
+        }
+        int32_t *t = b->L; b->L = b->L2; b->L2 = t;
+        b->nL = nL2;
+        steps++;
+    }
+    return steps;
+}
+
+/* hand-over (reference :2006-2040 etc.) into a band state */
+static void band_handover(const fstate_t *s, long isz_s, long isx_s, bstate_t *d, long isz_d, long isx_d) {
+    for (long i = 0; i < s->nnz + 1; i += 3) {
+        for (long j = 0; j < s->nnx + 1; j += 3) {
+            long pz = isz_d + (i - isz_s) / 3, px = isx_d + (j - isx_s) / 3;
+            long di = pz * d->f.nnx + px;
+            d->f.ttn[di] = s->ttn[i * s->nnx + j];
+            int32_t st = s->nsts[i * s->nnx + j];
+            if (st == 0) {
+                d->f.nsts[di] = S_KNOWN;
+                int outer = 0;
+                if (i - 3 >= 0) { if (s->nsts[(i - 3) * s->nnx + j] == -1) outer = 1; } else outer = 1;
+                if (i + 3 <= s->nnz - 1) { if (s->nsts[(i + 3) * s->nnx + j] == -1) outer = 1; } else outer = 1;
+                if (j - 3 >= 0) { if (s->nsts[i * s->nnx + j - 3] == -1) outer = 1; } else outer = 1;
+                if (j + 3 <= s->nnx - 1) { if (s->nsts[i * s->nnx + j + 3] == -1) outer = 1; } else outer = 1;
+                if (outer) push_close(d, di);
+            }
+            if (st > 0) push_close(d, di);
+        }
+    }
+}
+
+/* travel() with band stages (exact_init=0) or the reference's heap stages (exact_init=1) */
+int oband_travel(double scx, double scz, int nnz, int nnx, const double *veln, const int64_t *velpn,
+                 const double *vel_map, const int64_t *stif, const double *av_, const double *ph_, int ncol,
+                 double gox, double goz, double dnx, double dnz, double cdelta, double vmax, int exact_init,
+                 int sweeps, double r0, double *ttn, long *steps_out) {
+    base_t bb;
+    if (make_base(&bb, nnz, nnx, veln, velpn, vel_map, stif)) return -1;
+    const mat_t *base = &bb.m;
+    table_t tav = {av_, ncol}, tph = {ph_, ncol};
+    const table_t *av = &tav, *ph = &tph;
+    memset(ttn, 0, sizeof(double) * (size_t)nnz * nnx);
+    long isx = pyround((scx - gox) / dnx), isz = pyround((scz - goz) / dnz);
+    long steps[4] = {0, 0, 0, 0};
+    long sgs[3] = {27, 9, 3}, sizes[3] = {2, 6, 13};
+    fstate_t prev;       /* previous stage (heap or band) in fstate form */
+    bstate_t bprev;
+    int have_b = 0;
+    long pisz = 0, pisx = 0;
+    view_t views[3];
+    for (int st = 0; st < 3; st++) {
+        long sg = sgs[st], size = sizes[st];
+        long left = imax(0, isx - size), right = imin(nnx - 1, isx + size);
+        long bottom = imax(0, isz - size), top = imin(nnz - 1, isz + size);
+        make_view(&views[st], base, bottom, top, left, right, sg);
+        long isx_s = sg * (isx - left), isz_s = sg * (isz - bottom);
+        double dn = dnx / sg;
+        loopcfg_t c = {av, ph, dn, dn, 1, (int)isx_s, (int)isz_s, (int)(sg * size), st == 0};
+        if (exact_init == 1 || (exact_init == 2 && st == 0) || (exact_init == 3 && st < 2)) {
+            fstate_t f;
+            fstate_alloc(&f, views[st].m.nnz, views[st].m.nnx, 0, NULL);
+            if (st == 0) {
+                straight_rays(&f, isz_s, isx_s, (sg - 1) / 2, dn, base, (int)isz, (int)isx, av, 0);
+                add_edges(&f, isz_s, isx_s, (sg - 1) / 2);
+            } else {
+                handover(&prev, pisz, pisx, &f, isz_s, isx_s);
+                fstate_free(&prev, 1);
+            }
+            fmm_loop(&f, &views[st].m, &c);
+            prev = f;
+            have_b = 0;
+        } else {
+            bstate_t b;
+            bstate_alloc(&b, views[st].m.nnz, views[st].m.nnx, NULL);
+            if (st == 0) {
+                straight_rays(&b.f, isz_s, isx_s, (sg - 1) / 2, dn, base, (int)isz, (int)isx, av, 0);
+                /* add_edges: the window border of the straight-ray square becomes close */
+                long s1 = (sg - 1) / 2, n1z = b.f.nnz, n1x = b.f.nnx;
+                if (isz_s - s1 >= 0) for (long i = imax(0, isx_s - s1); i <= imin(n1x - 1, isx_s + s1); i++) push_close(&b, (isz_s - s1) * n1x + i);
+                if (isz_s + s1 <= n1z - 1) for (long i = imax(0, isx_s - s1); i <= imin(n1x - 1, isx_s + s1); i++) push_close(&b, (isz_s + s1) * n1x + i);
+                if (isx_s - s1 >= 0) for (long i = imax(0, isz_s - s1); i <= imin(n1z - 1, isz_s + s1); i++) push_close(&b, i * n1x + isx_s - s1);
+                if (isx_s + s1 <= n1x - 1) for (long i = imax(0, isz_s - s1); i <= imin(n1z - 1, isz_s + s1); i++) push_close(&b, i * n1x + isx_s + s1);
+            } else if (!have_b) {
+                band_handover(&prev, pisz, pisx, &b, isz_s, isx_s);
+                fstate_free(&prev, 1);
+            } else {
+                band_handover(&bprev.f, pisz, pisx, &b, isz_s, isx_s);
+                /* map band status back to heap-style codes for the hand-over test (close > 0) */
+                bstate_free(&bprev, 1);
+            }
+            steps[st] = band_run(&b, &views[st].m, &c, cdelta * dn / vmax, sweeps, r0 * dnx / vmax);
+            bprev = b;
+            have_b = 1;
+        }
+        pisz = isz_s; pisx = isx_s;
+    }
+    loopcfg_t c = {av, ph, dnx, dnz, 0, 0, 0, 0, 0};
+    bstate_t bm;
+    bstate_alloc(&bm, nnz, nnx, ttn);
+    if (!have_b) { band_handover(&prev, pisz, pisx, &bm, isz, isx); fstate_free(&prev, 1); }
+    else { band_handover(&bprev.f, pisz, pisx, &bm, isz, isx); bstate_free(&bprev, 1); }
+    steps[3] = band_run(&bm, base, &c, cdelta * dnx / vmax, sweeps, r0 * dnx / vmax);
+    bstate_free(&bm, 0);
+    for (int st = 0; st < 3; st++) free_view(&views[st]);
+    free_base(&bb);
+    if (steps_out) for (int i = 0; i < 4; i++) steps_out[i] = steps[i];
+    (void)have_b;
+    return 0;
+}
