@@ -1,0 +1,608 @@
+"""
+Anisotropic travel-time fields and ray tracing — MI355X drop-in for the reference module
+``Anis_TTF_rays`` (WiPi-UoS/ALI-FMM-and-ray-tracing, Anis_TTF_rays.py).
+
+Same names, positional signatures, argument meaning, return values and error behaviour as the
+reference, so ``Weld_rays.py`` and the tutorial notebook run unchanged.  The hot path runs on the
+GPU through the C-ABI of ``lib/libalifmm.so`` (include/alifmm.h):
+
+  travel / travel_finer_grid        -> alifmm_travel      (exact-heap source init in LDS +
+                                                           band-synchronous FMM, csrc/fmm_*.hip)
+  find_ray / ray_time               -> alifmm_find_rays   (one wavefront per ray, csrc/rays.hip)
+  time_between_points               -> alifmm_time_between_points
+  update / fouds18_A                -> alifmm_local_ops   (the reference's local operators)
+
+Host-side utilities that are not on the hot path (velocity-table generation, material tables,
+grid refinement helpers, plotting) are plain Python/numpy with the reference's semantics.
+There is no CPU fallback: without the library or a GPU every GPU entry point raises.
+Parity contract (what matches the reference bit-for-bit and what within a stated tolerance):
+DESIGN.md §4.
+"""
+import math
+import os
+import sys
+import threading
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import _alifmm  # noqa: E402
+
+# Parameter used to enable/disable progress bars (reference :22-24; kept for API compatibility)
+tqdm_disable = False
+
+_EARLY_MSG = "Travel time to receiver increasing: Finishing ray early"
+
+
+# ------------------------------------------------------------------------------------------------
+# model hashing (re-upload only when the arrays change)
+def _digest(*arrays):
+    import xxhash
+
+    h = xxhash.xxh3_64()
+    for a in arrays:
+        if a is None:
+            h.update(b"None")
+            continue
+        a = np.ascontiguousarray(a)
+        h.update(str((a.dtype.str, a.shape)).encode())
+        h.update(memoryview(a).cast("B"))
+    return h.hexdigest()
+
+
+def _prep_model(veln, velpn, vel_map, stif_den, group_tab, phase_tab):
+    veln = np.ascontiguousarray(veln, dtype=np.float64)
+    velpn = np.ascontiguousarray(velpn).astype(np.int64, copy=False)
+    vel_map = np.ones(veln.shape) if vel_map is None else np.ascontiguousarray(vel_map, dtype=np.float64)
+    stif = None if stif_den is None else np.ascontiguousarray(stif_den).astype(np.int64, copy=False)
+    gt = np.ascontiguousarray(group_tab, dtype=np.float64)
+    pt = gt if phase_tab is None else np.ascontiguousarray(phase_tab, dtype=np.float64)
+    return veln, velpn, vel_map, stif, gt, pt
+
+
+def _load_model(ctx, veln, velpn, vel_map, stif_den, group_tab, phase_tab, dnx, dnz, gox=0.0, goz=0.0):
+    veln, velpn, vel_map, stif, gt, pt = _prep_model(veln, velpn, vel_map, stif_den, group_tab, phase_tab)
+    key = (_digest(veln, velpn, vel_map, stif, gt, pt), float(dnx), float(dnz), float(gox), float(goz))
+    ctx.set_model(veln, velpn, vel_map, stif, gt, pt, dnx, dnz, gox, goz, key=key)
+    return veln.shape
+
+
+_module_ctx = None
+_module_lock = threading.Lock()
+
+
+def _mctx():
+    global _module_ctx
+    with _module_lock:
+        if _module_ctx is None:
+            _module_ctx = _alifmm.Context(0)
+        return _module_ctx
+
+
+# ------------------------------------------------------------------------------------------------
+# Host utilities (reference :26-91, :3521-3558, :3737-3787)
+def finer_grid_n(veln, scale, dtype=np.int32):
+    """Nearest-neighbour refinement by odd `scale` (reference :26-56); default dtype int32 truncates."""
+    veln = np.asarray(veln)
+    side = (scale - 1) // 2
+    nz, nx = scale * (veln.shape[0] - 1) + 1, scale * (veln.shape[1] - 1) + 1
+    iz = (np.arange(nz) + side) // scale
+    ix = (np.arange(nx) + side) // scale
+    return veln[iz][:, ix].astype(dtype)
+
+
+def finer_grid_n_2(data, scale):
+    """Refinement of the (nnz, nnx, 5) stiffness/density array (reference :59-91); None -> None."""
+    if data is None:
+        return None
+    data = np.asarray(data)
+    side = (scale - 1) // 2
+    nz, nx = scale * (data.shape[0] - 1) + 1, scale * (data.shape[1] - 1) + 1
+    iz = (np.arange(nz) + side) // scale
+    ix = (np.arange(nx) + side) // scale
+    return data[iz][:, ix].astype(np.int64)
+
+
+def group_vel(angle, c_22, c_23, c_33, c_44, sigma, vel_scale=1):
+    """Closed-form 2D orthotropic Christoffel group velocity (reference :3521-3558)."""
+    if angle % 90 < 0.01 or angle % 90 > 90 - 0.01:
+        if abs((angle % 180) - 90) < 1:
+            lambda_val = c_33
+        else:
+            lambda_val = c_22
+        return 1000 * vel_scale * math.sqrt(lambda_val / sigma)
+    tan_ang = math.tan(math.radians(angle))
+    A = c_22 + c_33 - 2 * c_44
+    B = (c_23 + c_44) * (tan_ang - 1 / tan_ang)
+    C = c_22 - c_33
+    if angle < 90:
+        phase_angle_rad = math.atan((-B - math.sqrt(B ** 2 + A ** 2 - C ** 2)) / (C - A)) % math.pi
+    else:
+        phase_angle_rad = math.atan((-B + math.sqrt(B ** 2 + A ** 2 - C ** 2)) / (C - A)) % math.pi
+    lambda_val = 0.5 * (math.cos(2 * phase_angle_rad) * (c_22 - c_44) + math.sin(2 * phase_angle_rad) * (c_23 + c_44) *
+                        tan_ang + c_22 + c_44)
+    return 1000 * vel_scale * math.sqrt(lambda_val / sigma) / math.cos(math.radians(angle) - phase_angle_rad)
+
+
+def min_max_vel(veln, velpn, vel_map, stif_den, group_vel_table):
+    """Model velocity range sanity check (reference :3737-3787; note it branches on velpn[0, 0])."""
+    velpn = np.asarray(velpn)
+    vel_map = np.asarray(vel_map, dtype=np.float64)
+    tab = np.asarray(group_vel_table, dtype=np.float64)
+    gmin = tab.min(axis=0)
+    gmax = tab.max(axis=0)
+    if velpn[0, 0] == 0:
+        sd = np.asarray(stif_den)
+        s0 = sd[0, 0]
+        mn = mx = group_vel(0, int(s0[0]), int(s0[1]), int(s0[2]), int(s0[3]), int(s0[4]), vel_map[0, 0])
+        rows = np.concatenate([sd.reshape(-1, 5).astype(np.float64), vel_map.reshape(-1, 1)], axis=1)
+        uniq = np.unique(rows, axis=0)
+        for r in uniq:
+            c = [int(v) for v in r[:5]]
+            for a in (0, 45, 90, 135):
+                v = group_vel(a, c[0], c[1], c[2], c[3], c[4], r[5])
+                mn, mx = min(mn, v), max(mx, v)
+        return mn, mx
+    mn = mx = vel_map[0, 0] * tab[0, velpn[0, 0]]
+    mn = min(mn, float(np.min(vel_map * gmin[velpn])))
+    mx = max(mx, float(np.max(vel_map * gmax[velpn])))
+    return mn, mx
+
+
+# ------------------------------------------------------------------------------------------------
+# Hot-path module functions (GPU)
+def travel(scx, scz, nsts, btg, ntr, ttn, veln, velpn, vel_map, stif_den, avlist2, phase_vel, gox, goz, dnx, dnz,
+           nnx, nnz):
+    """Travel-time field of one source, subgrid 1 (reference :1463-2117).
+
+    Like the reference, writes the field into `ttn` and returns it; nsts/btg/ntr are ignored
+    (the GPU keeps its own node status and work lists)."""
+    ctx = _mctx()
+    _load_model(ctx, veln, velpn, vel_map, stif_den, avlist2, phase_vel, dnx, dnz, gox, goz)
+    T = ctx.travel([scx], [scz], subgrid=1, first_slot=0)[0]
+    ttn[...] = T
+    return ttn
+
+
+def travel_finer_grid(scx, scz, veln0, velpn0, vel_map0, stif_den0, subgrid_size, avlist2, phase_vel, gox, goz, dnx,
+                      dnz):
+    """Travel-time field on the subgrid_size-refined grid, divided by subgrid_size (reference :2120-2832)."""
+    ctx = _mctx()
+    _load_model(ctx, veln0, velpn0, vel_map0, stif_den0, avlist2, phase_vel, dnx, dnz, gox, goz)
+    return ctx.travel([scx], [scz], subgrid=int(subgrid_size), first_slot=0)[0]
+
+
+def find_ray(dnx, velocity_dat, source, receiver, rec_TTF, veln, velpn, vel_map, stif_den, subgrid_size):
+    """Ray back-trace through the receiver's field (reference :3104-3465) -> (ray_x, ray_y, time)."""
+    ctx = _mctx()
+    _load_model(ctx, veln, velpn, vel_map, stif_den, velocity_dat, velocity_dat, dnx, dnx)
+    sg = int(subgrid_size)
+    ctx.put_field(0, sg, rec_TTF)
+    times, lens, flags, rays = ctx.find_rays([0], [source[0], source[1]], [receiver[0], receiver[1]])
+    if flags[0] & 1:
+        print(_EARLY_MSG)
+    return rays[0][0], rays[0][1], float(times[0])
+
+
+def time_between_points(x1, x2, y1, y2, dnx, subgrid_size, velocity_dat, veln, velpn, vel_map, stif_den):
+    """Straight-segment travel time over coarse cells (reference :2835-2989)."""
+    ctx = _mctx()
+    _load_model(ctx, veln, velpn, vel_map, stif_den, velocity_dat, velocity_dat, dnx, dnx)
+    return float(ctx.time_between_points([x1], [x2], [y1], [y2], int(subgrid_size))[0])
+
+
+def ray_time(ray_x, ray_y, dnx, subgrid_size, velocity_dat, veln, velpn, vel_map, stif_den):
+    """Travel time along a ray: segment times summed in order (reference :2992-3022)."""
+    ray_x = np.asarray(ray_x, dtype=np.float64)
+    ray_y = np.asarray(ray_y, dtype=np.float64)
+    if len(ray_x) < 2:
+        return 0.0
+    ctx = _mctx()
+    _load_model(ctx, veln, velpn, vel_map, stif_den, velocity_dat, velocity_dat, dnx, dnx)
+    seg = ctx.time_between_points(ray_x[:-1], ray_x[1:], ray_y[:-1], ray_y[1:], int(subgrid_size))
+    t = 0.0
+    for s in seg:
+        t += float(s)
+    return t
+
+
+def _cell(a, iz, ix):
+    return np.asarray(a)[iz, ix]
+
+
+def update(veln, velpn, vel_map, nsts, ttn, iz, ix, dnx, nnz, nnx, phase_vel, stif_den):
+    """ALI local wavefront update of cell (iz, ix) (reference :904-1410); -1.0 if no stencil."""
+    ttn = np.asarray(ttn, dtype=np.float64)
+    st = None if stif_den is None else np.asarray(stif_den)[iz, ix][None, :]
+    out = _mctx().local_ops(0, ttn[None], np.asarray(nsts)[None], [iz], [ix], [dnx], [dnx], [nnz], [nnx],
+                            [_cell(veln, iz, ix)], [_cell(velpn, iz, ix)], [_cell(vel_map, iz, ix)], st, phase_vel)
+    return float(out[0])
+
+
+def fouds18_A(iz, ix, nsts, ttn, dnx, dnz, nnx, nnz, veln, velpn, vel_map, avlist2, stif_den):
+    """Multi-stencil quadratic fallback of cell (iz, ix) with group velocity (reference :240-901)."""
+    ttn = np.asarray(ttn, dtype=np.float64)
+    st = None if stif_den is None else np.asarray(stif_den)[iz, ix][None, :]
+    out = _mctx().local_ops(1, ttn[None], np.asarray(nsts)[None], [iz], [ix], [dnx], [dnz], [nnz], [nnx],
+                            [_cell(veln, iz, ix)], [_cell(velpn, iz, ix)], [_cell(vel_map, iz, ix)], st, avlist2)
+    return float(out[0])
+
+
+# ------------------------------------------------------------------------------------------------
+class ALI_FMM:
+    """
+    Class for calculating travel time fields and performing ray tracing through the travel time fields
+    (reference :3789-4705).  GPU work goes to one context per MI355X (device 0 unless n_threads > 1
+    spreads the sources of the *_parallel methods over the visible GPUs).
+    """
+
+    def __init__(self, veln, velpn, vel_map, scx, scz, group_vel=None, phase_vel=None, stif_den=None, dnx=1e-3):
+        self.stif_den = stif_den
+        if type(stif_den) != type(None):
+            if type(stif_den[0, 0, 0]) != np.int64:
+                raise TypeError("Stifness tensors and density array must have the type np.int64. 32bit integers will "
+                                "not work correctly.")
+            elif stif_den[0, 0, 0] > 1e9:
+                print("Warning: Stifness tensors must be in MPa, due to 64 bit integer limitations when solving the "
+                      "christoffel equation")
+        if type(group_vel) == type(None):
+            self.velocity_dat = 1 * np.ones((361, 2))
+            self.velocity_dat[:, 0] = np.arange(0, 361)
+            self.phase_vel = np.copy(self.velocity_dat)
+        else:
+            self.velocity_dat = group_vel
+            self.phase_vel = phase_vel
+        self.veln = veln
+        self.velpn = velpn
+        try:
+            if np.issubdtype(velpn[0, 0], np.integer) == False:  # noqa: E712
+                raise TypeError("velpn must be a numpy array of integers")
+        except Exception:
+            raise TypeError("velpn must be a numpy array of integers")
+        self.vel_map = vel_map
+        self.dnx = dnx
+        self.dnz = dnx
+        self.nnx = veln.shape[1]
+        self.nnz = veln.shape[0]
+        self.ttn = np.zeros(veln.shape)
+        self.scx = scx
+        self.scz = scz
+        self.gox = 0
+        self.goz = 0
+        self.isx = np.zeros(len(scx))
+        self.isz = np.zeros(len(scx))
+        for i in range(len(scx)):
+            self.isx[i] = round((scx[i] - self.gox) / self.dnx)
+            self.isz[i] = round((scz[i] - self.goz) / self.dnz)
+        self.ntr = 0
+        self.nsrc = len(scx)
+        # The reference's CPU heap buffers (nsts, btg) are not used: the GPU owns its work lists.
+        self.maxbt = round(0.5 * self.nnx * self.nnz)
+        self.nsts = None
+        self.btg = None
+        self.ray_paths_x = None
+        self.ray_paths_y = None
+        self.ray_len = None
+        self._ctxs = {}
+
+    # ---- GPU plumbing ----
+    def _ctx(self, device=0):
+        c = self._ctxs.get(device)
+        if c is None:
+            c = _alifmm.Context(device)
+            self._ctxs[device] = c
+        return c
+
+    def _devices(self, n_threads):
+        n = max(1, min(int(n_threads), _alifmm.device_count()))
+        return list(range(n))
+
+    def _fields(self, veln, velpn, vel_map, stif_den, subgrid_size, idx, devices, copy_out=True, slot_of=None):
+        """Fields of the sources `idx`, block-distributed over `devices` (one host thread per GPU)."""
+        idx = list(idx)
+        parts = [idx[k::len(devices)] for k in range(len(devices))]
+        results = {}
+        errors = []
+
+        def work(dev, ids):
+            try:
+                ctx = self._ctx(dev)
+                _load_model(ctx, veln, velpn, vel_map, stif_den, self.velocity_dat, self.phase_vel, self.dnx,
+                            self.dnz, self.gox, self.goz)
+                if not ids:
+                    return
+                x = np.array([float(self.scx[i]) for i in ids])
+                z = np.array([float(self.scz[i]) for i in ids])
+                out = ctx.travel(x, z, subgrid=int(subgrid_size), first_slot=0, copy_out=copy_out)
+                for k, i in enumerate(ids):
+                    results[i] = (dev, k, None if out is None else out[k])
+            except Exception as e:  # surfaced below
+                errors.append(e)
+
+        if len(devices) == 1:
+            work(devices[0], parts[0])
+        else:
+            th = [threading.Thread(target=work, args=(d, p)) for d, p in zip(devices, parts)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+        if errors:
+            raise errors[0]
+        return results
+
+    # ---- reference API ----
+    def update(self, veln, velpn, vel_map=None, stif_den=None, subgrid_size=1, sources=None):
+        """Travel-time fields for all (or the selected) sources (reference :3870-3936)."""
+        if type(stif_den) == type(None):
+            self.stif_den = np.zeros((veln.shape[0], veln.shape[1], 5))
+        else:
+            self.stif_den = stif_den
+        self.veln = veln
+        self.velpn = velpn
+        self.vel_map = np.ones(veln.shape) if type(vel_map) == type(None) else vel_map
+        if type(sources) == type(None):
+            sources = np.ones(len(self.scx))
+        idx = [i for i in range(self.nsrc) if sources[i] == 1]
+        res = self._fields(veln, velpn, self.vel_map, stif_den, subgrid_size, idx, [0])
+        ctx = self._ctx(0)
+        fz, fx = ctx.field_shape(subgrid_size)
+        travel_time_field = np.zeros((self.nsrc, fz, fx))
+        for i, (_, _, T) in res.items():
+            travel_time_field[i] = T
+        return travel_time_field
+
+    def update_parallel(self, veln, velpn, vel_map=None, stif_den=None, subgrid_size=1, sources=None, n_threads=2,
+                        low_mem=False):
+        """As update(), spread over min(n_threads, #GPUs) GPUs (reference :3938-4051).
+
+        low_mem=True saves each field to temp_TTF_<i>.npy in the working directory and returns None."""
+        if type(stif_den) == type(None):
+            self.stif_den = np.zeros((veln.shape[0], veln.shape[1], 5))
+        else:
+            self.stif_den = stif_den
+        self.veln = veln
+        self.velpn = velpn
+        self.vel_map = np.ones(veln.shape) if type(vel_map) == type(None) else vel_map
+        if type(sources) == type(None):
+            sources = np.ones(len(self.scx), dtype=int)
+        idx = [i for i in range(self.nsrc) if sources[i] == 1]
+        res = self._fields(veln, velpn, self.vel_map, stif_den, subgrid_size, idx, self._devices(n_threads))
+        if low_mem:
+            for i, (_, _, T) in res.items():
+                np.save("temp_TTF_" + str(i) + ".npy", T)
+            return None
+        fz, fx = self._ctx(0).field_shape(subgrid_size)
+        travel_time_field = np.zeros((self.nsrc, fz, fx))
+        for i, (_, _, T) in res.items():
+            travel_time_field[i] = T
+        return travel_time_field
+
+    def update_i(self, source_i, veln, velpn, vel_map, stif_den=None, subgrid_size=1):
+        """Travel-time field of one source (reference :4053-4088)."""
+        if type(vel_map) == type(None):
+            vel_map = np.ones(veln.shape)
+        if type(stif_den) == type(None):
+            stif_den = np.zeros((veln.shape[0], veln.shape[1], 5))
+        res = self._fields(veln, velpn, vel_map, stif_den, subgrid_size, [source_i], [0])
+        return res[source_i][2]
+
+    def plot_phase(self, material_index=1):
+        import matplotlib.pyplot as plt
+
+        plt.polar(math.pi / 180 * self.velocity_dat[:, 0], self.phase_vel[:, material_index])
+        plt.show()
+
+    def plot_group(self, material_index=1):
+        import matplotlib.pyplot as plt
+
+        plt.polar(math.pi / 180 * self.velocity_dat[:, 0], self.velocity_dat[:, material_index])
+        plt.show()
+
+    def generate_group_vel(self, c_22, c_23, c_33, c_44, density, plot=True):
+        """Group velocity table 0..360 deg (reference :4112-4160)."""
+        group_vel = np.zeros(361)
+        for angle in range(361):
+            if angle < 180:
+                if angle % 90 == 0:
+                    lambda_val = c_33 if angle % 180 == 90 else c_22
+                    velocity = math.sqrt(lambda_val / density)
+                else:
+                    tan_ang = math.tan(math.radians(angle))
+                    A = c_22 + c_33 - 2 * c_44
+                    B = (c_23 + c_44) * (tan_ang - 1 / tan_ang)
+                    C = c_22 - c_33
+                    if angle < 90:
+                        phase_angle_rad = math.atan((-B - math.sqrt(B ** 2 + A ** 2 - C ** 2)) / (C - A)) % math.pi
+                    else:
+                        phase_angle_rad = math.atan((-B + math.sqrt(B ** 2 + A ** 2 - C ** 2)) / (C - A)) % math.pi
+                    lambda_val = 0.5 * (math.cos(2 * phase_angle_rad) * (c_22 - c_44) + math.sin(2 * phase_angle_rad) *
+                                        (c_23 + c_44) * tan_ang + c_22 + c_44)
+                    velocity = math.sqrt(lambda_val / density) / math.cos(math.radians(angle) - phase_angle_rad)
+                group_vel[angle] = velocity
+            else:
+                group_vel[angle] = group_vel[angle - 180]
+        if plot == True:  # noqa: E712
+            import matplotlib.pyplot as plt
+
+            plt.polar(math.pi / 180 * np.arange(0, 361), group_vel)
+            plt.title("Group Velocity")
+            plt.show()
+        return group_vel
+
+    def generate_phase_vel(self, c_22, c_23, c_33, c_44, density, plot=True):
+        """Phase velocity table 0..360 deg (reference :4162-4206)."""
+        phase_vel = np.zeros(361)
+        for angle in range(361):
+            if angle < 180:
+                if angle % 90 == 0:
+                    lambda_val = c_33 if angle % 180 == 90 else c_22
+                    velocity = math.sqrt(lambda_val / density)
+                else:
+                    cos_ang = math.cos(math.radians(angle))
+                    sin_ang = math.sin(math.radians(angle))
+                    A = cos_ang ** 2 * c_22 + sin_ang ** 2 * c_44
+                    B = cos_ang * sin_ang * (c_23 + c_44)
+                    C = cos_ang ** 2 * c_44 + sin_ang ** 2 * c_33
+                    velocity = math.sqrt((A + C + math.sqrt((A - C) ** 2 + 4 * B ** 2)) / (2 * density))
+                phase_vel[angle] = velocity
+            else:
+                phase_vel[angle] = phase_vel[angle - 180]
+        if plot == True:  # noqa: E712
+            import matplotlib.pyplot as plt
+
+            plt.polar(math.pi / 180 * np.arange(0, 361), phase_vel)
+            plt.title("Phase Velocity")
+            plt.show()
+        return phase_vel
+
+    def add_materials(self, materials, keep_materials=False):
+        """Append (or replace) table materials from stiffness/density rows (reference :4208-4256,
+        including its column-count behaviour for 2D input without keep_materials, SURVEY B-D10)."""
+        if keep_materials == True:  # noqa: E712
+            if materials.ndim == 1:
+                group_vel_data = np.zeros((361, self.velocity_dat.shape[1] + 1))
+                group_vel_data[:, 0:self.velocity_dat.shape[1]] = self.velocity_dat
+                group_vel_data[:, group_vel_data.shape[1] - 1] = self.generate_group_vel(
+                    materials[0], materials[1], materials[2], materials[3], materials[4], False)
+                phase_vel_data = np.zeros((361, self.phase_vel.shape[1] + 1))
+                phase_vel_data[:, 0:self.velocity_dat.shape[1]] = self.phase_vel
+                phase_vel_data[:, group_vel_data.shape[1] - 1] = self.generate_phase_vel(
+                    materials[0], materials[1], materials[2], materials[3], materials[4], False)
+                print("material id of new material is " + str(self.velocity_dat.shape[1]))
+            else:
+                group_vel_data = np.zeros((361, self.velocity_dat.shape[1] + materials.shape[1]))
+                group_vel_data[:, 0:self.velocity_dat.shape[1]] = self.velocity_dat
+                phase_vel_data = np.zeros((361, self.velocity_dat.shape[1] + materials.shape[1]))
+                phase_vel_data[:, 0:self.velocity_dat.shape[1]] = self.phase_vel
+                for i in range(materials.shape[0]):
+                    index = i + self.velocity_dat.shape[1]
+                    group_vel_data[:, index] = self.generate_group_vel(materials[i, 0], materials[i, 1],
+                                                                       materials[i, 2], materials[i, 3],
+                                                                       materials[i, 4], False)
+                    phase_vel_data[:, index] = self.generate_phase_vel(materials[i, 0], materials[i, 1],
+                                                                       materials[i, 2], materials[i, 3],
+                                                                       materials[i, 4], False)
+                print("material id's of new materials are " + str(self.velocity_dat.shape[1]) + " - " +
+                      str(self.velocity_dat.shape[1] + materials.shape[0] - 1))
+        else:
+            if materials.ndim == 1:
+                group_vel_data = np.zeros((361, 2))
+                phase_vel_data = np.zeros((361, 2))
+            else:
+                group_vel_data = np.zeros((361, materials.shape[1] + 1))
+                phase_vel_data = np.zeros((361, materials.shape[1] + 1))
+            group_vel_data[:, 0] = np.arange(0, 361)
+            phase_vel_data[:, 0] = np.arange(0, 361)
+            if materials.ndim == 1:
+                group_vel_data[:, 1] = self.generate_group_vel(materials[0], materials[1], materials[2], materials[3],
+                                                               materials[4], False)
+                phase_vel_data[:, 1] = self.generate_phase_vel(materials[0], materials[1], materials[2], materials[3],
+                                                               materials[4], False)
+            else:
+                for i in range(materials.shape[1]):
+                    index = i + 1
+                    group_vel_data[:, index] = self.generate_group_vel(materials[i, 0], materials[i, 1],
+                                                                       materials[i, 2], materials[i, 3],
+                                                                       materials[i, 4], False)
+                    phase_vel_data[:, index] = self.generate_phase_vel(materials[i, 0], materials[i, 1],
+                                                                       materials[i, 2], materials[i, 3],
+                                                                       materials[i, 4], False)
+        self.velocity_dat = group_vel_data
+        self.phase_vel = phase_vel_data
+
+    def _rays(self, veln, velpn, vel_map, stif_den, subgrid_size, trans_pairs, save_rays, n_devices, include_self):
+        n_trans = len(self.isx)
+        if save_rays:
+            self.ray_paths_x = np.zeros((n_trans, n_trans, 5 * (veln.shape[0] + veln.shape[1])))
+            self.ray_paths_y = np.copy(self.ray_paths_x)
+            self.ray_len = np.zeros((n_trans, n_trans), dtype=int)
+        if type(trans_pairs) == type(None):
+            trans_pairs = np.zeros((n_trans, n_trans))
+            for i in range(n_trans):
+                for j in range(n_trans):
+                    if i < j:
+                        trans_pairs[i, j] = 1
+        rec = [j for j in range(n_trans) if np.sum(trans_pairs[:, j]) > 0]
+        sg = int(subgrid_size)
+        new_trans_x = sg * self.isx
+        new_trans_y = sg * self.isz
+        times = np.zeros((n_trans, n_trans))
+        devices = self._devices(n_devices)
+        # receivers block-distributed over GPUs; each ray is traced on the GPU holding its receiver field
+        res = self._fields(veln, velpn, vel_map, stif_den, sg, rec, devices, copy_out=False)
+        errors = []
+
+        def trace(dev):
+            try:
+                pairs = []
+                for j, (d, slot, _) in res.items():
+                    if d != dev:
+                        continue
+                    for i in range(n_trans):
+                        if (include_self or i != j) and trans_pairs[i, j] == 1:
+                            pairs.append((i, j, slot))
+                if not pairs:
+                    return
+                ctx = self._ctx(dev)
+                src = np.array([[new_trans_x[i], new_trans_y[i]] for i, _, _ in pairs])
+                dst = np.array([[new_trans_x[j], new_trans_y[j]] for _, j, _ in pairs])
+                t, lens, flags, rays = ctx.find_rays([s for _, _, s in pairs], src, dst, with_points=save_rays)
+                for k, (i, j, _) in enumerate(pairs):
+                    if flags[k] & 1:
+                        print(_EARLY_MSG)
+                    times[i, j] = t[k]
+                    if save_rays:
+                        ray_x = rays[k][0] / sg
+                        ray_y = rays[k][1] / sg
+                        ray_len = len(ray_x)
+                        self.ray_paths_x[i, j, 0:ray_len] = ray_x
+                        self.ray_paths_y[i, j, 0:ray_len] = ray_y
+                        self.ray_len[i, j] = ray_len
+            except Exception as e:
+                errors.append(e)
+
+        if len(devices) == 1:
+            trace(devices[0])
+        else:
+            th = [threading.Thread(target=trace, args=(d,)) for d in devices]
+            for t_ in th:
+                t_.start()
+            for t_ in th:
+                t_.join()
+        for d in devices:
+            self._ctx(d).release_fields()
+        if errors:
+            raise errors[0]
+        return times
+
+    def find_all_TTF_rays(self, veln, velpn, vel_map=None, subgrid_size=9, trans_pairs=None, stif_den=None,
+                          save_rays=True):
+        """Receiver fields + rays for all transducer pairs (reference :4258-4364); returns times (n, n)."""
+        if type(vel_map) == type(None):
+            vel_map = np.ones(veln.shape)
+        if type(stif_den) == type(None):
+            stif_den = np.zeros((veln.shape[0], veln.shape[1], 5), dtype=np.int64)
+        return self._rays(veln, velpn, vel_map, stif_den, subgrid_size, trans_pairs, save_rays, 1, False)
+
+    def find_all_TTF_rays_parallel(self, veln, velpn, vel_map=None, subgrid_size=9, trans_pairs=None, stif_den=None,
+                                   n_threads=2, save_rays=True):
+        """As find_all_TTF_rays over min(n_threads, #GPUs) GPUs (reference :4550-4685).
+
+        Like the reference: ValueError for n_threads == 1, and pairs (j, j) are traced when
+        trans_pairs[j, j] == 1.  Subgrid-1 fields use travel() semantics (SURVEY B-D4)."""
+        if n_threads == 1:
+            raise ValueError("n_threads should not equal one. Use find_all_TTF_rays for single process.")
+        if type(vel_map) == type(None):
+            vel_map = np.ones(veln.shape)
+        if type(stif_den) == type(None):
+            stif_den = np.zeros((veln.shape[0], veln.shape[1], 5), dtype=np.int64)
+        return self._rays(veln, velpn, vel_map, stif_den, subgrid_size, trans_pairs, save_rays, n_threads, True)
+
+    def ray_path(self, i, j):
+        """Ray (i, j) from the last find_all_TTF_rays* call (reference :4687-4705)."""
+        if self.ray_len[i, j] == 0:
+            print("Ray path has not been calculated")
+            return None, None
+        ray_len = self.ray_len[i, j]
+        return self.ray_paths_x[i, j, 0:ray_len], self.ray_paths_y[i, j, 0:ray_len]

@@ -1,0 +1,251 @@
+"""ctypes binding of libalifmm.so (include/alifmm.h) — the MI355X hot path.
+
+The library is built in-tree (csrc/Makefile -> lib/libalifmm.so).  There is no CPU fallback:
+if the library or a GPU is missing, every entry point raises AlifmmError.
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libalifmm.so")
+
+_d, _i, _l, _p = ctypes.c_double, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p
+_lib = None
+_lock = threading.Lock()
+
+
+class AlifmmError(RuntimeError):
+    pass
+
+
+def _load():
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise AlifmmError("libalifmm.so not built (%s); run `make -C %s/csrc` or __graft_entry__.build()"
+                              % (LIB_PATH, HERE))
+        L = ctypes.CDLL(LIB_PATH)
+        sig = {
+            "alifmm_version": (ctypes.c_char_p, []),
+            "alifmm_device_count": (_i, [_p]),
+            "alifmm_ctx_create": (_i, [_i, _p]),
+            "alifmm_ctx_destroy": (_i, [_p]),
+            "alifmm_last_error": (ctypes.c_char_p, [_p]),
+            "alifmm_set_model": (_i, [_p, _i, _i, _p, _p, _p, _p, _p, _p, _i, _d, _d, _d, _d]),
+            "alifmm_set_option": (_i, [_p, ctypes.c_char_p, _d]),
+            "alifmm_field_shape": (_i, [_p, _i, _p, _p]),
+            "alifmm_travel": (_i, [_p, _i, _i, _p, _p, _i, _p]),
+            "alifmm_get_field": (_i, [_p, _i, _p]),
+            "alifmm_release_fields": (_i, [_p]),
+            "alifmm_find_rays": (_i, [_p, _i, _p, _p, _p, _p, _p, _p, _p, _l]),
+            "alifmm_source_stats": (_i, [_p, _i, _p, _p]),
+            "alifmm_last_timing": (_i, [_p, _p, _p, _p]),
+            "alifmm_put_field": (_i, [_p, _i, _i, _p]),
+            "alifmm_time_between_points": (_i, [_p, _i, _p, _p, _p, _p, _i, _p]),
+            "alifmm_local_ops": (_i, [_p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i,
+                                      _p]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+        return L
+
+
+def lib():
+    return _load()
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    lib().alifmm_device_count(ctypes.byref(n))
+    return n.value
+
+
+def _c64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def _ci64(a):
+    return np.ascontiguousarray(a, dtype=np.int64)
+
+
+def _ci32(a):
+    return np.ascontiguousarray(a, dtype=np.int32)
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+class Context:
+    """One GPU (HIP device index).  Holds the resident model and travel-time fields."""
+
+    def __init__(self, device=0, cdelta=None, r0=None, batch=None):
+        L = lib()
+        h = ctypes.c_void_p()
+        rc = L.alifmm_ctx_create(int(device), ctypes.byref(h))
+        if rc != 0 or not h.value:
+            raise AlifmmError("alifmm_ctx_create(device=%d) failed (rc=%d): no usable MI355X/HIP device"
+                              % (device, rc))
+        self._h = h
+        self.device = device
+        self._model_key = None
+        self.shape = None
+        for k, v in (("cdelta", cdelta), ("r0", r0), ("batch", batch)):
+            if v is not None:
+                self.set_option(k, v)
+
+    def _chk(self, rc, what):
+        if rc != 0:
+            msg = lib().alifmm_last_error(self._h)
+            raise AlifmmError("%s failed (rc=%d): %s" % (what, rc, msg.decode() if msg else ""))
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            lib().alifmm_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_option(self, name, value):
+        self._chk(lib().alifmm_set_option(self._h, name.encode(), float(value)), "set_option(%s)" % name)
+
+    def set_model(self, veln, velpn, vel_map, stif_den, group_tab, phase_tab, dnx, dnz=None, gox=0.0, goz=0.0,
+                  key=None):
+        """Upload the model unless `key` equals the key of the resident model."""
+        if key is not None and key == self._model_key:
+            return
+        veln = _c64(veln)
+        nnz, nnx = veln.shape
+        velpn = _ci64(velpn)
+        vel_map = _c64(vel_map)
+        stif = None if stif_den is None else _ci64(stif_den)
+        gt = _c64(group_tab)
+        pt = _c64(phase_tab if phase_tab is not None else group_tab)
+        if velpn.shape != veln.shape or vel_map.shape != veln.shape:
+            raise ValueError("veln, velpn and vel_map must have the same shape")
+        if stif is not None and stif.shape != (nnz, nnx, 5):
+            raise ValueError("stif_den must have shape (nnz, nnx, 5)")
+        if gt.ndim != 2 or gt.shape[0] != 361 or pt.shape != gt.shape:
+            raise ValueError("velocity tables must have shape (361, ncol)")
+        dnz = dnx if dnz is None else dnz
+        self._chk(lib().alifmm_set_model(self._h, nnz, nnx, _ptr(veln), _ptr(velpn), _ptr(vel_map), _ptr(stif),
+                                         _ptr(gt), _ptr(pt), gt.shape[1], float(dnx), float(dnz), float(gox),
+                                         float(goz)), "set_model")
+        self._model_key = key
+        self.shape = (nnz, nnx)
+
+    def field_shape(self, subgrid):
+        a, b = ctypes.c_int(0), ctypes.c_int(0)
+        self._chk(lib().alifmm_field_shape(self._h, int(subgrid), ctypes.byref(a), ctypes.byref(b)), "field_shape")
+        return a.value, b.value
+
+    def travel(self, scx, scz, subgrid=1, first_slot=0, copy_out=True):
+        """Travel-time fields for sources (scx, scz) [m]; resident in slots first_slot.. ."""
+        scx = _c64(np.atleast_1d(scx))
+        scz = _c64(np.atleast_1d(scz))
+        fz, fx = self.field_shape(subgrid)
+        out = np.empty((len(scx), fz, fx)) if copy_out else None
+        self._chk(lib().alifmm_travel(self._h, int(subgrid), len(scx), _ptr(scx), _ptr(scz), int(first_slot),
+                                      _ptr(out)), "travel")
+        return out
+
+    def get_field(self, slot, subgrid):
+        fz, fx = self.field_shape(subgrid)
+        out = np.empty((fz, fx))
+        self._chk(lib().alifmm_get_field(self._h, int(slot), _ptr(out)), "get_field")
+        return out
+
+    def put_field(self, slot, subgrid, data):
+        data = _c64(data)
+        if data.shape != self.field_shape(subgrid):
+            raise ValueError("field shape %s does not match subgrid %d" % (data.shape, subgrid))
+        self._chk(lib().alifmm_put_field(self._h, int(slot), int(subgrid), _ptr(data)), "put_field")
+
+    def release_fields(self):
+        self._chk(lib().alifmm_release_fields(self._h), "release_fields")
+
+    def find_rays(self, slots, src_xy, rec_xy, with_points=True):
+        """Rays through resident receiver fields; returns (times, lens, flags, list of (x, z) arrays)."""
+        slots = _ci32(slots)
+        n = len(slots)
+        src_xy = _c64(src_xy).reshape(n, 2)
+        rec_xy = _c64(rec_xy).reshape(n, 2)
+        times = np.zeros(n)
+        lens = np.zeros(n, dtype=np.int32)
+        flags = np.zeros(n, dtype=np.int32)
+        cap = 0
+        pts = None
+        if with_points and n:
+            nnz, nnx = self.shape
+            cap = n * 5 * (nnz + nnx)
+            pts = np.empty(2 * cap)
+        self._chk(lib().alifmm_find_rays(self._h, n, _ptr(slots), _ptr(src_xy), _ptr(rec_xy), _ptr(times),
+                                         _ptr(lens), _ptr(flags), _ptr(pts), cap), "find_rays")
+        rays = None
+        if with_points:
+            rays = []
+            off = 0
+            for k in range(n):
+                p = pts[2 * off:2 * (off + lens[k])].reshape(-1, 2)
+                rays.append((p[:, 0].copy(), p[:, 1].copy()))
+                off += lens[k]
+        return times, lens, flags, rays
+
+    def source_stats(self, slot):
+        steps = np.zeros(4, dtype=np.int64)
+        sw = ctypes.c_int64(0)
+        self._chk(lib().alifmm_source_stats(self._h, int(slot), _ptr(steps), ctypes.byref(sw)), "source_stats")
+        return steps, sw.value
+
+    def last_timing(self):
+        a, b, c = ctypes.c_double(0), ctypes.c_double(0), ctypes.c_double(0)
+        self._chk(lib().alifmm_last_timing(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)),
+                  "last_timing")
+        return a.value, b.value, c.value
+
+    def time_between_points(self, x1, x2, y1, y2, subgrid):
+        x1, x2, y1, y2 = (_c64(np.atleast_1d(v)) for v in (x1, x2, y1, y2))
+        out = np.empty(len(x1))
+        self._chk(lib().alifmm_time_between_points(self._h, len(x1), _ptr(x1), _ptr(x2), _ptr(y1), _ptr(y2),
+                                                   int(subgrid), _ptr(out)), "time_between_points")
+        return out
+
+    def local_ops(self, op, ttn, nsts, iz, ix, dnx, dnz, nnz_arg, nnx_arg, cveln, cvelpn, cvm, cstif, tab):
+        """Batched update() (op 0) / fouds18_A() (op 1) on (n, pz, px) patches."""
+        ttn = _c64(ttn)
+        n, pz, px = ttn.shape
+        nsts = _ci32(nsts)
+        out = np.empty(n)
+        tab = _c64(tab)
+        cst = None if cstif is None else _ci64(cstif).reshape(n, 5)
+        args = [_ci32(iz), _ci32(ix), _c64(dnx), _c64(dnz), _ci32(nnz_arg), _ci32(nnx_arg), _c64(cveln),
+                _ci64(cvelpn), _c64(cvm)]
+        self._chk(lib().alifmm_local_ops(self._h, int(op), n, pz, px, _ptr(ttn), _ptr(nsts), *[_ptr(a) for a in args],
+                                         _ptr(cst), _ptr(tab), tab.shape[1], _ptr(out)), "local_ops")
+        return out
+
+
+_default = {}
+
+
+def default_context(device=0):
+    """Process-wide context per device (created on first use)."""
+    with _lock:
+        ctx = _default.get(device)
+    if ctx is None:
+        ctx = Context(device)
+        with _lock:
+            _default[device] = ctx
+    return ctx

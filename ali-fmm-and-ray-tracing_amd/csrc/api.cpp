@@ -1,0 +1,773 @@
+// api.cpp — host runtime behind include/alifmm.h (HIP, one context per GPU).
+//
+// Owns the HBM-resident model, the per-source work arena (status grid + band work lists) and
+// the resident travel-time fields that the ray tracer reads without a host round trip.
+// Sources are processed in chunks of `batch` (one persistent workgroup per source).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <array>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/alifmm.h"
+#include "kernels.h"
+
+namespace {
+
+struct Field {
+  double* d = nullptr;
+  size_t bytes = 0;
+  int sg = 0, nz = 0, nx = 0;
+  int64_t steps[4] = {0, 0, 0, 0};
+  int64_t sweeps = 0;
+};
+
+struct Arena {  // per-chunk scratch, reused across calls
+  int nsrc = 0;
+  long cells = 0, capL = 0, capC = 0, capS = 0;
+  int* S = nullptr;
+  int* lists = nullptr;  // L0 | L1 | A | C per source
+  double* V = nullptr;
+  double* Ts = nullptr;  // stage grids (travel_finer_grid), 2 per source
+  int* Ss = nullptr;
+  af::BandSrc* srcs = nullptr;
+  af::HandoverOut* ho = nullptr;
+  af::InitJob* jobs = nullptr;
+  double* dscx = nullptr;
+  double* dscz = nullptr;
+};
+
+}  // namespace
+
+struct alifmm_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  std::string err;
+  // model
+  bool have_model = false;
+  int nz0 = 0, nx0 = 0, ncol = 0;
+  double dnx = 0, dnz = 0, gox = 0, goz = 0, vmax = 0;
+  double* d_veln = nullptr;
+  double* d_vm = nullptr;
+  int* d_velpn = nullptr;
+  int* d_sidx = nullptr;
+  double* d_stab = nullptr;
+  double* d_gtab = nullptr;
+  double* d_ptab = nullptr;
+  // options
+  double cdelta = 0.5, r0 = 40.0;
+  int exact_r = 40;
+  int batch = 256;
+  long cap_scale = 1;
+  // state
+  std::vector<Field> fields;
+  Arena arena;
+  double t_init = 0, t_band = 0, t_total = 0;
+};
+
+static int fail(alifmm_ctx* c, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (c) c->err = buf;
+  return code;
+}
+
+#define HIPCHK(call)                                                                          \
+  do {                                                                                        \
+    hipError_t e_ = (call);                                                                   \
+    if (e_ != hipSuccess) return fail(ctx, ALIFMM_E_HIP, "%s: %s", #call, hipGetErrorString(e_)); \
+  } while (0)
+
+template <class T>
+static hipError_t dalloc(T** p, size_t n) {
+  return hipMalloc((void**)p, std::max<size_t>(n, 1) * sizeof(T));
+}
+static void dfree(void* p) {
+  if (p) (void)hipFree(p);
+}
+
+static void free_arena(Arena& a) {
+  dfree(a.S); dfree(a.lists); dfree(a.V); dfree(a.Ts); dfree(a.Ss); dfree(a.srcs); dfree(a.ho); dfree(a.jobs);
+  dfree(a.dscx); dfree(a.dscz);
+  a = Arena();
+}
+
+// ---- host-side velocity maximum (for the band width) ----
+static double pymod(double a, double b) {
+  double m = std::fmod(a, b);
+  if (m != 0.0) {
+    if ((b < 0) != (m < 0)) m += b;
+  } else {
+    m = std::copysign(0.0, b);
+  }
+  return m;
+}
+static double christoffel_group_host(const double* s, double eff, double vm) {
+  double e90 = pymod(eff, 90);
+  if (e90 < 0.01 || e90 > 90 - 0.01) {
+    double lam = (std::fabs(pymod(eff, 180) - 90) < 1) ? s[2] : s[0];
+    return 1000 * vm * std::sqrt(lam / s[4]);
+  }
+  double tan_ang = std::tan(eff * M_PI / 180.0);
+  double A = s[0] + s[2] - 2 * s[3], B = (s[1] + s[3]) * (tan_ang - 1 / tan_ang), C = s[0] - s[2];
+  double disc = B * B + A * A - C * C;
+  double pa = eff < 90 ? pymod(std::atan((-B - std::sqrt(disc)) / (C - A)), M_PI)
+                       : pymod(std::atan((-B + std::sqrt(disc)) / (C - A)), M_PI);
+  double lam = 0.5 * (std::cos(2 * pa) * (s[0] - s[3]) + std::sin(2 * pa) * (s[1] + s[3]) * tan_ang + s[0] + s[3]);
+  return 1000 * vm * std::sqrt(lam / s[4]) / std::cos(eff * M_PI / 180.0 - pa);
+}
+
+extern "C" {
+
+const char* alifmm_version(void) { return "alifmm-mi355x 0.1 (gfx950)"; }
+
+int alifmm_device_count(int* n) {
+  int k = 0;
+  hipError_t e = hipGetDeviceCount(&k);
+  if (e != hipSuccess) k = 0;
+  *n = k;
+  return e == hipSuccess ? ALIFMM_OK : ALIFMM_E_HIP;
+}
+
+int alifmm_ctx_create(int device, alifmm_ctx** out) {
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return ALIFMM_E_HIP;
+  if (device < 0 || device >= n) return ALIFMM_E_ARG;
+  alifmm_ctx* ctx = new alifmm_ctx();
+  ctx->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete ctx;
+    return ALIFMM_E_HIP;
+  }
+  for (auto& e : ctx->ev) (void)hipEventCreate(&e);
+  *out = ctx;
+  return ALIFMM_OK;
+}
+
+static void free_model(alifmm_ctx* c) {
+  dfree(c->d_veln); dfree(c->d_vm); dfree(c->d_velpn); dfree(c->d_sidx); dfree(c->d_stab); dfree(c->d_gtab);
+  dfree(c->d_ptab);
+  c->d_veln = c->d_vm = c->d_stab = c->d_gtab = c->d_ptab = nullptr;
+  c->d_velpn = c->d_sidx = nullptr;
+  c->have_model = false;
+}
+
+int alifmm_release_fields(alifmm_ctx* ctx) {
+  if (!ctx) return ALIFMM_E_ARG;
+  (void)hipSetDevice(ctx->device);
+  for (auto& f : ctx->fields) dfree(f.d);
+  ctx->fields.clear();
+  return ALIFMM_OK;
+}
+
+int alifmm_ctx_destroy(alifmm_ctx* ctx) {
+  if (!ctx) return ALIFMM_OK;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  alifmm_release_fields(ctx);
+  free_arena(ctx->arena);
+  free_model(ctx);
+  for (auto& e : ctx->ev) if (e) (void)hipEventDestroy(e);
+  (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return ALIFMM_OK;
+}
+
+const char* alifmm_last_error(alifmm_ctx* ctx) { return ctx ? ctx->err.c_str() : "no context"; }
+
+int alifmm_set_option(alifmm_ctx* ctx, const char* name, double value) {
+  if (!ctx || !name) return ALIFMM_E_ARG;
+  if (!strcmp(name, "cdelta") && value > 0) ctx->cdelta = value;
+  else if (!strcmp(name, "r0") && value >= 0) ctx->r0 = value;
+  else if (!strcmp(name, "batch") && value >= 1) ctx->batch = (int)value;
+  else if (!strcmp(name, "exact_r") && value >= 0 && value <= 48) ctx->exact_r = (int)value;
+  else return fail(ctx, ALIFMM_E_ARG, "unknown option or bad value: %s=%g", name, value);
+  return ALIFMM_OK;
+}
+
+int alifmm_set_model(alifmm_ctx* ctx, int nnz, int nnx, const double* veln, const int64_t* velpn,
+                     const double* vel_map, const int64_t* stif_den, const double* group_tab,
+                     const double* phase_tab, int ncol, double dnx, double dnz, double gox, double goz) {
+  if (!ctx || nnz < 2 || nnx < 2 || !veln || !velpn || !vel_map || !group_tab || !phase_tab || ncol < 1)
+    return fail(ctx, ALIFMM_E_ARG, "set_model: bad arguments");
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  free_model(ctx);
+  const size_t n = (size_t)nnz * nnx;
+  std::vector<int> vp(n);
+  for (size_t i = 0; i < n; i++) {
+    if (velpn[i] < 0 || velpn[i] >= ncol) return fail(ctx, ALIFMM_E_ARG, "velpn[%zu]=%lld outside the table", i,
+                                                      (long long)velpn[i]);
+    vp[i] = (int)velpn[i];
+  }
+  // unique stiffness rows
+  std::vector<int> sidx;
+  std::vector<double> stab;
+  if (stif_den) {
+    sidx.resize(n);
+    std::map<std::array<int64_t, 5>, int> uniq;
+    std::array<int64_t, 5> last{};
+    int last_id = -1;
+    for (size_t i = 0; i < n; i++) {
+      std::array<int64_t, 5> row;
+      for (int k = 0; k < 5; k++) row[k] = stif_den[5 * i + k];
+      if (last_id >= 0 && row == last) {  // runs of equal rows: no map lookup
+        sidx[i] = last_id;
+        continue;
+      }
+      auto it = uniq.find(row);
+      int id;
+      if (it == uniq.end()) {
+        id = (int)uniq.size();
+        uniq.emplace(row, id);
+        for (int k = 0; k < 5; k++) stab.push_back((double)row[k]);
+      } else {
+        id = it->second;
+      }
+      sidx[i] = id;
+      last = row;
+      last_id = id;
+    }
+  }
+  // maximum group velocity over the model (band width scale)
+  double vmax = 0;
+  {
+    std::vector<double> colmax(ncol, 0.0);
+    for (int c = 0; c < ncol; c++)
+      for (int a = 0; a <= 180; a++) colmax[c] = std::max(colmax[c], group_tab[a * ncol + c]);
+    const int nrow = (int)stab.size() / 5;
+    std::vector<double> rowmax(nrow, 0.0);
+    for (int r = 0; r < nrow; r++)
+      for (int k = 0; k <= 3600; k++)
+        rowmax[r] = std::max(rowmax[r], christoffel_group_host(&stab[5 * r], 0.05 * k, 1.0));
+    for (size_t i = 0; i < n; i++) {
+      double v = (vp[i] != 0 || !stif_den) ? colmax[vp[i]] * vel_map[i] : rowmax[sidx[i]] * vel_map[i];
+      if (std::isfinite(v)) vmax = std::max(vmax, v);
+    }
+  }
+  if (!(vmax > 0)) return fail(ctx, ALIFMM_E_ARG, "model has no positive velocity");
+  HIPCHK(dalloc(&ctx->d_veln, n));
+  HIPCHK(dalloc(&ctx->d_vm, n));
+  HIPCHK(dalloc(&ctx->d_velpn, n));
+  HIPCHK(dalloc(&ctx->d_gtab, (size_t)361 * ncol));
+  HIPCHK(dalloc(&ctx->d_ptab, (size_t)361 * ncol));
+  HIPCHK(hipMemcpy(ctx->d_veln, veln, n * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(ctx->d_vm, vel_map, n * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(ctx->d_velpn, vp.data(), n * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(ctx->d_gtab, group_tab, (size_t)361 * ncol * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(ctx->d_ptab, phase_tab, (size_t)361 * ncol * 8, hipMemcpyHostToDevice));
+  if (stif_den) {
+    HIPCHK(dalloc(&ctx->d_sidx, n));
+    HIPCHK(dalloc(&ctx->d_stab, stab.size()));
+    HIPCHK(hipMemcpy(ctx->d_sidx, sidx.data(), n * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(ctx->d_stab, stab.data(), stab.size() * 8, hipMemcpyHostToDevice));
+  }
+  ctx->nz0 = nnz;
+  ctx->nx0 = nnx;
+  ctx->ncol = ncol;
+  ctx->dnx = dnx;
+  ctx->dnz = dnz;
+  ctx->gox = gox;
+  ctx->goz = goz;
+  ctx->vmax = vmax;
+  ctx->have_model = true;
+  return ALIFMM_OK;
+}
+
+int alifmm_field_shape(alifmm_ctx* ctx, int subgrid, int* fnz, int* fnx) {
+  if (!ctx || !ctx->have_model || subgrid < 1 || subgrid % 2 == 0)
+    return fail(ctx, ALIFMM_E_ARG, "field_shape: no model or even subgrid %d", subgrid);
+  *fnz = subgrid * (ctx->nz0 - 1) + 1;
+  *fnx = subgrid * (ctx->nx0 - 1) + 1;
+  return ALIFMM_OK;
+}
+
+static af::DevModel dev_model(const alifmm_ctx* c) {
+  af::DevModel M;
+  M.nz0 = c->nz0;
+  M.nx0 = c->nx0;
+  M.veln = c->d_veln;
+  M.velpn = c->d_velpn;
+  M.vm = c->d_vm;
+  M.sidx = c->d_sidx;
+  M.stab = c->d_stab;
+  M.gtab = c->d_gtab;
+  M.ptab = c->d_ptab;
+  M.ncol = c->ncol;
+  return M;
+}
+
+static int ensure_arena(alifmm_ctx* ctx, int nsrc, long cells, long capL, long capC, long capS) {
+  Arena& a = ctx->arena;
+  if (a.nsrc >= nsrc && a.cells >= cells && a.capL >= capL && a.capC >= capC && a.capS >= capS) return ALIFMM_OK;
+  free_arena(a);
+  a.nsrc = nsrc;
+  a.cells = cells;
+  a.capL = capL;
+  a.capC = capC;
+  a.capS = capS;
+  HIPCHK(dalloc(&a.S, (size_t)nsrc * cells));
+  HIPCHK(dalloc(&a.lists, (size_t)nsrc * (3 * capL + capC)));
+  HIPCHK(dalloc(&a.V, (size_t)nsrc * capC));
+  if (capS > 0) {
+    HIPCHK(dalloc(&a.Ts, (size_t)nsrc * 2 * capS));
+    HIPCHK(dalloc(&a.Ss, (size_t)nsrc * 2 * capS));
+  }
+  HIPCHK(dalloc(&a.srcs, nsrc));
+  HIPCHK(dalloc(&a.ho, nsrc));
+  HIPCHK(dalloc(&a.jobs, nsrc));
+  HIPCHK(dalloc(&a.dscx, nsrc));
+  HIPCHK(dalloc(&a.dscz, nsrc));
+  return ALIFMM_OK;
+}
+
+static int ensure_field(alifmm_ctx* ctx, int slot, int sg, int fz, int fx) {
+  if ((int)ctx->fields.size() <= slot) ctx->fields.resize(slot + 1);
+  Field& f = ctx->fields[slot];
+  size_t bytes = (size_t)fz * fx * sizeof(double);
+  if (f.d && f.bytes != bytes) {
+    dfree(f.d);
+    f.d = nullptr;
+  }
+  if (!f.d) {
+    HIPCHK(hipMalloc((void**)&f.d, bytes));
+    f.bytes = bytes;
+  }
+  f.sg = sg;
+  f.nz = fz;
+  f.nx = fx;
+  return ALIFMM_OK;
+}
+
+// one chunk of sources; returns ALIFMM_E_CAPACITY when a work list overflowed
+static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const double* scz, int first_slot, int fz,
+                        int fx, float* ms_init, float* ms_band) {
+  const long cells = (long)fz * fx;
+  long capL = std::min(cells, std::max(65536L, cells / 8) * ctx->cap_scale);
+  long capC = capL;
+  long capS = 0;
+  if (sg > 1) {
+    long s1 = 9L * 2 * (2L * sg + (sg - 1) / 2) + 1;             // stage-1 grid side (x9)
+    long s2 = 3L * 2 * (2L * sg + (sg - 1) / 2 + 3L * sg) + 1;  // stage-2 grid side (x3)
+    capS = std::max(s1 * s1, s2 * s2);
+    capL = std::max(capL, std::min(capS, 262144L));
+    capC = capL;
+  }
+  int rc = ensure_arena(ctx, std::max(n, std::min(ctx->batch, 1)), cells, capL, capC, capS);
+  if (rc) return rc;
+  Arena& a = ctx->arena;
+  std::vector<af::BandSrc> hs(n);
+  for (int i = 0; i < n; i++) {
+    int slot = first_slot + i;
+    if ((rc = ensure_field(ctx, slot, sg, fz, fx))) return rc;
+    af::BandSrc& b = hs[i];
+    memset(&b, 0, sizeof b);
+    b.T = ctx->fields[slot].d;
+    b.S = a.S + (size_t)i * a.cells;
+    int* base = a.lists + (size_t)i * (3 * a.capL + a.capC);
+    b.L0 = base;
+    b.L1 = base + a.capL;
+    b.A = base + 2 * a.capL;
+    b.C = base + 3 * a.capL;
+    b.V = a.V + (size_t)i * a.capC;
+    if (capS > 0) {
+      b.Ts[0] = a.Ts + (size_t)i * 2 * a.capS;
+      b.Ts[1] = b.Ts[0] + a.capS;
+      b.Ss[0] = a.Ss + (size_t)i * 2 * a.capS;
+      b.Ss[1] = b.Ss[0] + a.capS;
+    }
+    HIPCHK(hipMemsetAsync(b.T, 0, (size_t)cells * 8, ctx->stream));
+    HIPCHK(hipMemsetAsync(b.S, 0xFF, (size_t)cells * 4, ctx->stream));  // kFar = -1
+  }
+  HIPCHK(hipMemcpyAsync(a.srcs, hs.data(), sizeof(af::BandSrc) * n, hipMemcpyHostToDevice, ctx->stream));
+  af::DevModel M = dev_model(ctx);
+  af::BandParams P;
+  memset(&P, 0, sizeof P);
+  P.M = M;
+  P.nsrc = n;
+  P.sg = sg;
+  P.nz = fz;
+  P.nx = fx;
+  P.dnx = ctx->dnx;
+  P.dnz = ctx->dnz;
+  P.cdelta = ctx->cdelta;
+  P.vmax = ctx->vmax;
+  P.r0 = ctx->r0;
+  P.capL = (int)capL;
+  P.capC = (int)capC;
+  P.capS = (int)capS;
+  P.src = a.srcs;
+  P.gox = ctx->gox;
+  P.goz = ctx->goz;
+  HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
+  if (sg == 1) {
+    std::vector<af::InitJob> jobs(n);
+    for (int i = 0; i < n; i++) {
+      jobs[i].isx = (long)std::nearbyint((scx[i] - ctx->gox) / ctx->dnx);
+      jobs[i].isz = (long)std::nearbyint((scz[i] - ctx->goz) / ctx->dnz);
+      jobs[i].dnx = ctx->dnx;
+      jobs[i].dnz = ctx->dnz;
+      jobs[i].exact_r = ctx->exact_r;
+      jobs[i].tstop = ctx->exact_r * ctx->dnx / ctx->vmax;
+      if (jobs[i].isx < 0 || jobs[i].isx >= ctx->nx0 || jobs[i].isz < 0 || jobs[i].isz >= ctx->nz0)
+        return fail(ctx, ALIFMM_E_ARG, "source %d (%g, %g) outside the grid", i, scx[i], scz[i]);
+    }
+    HIPCHK(hipMemcpyAsync(a.jobs, jobs.data(), sizeof(af::InitJob) * n, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(af_launch_init(&M, a.jobs, n, a.ho, ctx->stream));
+    P.mode = 0;
+    P.ho = a.ho;
+  } else {
+    for (int i = 0; i < n; i++) {
+      long ix = (long)std::nearbyint((scx[i] - ctx->gox) / ctx->dnx), iz = (long)std::nearbyint((scz[i] - ctx->goz) / ctx->dnz);
+      if (ix < 0 || ix >= ctx->nx0 || iz < 0 || iz >= ctx->nz0)
+        return fail(ctx, ALIFMM_E_ARG, "source %d (%g, %g) outside the grid", i, scx[i], scz[i]);
+    }
+    HIPCHK(hipMemcpyAsync(a.dscx, scx, 8 * n, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipMemcpyAsync(a.dscz, scz, 8 * n, hipMemcpyHostToDevice, ctx->stream));
+    P.mode = 1;
+    P.scx = a.dscx;
+    P.scz = a.dscz;
+  }
+  HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
+  HIPCHK(af_launch_band(&P, ctx->stream));
+  HIPCHK(hipEventRecord(ctx->ev[2], ctx->stream));
+  if (sg > 1)
+    for (int i = 0; i < n; i++) HIPCHK(af_launch_scale(hs[i].T, cells, (double)sg, ctx->stream));
+  HIPCHK(hipMemcpyAsync(hs.data(), a.srcs, sizeof(af::BandSrc) * n, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  float t1 = 0, t2 = 0;
+  (void)hipEventElapsedTime(&t1, ctx->ev[0], ctx->ev[1]);
+  (void)hipEventElapsedTime(&t2, ctx->ev[1], ctx->ev[2]);
+  *ms_init += t1;
+  *ms_band += t2;
+  int cap_err = 0;
+  for (int i = 0; i < n; i++) {
+    Field& f = ctx->fields[first_slot + i];
+    for (int k = 0; k < 4; k++) f.steps[k] = hs[i].steps[k];
+    f.sweeps = hs[i].nupd;
+    if (hs[i].err == 2) cap_err = 1;
+    else if (hs[i].err == 3) return fail(ctx, ALIFMM_E_KERNEL, "source %d: init heap overflow", i);
+    else if (hs[i].err == 4) return fail(ctx, ALIFMM_E_KERNEL, "source %d: stage grid capacity", i);
+    else if (hs[i].err) return fail(ctx, ALIFMM_E_KERNEL, "source %d: kernel error %d", i, hs[i].err);
+  }
+  if (cap_err) return fail(ctx, ALIFMM_E_CAPACITY, "work-list capacity %ld exceeded", capL);
+  return ALIFMM_OK;
+}
+
+int alifmm_travel(alifmm_ctx* ctx, int subgrid, int nsrc, const double* scx, const double* scz, int first_slot,
+                  double* out) {
+  if (!ctx || !ctx->have_model) return fail(ctx, ALIFMM_E_ARG, "travel: no model");
+  if (subgrid < 1 || subgrid % 2 == 0) return fail(ctx, ALIFMM_E_ARG, "travel: subgrid must be odd, got %d", subgrid);
+  if (nsrc < 0 || first_slot < 0 || (nsrc > 0 && (!scx || !scz))) return fail(ctx, ALIFMM_E_ARG, "travel: bad args");
+  HIPCHK(hipSetDevice(ctx->device));
+  int fz, fx;
+  alifmm_field_shape(ctx, subgrid, &fz, &fx);
+  const long cells = (long)fz * fx;
+  float ms_init = 0, ms_band = 0;
+  HIPCHK(hipEventRecord(ctx->ev[3], ctx->stream));
+  hipEvent_t t_begin;
+  HIPCHK(hipEventCreate(&t_begin));
+  HIPCHK(hipEventRecord(t_begin, ctx->stream));
+  for (int s0 = 0; s0 < nsrc; s0 += ctx->batch) {
+    int n = std::min(ctx->batch, nsrc - s0);
+    int rc;
+    for (int attempt = 0;; attempt++) {
+      rc = travel_chunk(ctx, subgrid, n, scx + s0, scz + s0, first_slot + s0, fz, fx, &ms_init, &ms_band);
+      if (rc != ALIFMM_E_CAPACITY || ctx->cap_scale * 4 > 64) break;
+      ctx->cap_scale *= 4;  // retry the chunk with larger work lists
+    }
+    if (rc) {
+      (void)hipEventDestroy(t_begin);
+      return rc;
+    }
+    if (out) {
+      for (int i = 0; i < n; i++)
+        HIPCHK(hipMemcpyAsync(out + (size_t)(s0 + i) * cells, ctx->fields[first_slot + s0 + i].d, (size_t)cells * 8,
+                              hipMemcpyDeviceToHost, ctx->stream));
+    }
+  }
+  hipEvent_t t_end;
+  HIPCHK(hipEventCreate(&t_end));
+  HIPCHK(hipEventRecord(t_end, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  float tot = 0;
+  (void)hipEventElapsedTime(&tot, t_begin, t_end);
+  (void)hipEventDestroy(t_begin);
+  (void)hipEventDestroy(t_end);
+  ctx->t_init = ms_init;
+  ctx->t_band = ms_band;
+  ctx->t_total = tot;
+  return ALIFMM_OK;
+}
+
+int alifmm_get_field(alifmm_ctx* ctx, int slot, double* out) {
+  if (!ctx || slot < 0 || slot >= (int)ctx->fields.size() || !ctx->fields[slot].d || !out)
+    return fail(ctx, ALIFMM_E_ARG, "get_field: no field in slot %d", slot);
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(hipMemcpyAsync(out, ctx->fields[slot].d, ctx->fields[slot].bytes, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return ALIFMM_OK;
+}
+
+int alifmm_source_stats(alifmm_ctx* ctx, int slot, int64_t* steps4, int64_t* cell_sweeps) {
+  if (!ctx || slot < 0 || slot >= (int)ctx->fields.size()) return fail(ctx, ALIFMM_E_ARG, "stats: bad slot");
+  if (steps4)
+    for (int k = 0; k < 4; k++) steps4[k] = ctx->fields[slot].steps[k];
+  if (cell_sweeps) *cell_sweeps = ctx->fields[slot].sweeps;
+  return ALIFMM_OK;
+}
+
+int alifmm_last_timing(alifmm_ctx* ctx, double* init_ms, double* band_ms, double* total_ms) {
+  if (!ctx) return ALIFMM_E_ARG;
+  if (init_ms) *init_ms = ctx->t_init;
+  if (band_ms) *band_ms = ctx->t_band;
+  if (total_ms) *total_ms = ctx->t_total;
+  return ALIFMM_OK;
+}
+
+int alifmm_find_rays(alifmm_ctx* ctx, int npairs, const int32_t* field_slot, const double* src_xy,
+                     const double* rec_xy, double* times, int32_t* ray_len, int32_t* flags, double* ray_xy,
+                     int64_t ray_xy_cap) {
+  if (!ctx || !ctx->have_model) return fail(ctx, ALIFMM_E_ARG, "find_rays: no model");
+  if (npairs <= 0) return ALIFMM_OK;
+  HIPCHK(hipSetDevice(ctx->device));
+  const int max_pts = 5 * (ctx->nz0 + ctx->nx0);
+  // group rays by subgrid (one launch per subgrid size present)
+  std::map<int, std::vector<int>> by_sg;
+  for (int k = 0; k < npairs; k++) {
+    int s = field_slot[k];
+    if (s < 0 || s >= (int)ctx->fields.size() || !ctx->fields[s].d)
+      return fail(ctx, ALIFMM_E_ARG, "find_rays: ray %d refers to empty slot %d", k, s);
+    by_sg[ctx->fields[s].sg].push_back(k);
+  }
+  const int chunk = 8192;
+  double *d_rx = nullptr, *d_ry = nullptr, *d_t = nullptr, *d_packed = nullptr;
+  int *d_len = nullptr, *d_flags = nullptr;
+  af::RayJob* d_jobs = nullptr;
+  long long* d_off = nullptr;
+  int rc = ALIFMM_OK;
+  auto cleanup = [&]() {
+    dfree(d_rx); dfree(d_ry); dfree(d_t); dfree(d_len); dfree(d_flags); dfree(d_jobs); dfree(d_off); dfree(d_packed);
+  };
+#define RCHK(call)                                                                        \
+  do {                                                                                    \
+    hipError_t e_ = (call);                                                               \
+    if (e_ != hipSuccess) {                                                               \
+      cleanup();                                                                          \
+      return fail(ctx, ALIFMM_E_HIP, "%s: %s", #call, hipGetErrorString(e_));             \
+    }                                                                                     \
+  } while (0)
+  RCHK(dalloc(&d_rx, (size_t)chunk * max_pts));
+  RCHK(dalloc(&d_ry, (size_t)chunk * max_pts));
+  RCHK(dalloc(&d_t, chunk));
+  RCHK(dalloc(&d_len, chunk));
+  RCHK(dalloc(&d_flags, chunk));
+  RCHK(dalloc(&d_jobs, chunk));
+  RCHK(dalloc(&d_off, chunk));
+  std::vector<int64_t> offsets(npairs + 1, 0);
+  std::vector<int32_t> lens(npairs, 0);
+  std::vector<double> tms(npairs, 0.0);
+  std::vector<int32_t> flg(npairs, 0);
+  // pass 1: trace, lengths
+  struct Pending { std::vector<int> ids; };
+  std::vector<std::pair<int, std::vector<int>>> groups(by_sg.begin(), by_sg.end());
+  // Rays are traced chunk by chunk; packed points are written after lengths are known (pass 2 re-traces
+  // nothing: each chunk is packed right after its trace, at offsets relative to the ray order below).
+  std::vector<int> order;
+  for (auto& g : groups) order.insert(order.end(), g.second.begin(), g.second.end());
+  // offsets follow the caller's ray order; we first trace everything (times/lengths), packing each
+  // chunk into a host staging area keyed by ray id.
+  std::vector<std::vector<double>> staged(ray_xy ? npairs : 0);
+  for (auto& g : groups) {
+    const int sg = g.first;
+    const auto& ids = g.second;
+    const Field& f0 = ctx->fields[field_slot[ids[0]]];
+    for (size_t c0 = 0; c0 < ids.size(); c0 += chunk) {
+      int n = (int)std::min<size_t>(chunk, ids.size() - c0);
+      std::vector<af::RayJob> jobs(n);
+      for (int i = 0; i < n; i++) {
+        int k = ids[c0 + i];
+        const Field& f = ctx->fields[field_slot[k]];
+        jobs[i].ttf = f.d;
+        jobs[i].sx = src_xy[2 * k];
+        jobs[i].sy = src_xy[2 * k + 1];
+        jobs[i].rx = rec_xy[2 * k];
+        jobs[i].ry = rec_xy[2 * k + 1];
+        if (f.nz != f0.nz || f.nx != f0.nx) {
+          cleanup();
+          return fail(ctx, ALIFMM_E_ARG, "find_rays: mixed field shapes for subgrid %d", sg);
+        }
+      }
+      RCHK(hipMemcpyAsync(d_jobs, jobs.data(), sizeof(af::RayJob) * n, hipMemcpyHostToDevice, ctx->stream));
+      af::RayParams P;
+      memset(&P, 0, sizeof P);
+      P.M = dev_model(ctx);
+      P.fnz = f0.nz;
+      P.fnx = f0.nx;
+      P.sg = sg;
+      P.dnx = ctx->dnx;
+      P.nrays = n;
+      P.max_pts = max_pts;
+      P.jobs = d_jobs;
+      P.ray_x = d_rx;
+      P.ray_y = d_ry;
+      P.ray_len = d_len;
+      P.times = d_t;
+      P.flags = d_flags;
+      RCHK(af_launch_rays(&P, ctx->stream));
+      std::vector<double> t(n);
+      std::vector<int> l(n), fl(n);
+      RCHK(hipMemcpyAsync(t.data(), d_t, 8 * n, hipMemcpyDeviceToHost, ctx->stream));
+      RCHK(hipMemcpyAsync(l.data(), d_len, 4 * n, hipMemcpyDeviceToHost, ctx->stream));
+      RCHK(hipMemcpyAsync(fl.data(), d_flags, 4 * n, hipMemcpyDeviceToHost, ctx->stream));
+      RCHK(hipStreamSynchronize(ctx->stream));
+      for (int i = 0; i < n; i++) {
+        int k = ids[c0 + i];
+        tms[k] = t[i];
+        lens[k] = l[i];
+        flg[k] = fl[i];
+      }
+      if (ray_xy) {
+        std::vector<long long> off(n + 1, 0);
+        for (int i = 0; i < n; i++) off[i + 1] = off[i] + l[i];
+        dfree(d_packed);
+        d_packed = nullptr;
+        RCHK(dalloc(&d_packed, (size_t)2 * std::max<long long>(off[n], 1)));
+        RCHK(hipMemcpyAsync(d_off, off.data(), 8 * n, hipMemcpyHostToDevice, ctx->stream));
+        RCHK(af_launch_pack_rays(d_rx, d_ry, d_len, d_off, n, max_pts, d_packed, ctx->stream));
+        std::vector<double> packed(2 * off[n]);
+        RCHK(hipMemcpyAsync(packed.data(), d_packed, 16 * off[n], hipMemcpyDeviceToHost, ctx->stream));
+        RCHK(hipStreamSynchronize(ctx->stream));
+        for (int i = 0; i < n; i++)
+          staged[ids[c0 + i]].assign(packed.begin() + 2 * off[i], packed.begin() + 2 * off[i + 1]);
+      }
+    }
+  }
+  for (int k = 0; k < npairs; k++) offsets[k + 1] = offsets[k] + lens[k];
+  if (ray_xy && offsets[npairs] > ray_xy_cap) rc = fail(ctx, ALIFMM_E_ARG, "find_rays: ray_xy capacity %lld < %lld",
+                                                      (long long)ray_xy_cap, (long long)offsets[npairs]);
+  if (!rc) {
+    for (int k = 0; k < npairs; k++) {
+      times[k] = tms[k];
+      ray_len[k] = lens[k];
+      if (flags) flags[k] = flg[k];
+      if (ray_xy) std::copy(staged[k].begin(), staged[k].end(), ray_xy + 2 * offsets[k]);
+    }
+  }
+  cleanup();
+  return rc;
+}
+
+int alifmm_put_field(alifmm_ctx* ctx, int slot, int subgrid, const double* data) {
+  if (!ctx || !ctx->have_model || slot < 0 || !data) return fail(ctx, ALIFMM_E_ARG, "put_field: bad args");
+  int fz, fx;
+  int rc = alifmm_field_shape(ctx, subgrid, &fz, &fx);
+  if (rc) return rc;
+  HIPCHK(hipSetDevice(ctx->device));
+  if ((rc = ensure_field(ctx, slot, subgrid, fz, fx))) return rc;
+  HIPCHK(hipMemcpy(ctx->fields[slot].d, data, (size_t)fz * fx * 8, hipMemcpyHostToDevice));
+  return ALIFMM_OK;
+}
+
+int alifmm_time_between_points(alifmm_ctx* ctx, int n, const double* x1, const double* x2, const double* y1,
+                               const double* y2, int subgrid, double* out) {
+  if (!ctx || !ctx->have_model || n < 0 || subgrid < 1) return fail(ctx, ALIFMM_E_ARG, "time_between_points: bad args");
+  if (n == 0) return ALIFMM_OK;
+  HIPCHK(hipSetDevice(ctx->device));
+  double* d = nullptr;
+  HIPCHK(dalloc(&d, (size_t)5 * n));
+  hipError_t e = hipSuccess;
+  const double* src[4] = {x1, x2, y1, y2};
+  for (int k = 0; k < 4 && e == hipSuccess; k++) e = hipMemcpy(d + (size_t)k * n, src[k], 8 * (size_t)n, hipMemcpyHostToDevice);
+  af::DevModel M = dev_model(ctx);
+  if (e == hipSuccess) e = af_launch_tbp(&M, n, d, d + n, d + 2 * n, d + 3 * n, ctx->dnx, subgrid, d + 4 * n, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e == hipSuccess) e = hipMemcpy(out, d + 4 * (size_t)n, 8 * (size_t)n, hipMemcpyDeviceToHost);
+  dfree(d);
+  if (e != hipSuccess) return fail(ctx, ALIFMM_E_HIP, "time_between_points: %s", hipGetErrorString(e));
+  return ALIFMM_OK;
+}
+
+int alifmm_local_ops(alifmm_ctx* ctx, int op, int n, int pz, int px, const double* ttn, const int32_t* nsts,
+                     const int32_t* iz, const int32_t* ix, const double* dnx, const double* dnz, const int32_t* nnz_arg,
+                     const int32_t* nnx_arg, const double* cell_veln, const int64_t* cell_velpn, const double* cell_vm,
+                     const int64_t* cell_stif, const double* tab, int ncol, double* out) {
+  if (!ctx || (op != 0 && op != 1) || n < 0 || pz < 1 || px < 1 || ncol < 1)
+    return fail(ctx, ALIFMM_E_ARG, "local_ops: bad args");
+  if (n == 0) return ALIFMM_OK;
+  HIPCHK(hipSetDevice(ctx->device));
+  const size_t pn = (size_t)pz * px;
+  std::vector<int> vp(n);
+  for (int k = 0; k < n; k++) vp[k] = (int)cell_velpn[k];
+  std::vector<double> st;
+  if (cell_stif) {
+    st.resize((size_t)5 * n);
+    for (size_t k = 0; k < st.size(); k++) st[k] = (double)cell_stif[k];
+  }
+  // one device block: [ttn | cveln | cvm | dnx | dnz | tab | stif | out] doubles, [nsts | iz | ix | nnz | nnx | velpn] ints
+  size_t nd = pn * n + 4 * (size_t)n + 361 * (size_t)ncol + st.size() + n;
+  size_t ni = pn * n + 5 * (size_t)n;
+  double* dd = nullptr;
+  int* di = nullptr;
+  HIPCHK(dalloc(&dd, nd));
+  if (hipMalloc((void**)&di, ni * 4) != hipSuccess) {
+    dfree(dd);
+    return fail(ctx, ALIFMM_E_HIP, "local_ops: out of memory");
+  }
+  double* p = dd;
+  af::LocalOpsParams P;
+  memset(&P, 0, sizeof P);
+  P.op = op;
+  P.n = n;
+  P.pz = pz;
+  P.px = px;
+  hipError_t e = hipSuccess;
+  auto putd = [&](const double* h, size_t cnt) {
+    double* q = p;
+    if (e == hipSuccess && cnt) e = hipMemcpy(q, h, cnt * 8, hipMemcpyHostToDevice);
+    p += cnt;
+    return (const double*)q;
+  };
+  P.ttn = putd(ttn, pn * n);
+  P.cveln = putd(cell_veln, n);
+  P.cvm = putd(cell_vm, n);
+  P.dnx = putd(dnx, n);
+  P.dnz = putd(dnz ? dnz : dnx, n);
+  P.tab = putd(tab, 361 * (size_t)ncol);
+  P.cstif = cell_stif ? putd(st.data(), st.size()) : nullptr;
+  P.out = p;
+  int* q = di;
+  auto puti = [&](const int32_t* h, size_t cnt) {
+    int* r = q;
+    if (e == hipSuccess && cnt) e = hipMemcpy(r, h, cnt * 4, hipMemcpyHostToDevice);
+    q += cnt;
+    return (const int*)r;
+  };
+  P.nsts = puti(nsts, pn * n);
+  P.iz = puti(iz, n);
+  P.ix = puti(ix, n);
+  P.nnz_arg = puti(nnz_arg, n);
+  P.nnx_arg = puti(nnx_arg, n);
+  P.cvelpn = puti(vp.data(), n);
+  P.ncol = ncol;
+  if (e == hipSuccess) e = af_launch_local_ops(&P, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e == hipSuccess) e = hipMemcpy(out, P.out, 8 * (size_t)n, hipMemcpyDeviceToHost);
+  dfree(dd);
+  dfree(di);
+  if (e != hipSuccess) return fail(ctx, ALIFMM_E_HIP, "local_ops: %s", hipGetErrorString(e));
+  return ALIFMM_OK;
+}
+
+}  // extern "C"

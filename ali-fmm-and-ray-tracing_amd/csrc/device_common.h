@@ -1,0 +1,221 @@
+// device_common.h — shared gfx950 device code for the ALI-FMM travel-time-field solver.
+//
+// The local operators below are the reference's arithmetic (Anis_TTF_rays.py, cited per
+// function) in double precision, operation order preserved and compiled with
+// -ffp-contract=off, so that a cell evaluated on the same neighbourhood matches the CPU
+// oracle to the last bit except where ocml's atan/tan/sin/cos differ from glibc by an ulp.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define AF_DEV __device__ __forceinline__
+
+namespace af {
+
+constexpr double kDeg2Rad = M_PI / 180.0;
+constexpr double kRad2Deg = 180.0 / M_PI;
+
+// Python float '%' (CPython float_divmod; numba real_divmod_func_body).
+AF_DEV double pymod(double a, double b) {
+  double m = fmod(a, b);
+  if (m != 0.0) {
+    if ((b < 0) != (m < 0)) m += b;
+  } else {
+    m = copysign(0.0, b);
+  }
+  return m;
+}
+// round(): half-even (numba lowers to llvm.rint).
+AF_DEV long pyround(double x) { return (long)rint(x); }
+
+// ---------------------------------------------------------------------------------------------
+// Model resident in HBM (uploaded once per set_model, shared by every source on the GPU).
+struct DevModel {
+  int nz0, nx0;          // coarse grid
+  const double* veln;    // orientation [deg]
+  const int* velpn;      // material column (0 = stiffness)
+  const double* vm;      // velocity scale
+  const int* sidx;       // stiffness row index per cell, or nullptr when stif_den is None
+  const double* stab;    // unique stiffness rows [n][5] (exact int64 values as doubles)
+  const double* gtab;    // group velocity table (361, ncol)
+  const double* ptab;    // phase velocity table (361, ncol)
+  int ncol;
+};
+
+// Logical grid -> coarse cell: f = lo1 + (a + side1)/s1 ; c = lo2 + (f + side2)/s2
+// (finer_grid_n nearest-neighbour refinement, :26-56; windows :1516-1529, :2191-2204).
+struct MatView {
+  int s1z, side1z, lo1z, s1x, side1x, lo1x;
+  int s2, side2, lo2z, lo2x;
+  int quant;  // finer_grid_n quantisation: veln -> int32 (trunc), vel_map -> float32
+};
+
+AF_DEV long mv_cell(const DevModel& M, const MatView& v, int iz, int ix) {
+  int fz = v.lo1z + (iz + v.side1z) / v.s1z;
+  int fx = v.lo1x + (ix + v.side1x) / v.s1x;
+  int cz = v.lo2z + (fz + v.side2) / v.s2;
+  int cx = v.lo2x + (fx + v.side2) / v.s2;
+  return (long)cz * M.nx0 + cx;
+}
+
+struct CellMat {
+  double veln, vm;
+  int velpn;
+  const double* stif;  // nullptr => None
+};
+
+AF_DEV CellMat cell_mat(const DevModel& M, const MatView& v, int iz, int ix) {
+  long c = mv_cell(M, v, iz, ix);
+  CellMat r;
+  double a = M.veln[c];
+  double b = M.vm[c];
+  r.veln = v.quant ? (double)(int)a : a;
+  r.vm = v.quant ? (double)(float)b : b;
+  r.velpn = M.velpn[c];
+  r.stif = M.sidx ? M.stab + 5 * (long)M.sidx[c] : nullptr;
+  return r;
+}
+
+// Table lookup, linear in 1-degree bins (:288-291, :1372-1375, :2951-2954).
+AF_DEV double table_vel(const double* tab, int ncol, double eff, int col, double vm) {
+  long a1 = (long)floor(eff);
+  long a2 = (a1 + 1) % 180;
+  double rem = eff - (double)a1;
+  return vm * ((1 - rem) * tab[a1 * ncol + col] + rem * tab[a2 * ncol + col]);
+}
+
+// Closed-form 2D orthotropic Christoffel GROUP velocity (:294-315, group_vel :3542-3558).
+// s[] holds exact integers, so double arithmetic reproduces the reference's int64 sums/products.
+AF_DEV double christoffel_group(const double* s, double eff, double vm) {
+  double sigma = s[4];
+  double e90 = pymod(eff, 90);
+  if (e90 < 0.01 || e90 > 90 - 0.01) {
+    double lam = (fabs(pymod(eff, 180) - 90) < 1) ? s[2] : s[0];
+    return 1000 * vm * sqrt(lam / sigma);
+  }
+  double c22 = s[0], c23 = s[1], c33 = s[2], c44 = s[3];
+  double tan_ang = tan(eff * kDeg2Rad);
+  double A = c22 + c33 - 2 * c44;
+  double B = (c23 + c44) * (tan_ang - 1 / tan_ang);
+  double C = c22 - c33;
+  double disc = B * B + A * A - C * C;
+  double pa;
+  if (eff < 90)
+    pa = pymod(atan((-B - sqrt(disc)) / (C - A)), M_PI);
+  else
+    pa = pymod(atan((-B + sqrt(disc)) / (C - A)), M_PI);
+  double lam = 0.5 * (cos(2 * pa) * (c22 - c44) + sin(2 * pa) * (c23 + c44) * tan_ang + c22 + c44);
+  return 1000 * vm * sqrt(lam / sigma) / cos(eff * kDeg2Rad - pa);
+}
+
+// Christoffel PHASE velocity (update() :1400-1406).
+AF_DEV double christoffel_phase(const double* s, double eff, double vm) {
+  double ca = cos(eff * kDeg2Rad);
+  double sa = sin(eff * kDeg2Rad);
+  double A = ca * ca * s[0] + sa * sa * s[3];
+  double B = ca * sa * (s[1] + s[3]);
+  double C = ca * ca * s[3] + sa * sa * s[2];
+  return 1000 * vm * sqrt((A + C + sqrt((A - C) * (A - C) + 4 * (B * B))) / (2 * s[4]));
+}
+
+// group velocity with the selector 'velpn != 0 or stif_den == None' (:287, :2950)
+AF_DEV double group_vel_cell(const DevModel& M, const CellMat& c, double eff) {
+  if (c.velpn != 0 || c.stif == nullptr) return table_vel(M.gtab, M.ncol, eff, c.velpn, c.vm);
+  return christoffel_group(c.stif, eff, c.vm);
+}
+
+// wavefront_angle_dist :1413-1460
+AF_DEV void wad(long ix, long iz, long x1, long x2, long x3, long z1, long z2, long z3, double y1, double y2,
+                double y3, double& angle, double& dist) {
+  double a;
+  if (y3 != y1) {
+    a = (y2 - y1) / (y3 - y1);
+  } else {
+    angle = 0.0;
+    dist = -1.0;
+    return;
+  }
+  double xpos = (1 - a) * (double)x1 + a * (double)x3;
+  double zpos = (1 - a) * (double)z1 + a * (double)z3;
+  double dx = (double)x2 - xpos;
+  double dz = (double)z2 - zpos;
+  if (dx == 0)
+    angle = 0.0;
+  else
+    angle = pymod(atan(dz / dx) * kRad2Deg + 90, 180);
+  dist = fabs(dz * (double)(x2 - ix) - dx * (double)(z2 - iz)) / sqrt(dx * dx + dz * dz);
+}
+
+// time_between_points :2835-2989 (coarse material, numba negative-index wrap)
+AF_DEV double tbp(const DevModel& M, double x1, double x2, double y1, double y2, double dnx, int sg) {
+  x1 = x1 / (double)sg;
+  x2 = x2 / (double)sg;
+  y1 = y1 / (double)sg;
+  y2 = y2 / (double)sg;
+  double section_time = 0.0;
+  double start_x = x1, end_x = x2, start_y = y1, end_y = y2, prev_x = x1, prev_y = y1;
+  double angle = (x1 == x2) ? 0.0 : atan((y2 - y1) / (x2 - x1)) * kRad2Deg;
+  double mm = 0, cc = 0;
+  if (end_x != start_x) {
+    mm = (end_y - start_y) / (end_x - start_x);
+    cc = start_y - mm * start_x;
+  }
+  bool fin_x = false, fin_y = false;
+  int dir_x = (start_x < end_x) ? 1 : -1;
+  int dir_y = (start_y < end_y) ? 1 : -1;
+  double next_x = (double)pyround(start_x) + dir_x * 0.5;
+  double next_y = (double)pyround(start_y) + dir_y * 0.5;
+  const MatView ident{1, 0, 0, 1, 0, 0, 1, 0, 0, 0, 0};
+  while (!(fin_x && fin_y)) {
+    if (((next_x > end_x && dir_x == 1) || (next_x < end_x && dir_x == -1)) && !fin_x) {
+      fin_x = true;
+      next_x = end_x;
+    }
+    if (((next_y > end_y && dir_y == 1) || (next_y < end_y && dir_y == -1)) && !fin_y) {
+      fin_y = true;
+      next_y = end_y;
+    }
+    double nxv, nyv;
+    if (end_x == start_x) {
+      nxv = start_x;
+      nyv = next_y;
+      next_y += dir_y;
+    } else {
+      double next_x_yval = mm * next_x + cc;
+      if (mm != 0) {
+        double next_y_xval = (next_y - cc) / mm;
+        double d1x = start_x - next_x, d1y = start_y - next_x_yval;
+        double d2x = start_x - next_y_xval, d2y = start_y - next_y;
+        if (d1x * d1x + d1y * d1y < d2x * d2x + d2y * d2y) {
+          nxv = next_x;
+          nyv = next_x_yval;
+          next_x += dir_x;
+        } else {
+          nxv = next_y_xval;
+          nyv = next_y;
+          next_y += dir_y;
+        }
+      } else {
+        nxv = next_x;
+        nyv = next_x_yval;
+        next_x += dir_x;
+      }
+    }
+    long x_pos = pyround((prev_x + nxv) / 2);
+    long y_pos = pyround((prev_y + nyv) / 2);
+    if (x_pos < 0) x_pos += M.nx0;
+    if (y_pos < 0) y_pos += M.nz0;
+    CellMat cm = cell_mat(M, ident, (int)y_pos, (int)x_pos);
+    double eff = pymod(cm.veln - angle, 180);
+    double ddx = prev_x - nxv, ddy = prev_y - nyv;
+    double distance = dnx * sqrt(ddx * ddx + ddy * ddy);
+    double velocity = group_vel_cell(M, cm, eff);
+    double slown = 1.0 / velocity;
+    section_time += distance * slown;
+    prev_x = nxv;
+    prev_y = nyv;
+  }
+  return section_time;
+}
+
+}  // namespace af

@@ -1,0 +1,429 @@
+// fmm_init.hip — source initialisation of travel() (Anis_TTF_rays.py:1508-1993) on gfx950.
+//
+// One workgroup (one wave) per source.  The three refined stage grids (5x5 coarse window x27,
+// 13x13 x9, 27x27 x3; <= 109x109 nodes) live entirely in LDS (147.5 KB of the CU's 160 KB) and
+// are solved with the reference's own heap-ordered FMM: the heap (with its round-half-even parent,
+// SURVEY B-D3), the stage-1 nnz=nnx1 quirk (:1645, padded reads) and the hand-over order are
+// reproduced exactly, so the init region is the reference's up to device transcendental ulps.
+// The heap walk is inherently serial (lane 0); the 63 other lanes clear LDS, fill the straight-ray
+// footprint and decimate between stages.  Output: the decimated stage-3 nodes that the band
+// kernel hands over to the main grid (:2006-2040), as (cell, ttn, class) triples.
+#include "device_common.h"
+#include "local_ops.h"
+#include "kernels.h"
+
+namespace af {
+
+constexpr int kInitMaxN = 109 * 109;  // largest stage grid (stage 1 / 2)
+constexpr int kInitHeap = 8192;       // heap slots (reference sizes them 0.5 * cells)
+constexpr int kInitDec = 37 * 37;     // decimated stage-1/2 grid
+
+struct InitLds {
+  double T[kInitMaxN];
+  double decT[kInitDec];
+  short S[kInitMaxN];
+  unsigned short btg[kInitHeap];  // (z << 8) | x
+  signed char decC[kInitDec];     // 0 far, 1 known inner, 2 known outer, 3 close
+};
+
+struct LdsField {
+  const double* T;
+  const short* S;
+  int nz, nx;
+  AF_DEV int st(long z, long x) const { return z >= nz ? -1 : (int)S[z * nx + x]; }
+  AF_DEV double tt(long z, long x) const { return z >= nz ? 0.0 : T[z * nx + x]; }
+};
+
+struct Heap {
+  InitLds* L;
+  int nz, nx;
+  int ntr;
+  int err;
+  AF_DEV int bz(int k) const { return L->btg[k] >> 8; }
+  AF_DEV int bx(int k) const { return L->btg[k] & 255; }
+  AF_DEV double tb(int k) const { return L->T[bz(k) * nx + bx(k)]; }
+  AF_DEV static int parent(int t) { return (int)rint((double)t / 2.0); }  // half-even (:123)
+  AF_DEV void swap(int a, int b) {
+    unsigned short e = L->btg[a];
+    L->btg[a] = L->btg[b];
+    L->btg[b] = e;
+  }
+  // addtree :94-138
+  AF_DEV void add(int iz, int ix) {
+    ntr += 1;
+    if (ntr >= kInitHeap) { err = 1; ntr = kInitHeap - 1; return; }
+    L->S[iz * nx + ix] = (short)ntr;
+    L->btg[ntr] = (unsigned short)((iz << 8) | ix);
+    int tpc = ntr, tpp = parent(tpc);
+    double tv = L->T[iz * nx + ix];
+    while (tpp > 0) {
+      if (tv < tb(tpp)) {
+        L->S[iz * nx + ix] = (short)tpp;
+        L->S[bz(tpp) * nx + bx(tpp)] = (short)tpc;
+        swap(tpc, tpp);
+        tpc = tpp;
+        tpp = parent(tpc);
+      } else {
+        tpp = 0;
+      }
+    }
+  }
+  // updtree :141-175
+  AF_DEV void upd(int iz, int ix) {
+    int tpc = L->S[iz * nx + ix], tpp = parent(tpc);
+    double tv = L->T[iz * nx + ix];
+    while (tpp > 0) {
+      if (tv < tb(tpp)) {
+        L->S[iz * nx + ix] = (short)tpp;
+        L->S[bz(tpp) * nx + bx(tpp)] = (short)tpc;
+        swap(tpc, tpp);
+        tpc = tpp;
+        tpp = parent(tpc);
+      } else {
+        tpp = 0;
+      }
+    }
+  }
+  // downtree :178-237
+  AF_DEV void down() {
+    if (ntr == 1) { ntr -= 1; return; }
+    L->S[bz(ntr) * nx + bx(ntr)] = 1;
+    L->btg[1] = L->btg[ntr];
+    ntr -= 1;
+    int tpp = 1, tpc = 2;
+    while (tpc < ntr) {
+      if (tb(tpc) > tb(tpc + 1)) tpc = tpc + 1;
+      if (tb(tpc) < tb(tpp)) {
+        L->S[bz(tpp) * nx + bx(tpp)] = (short)tpc;
+        L->S[bz(tpc) * nx + bx(tpc)] = (short)tpp;
+        swap(tpc, tpp);
+        tpp = tpc;
+        tpc = 2 * tpp;
+      } else {
+        tpc = ntr + 1;
+      }
+    }
+    if (tpc == ntr) {
+      if (tb(tpc) < tb(tpp)) {
+        L->S[bz(tpp) * nx + bx(tpp)] = (short)tpc;
+        L->S[bz(tpc) * nx + bx(tpc)] = (short)tpp;
+        swap(tpc, tpp);
+      }
+    }
+  }
+};
+
+struct StageCfg {
+  double dnx;
+  int isx, isz, max_dist, quirk;
+  MatView mv;
+};
+
+// relax one neighbour: update() then fouds18_A() (:1635-1638)
+AF_DEV void relax(InitLds* L, const DevModel& M, const StageCfg& c, int nz, int nx, int iz, int ix, int quirk) {
+  LdsField F{L->T, L->S, nz, nx};
+  CellMat cm = cell_mat(M, c.mv, iz, ix);
+  double v = update(F, M, cm, iz, ix, c.dnx, quirk ? nx : nz, nx);
+  if (v == -1.0) v = fouds18(F, M, cm, iz, ix, c.dnx, c.dnx, nx, nz);
+  L->T[iz * nx + ix] = v;
+}
+
+// stage FMM loop (:1620-1674)
+AF_DEV void stage_loop(Heap& h, const DevModel& M, const StageCfg& c) {
+  InitLds* L = h.L;
+  const int nz = h.nz, nx = h.nx;
+  bool finished = false;
+  while (h.ntr > 0 && !finished && !h.err) {
+    int ix = h.bx(1), iz = h.bz(1);
+    L->S[iz * nx + ix] = 0;
+    h.down();
+    for (int s = 0; s < 2; s++) {
+      int i = s == 0 ? ix - 1 : ix + 1;
+      if (0 <= i && i <= nx - 1) {
+        int st = L->S[iz * nx + i];
+        if (st == -1) {
+          relax(L, M, c, nz, nx, iz, i, 0);
+          h.add(iz, i);
+        } else if (st > 0) {
+          relax(L, M, c, nz, nx, iz, i, c.quirk);
+          h.upd(iz, i);
+        }
+      } else if (abs(c.isx - i) == c.max_dist + 1) {
+        finished = true;
+      }
+    }
+    for (int s = 0; s < 2; s++) {
+      int i = s == 0 ? iz - 1 : iz + 1;
+      if (0 <= i && i <= nz - 1) {
+        int st = L->S[i * nx + ix];
+        if (st == -1) {
+          relax(L, M, c, nz, nx, i, ix, 0);
+          h.add(i, ix);
+        } else if (st > 0) {
+          relax(L, M, c, nz, nx, i, ix, 0);
+          h.upd(i, ix);
+        }
+      } else if (abs(c.isz - i) == c.max_dist + 1) {
+        finished = true;
+      }
+    }
+  }
+}
+
+// Decimate the stage grid (every 3rd node) into decT/decC with the hand-over's "outer" test
+// (:1719-1753).  All lanes.
+AF_DEV void decimate(InitLds* L, int nz, int nx, int lane, int nl) {
+  int dz = (nz - 1) / 3 + 1, dx = (nx - 1) / 3 + 1;
+  for (int k = lane; k < dz * dx; k += nl) {
+    int i = 3 * (k / dx), j = 3 * (k % dx);
+    int st = L->S[i * nx + j];
+    L->decT[k] = L->T[i * nx + j];
+    signed char cls = 0;
+    if (st == 0) {
+      bool outer = false;
+      if (i - 3 >= 0) { if (L->S[(i - 3) * nx + j] == -1) outer = true; } else outer = true;
+      if (i + 3 <= nz - 1) { if (L->S[(i + 3) * nx + j] == -1) outer = true; } else outer = true;
+      if (j - 3 >= 0) { if (L->S[i * nx + j - 3] == -1) outer = true; } else outer = true;
+      if (j + 3 <= nx - 1) { if (L->S[i * nx + j + 3] == -1) outer = true; } else outer = true;
+      cls = outer ? 2 : 1;
+    } else if (st > 0) {
+      cls = 3;
+    }
+    L->decC[k] = cls;
+  }
+}
+
+AF_DEV void clear_grid(InitLds* L, int n, int lane, int nl) {
+  for (int k = lane; k < n; k += nl) {
+    L->T[k] = 0.0;
+    L->S[k] = -1;
+  }
+}
+
+// field accessor of the exact main-loop prefix: main-grid coordinates, LDS window storage;
+// nodes outside the window have never been touched (far: nsts -1, ttn 0)
+struct WinField {
+  const double* T;
+  const short* S;
+  int wz0, wx0, wz1, wx1, ww;
+  AF_DEV int st(long z, long x) const {
+    return (z < wz0 || z > wz1 || x < wx0 || x > wx1) ? -1 : (int)S[(z - wz0) * ww + (x - wx0)];
+  }
+  AF_DEV double tt(long z, long x) const {
+    return (z < wz0 || z > wz1 || x < wx0 || x > wx1) ? 0.0 : T[(z - wz0) * ww + (x - wx0)];
+  }
+};
+
+// main loop :2055-2102 on the LDS window (heap in window-local coordinates)
+AF_DEV void main_prefix(Heap& h, const DevModel& M, const InitJob& J, int wz0, int wx0, int wz1, int wx1) {
+  InitLds* L = h.L;
+  const int ww = h.nx;
+  const int nnz = M.nz0, nnx = M.nx0;
+  const MatView ident{1, 0, 0, 1, 0, 0, 1, 0, 0, 0, 0};
+  const WinField F{L->T, L->S, wz0, wx0, wz1, wx1, ww};
+  auto relax_main = [&](int iz, int ix) {
+    CellMat cm = cell_mat(M, ident, iz, ix);
+    double v = update(F, M, cm, iz, ix, J.dnx, nnz, nnx);
+    if (v == -1.0) v = fouds18(F, M, cm, iz, ix, J.dnx, J.dnz, nnx, nnz);
+    L->T[(iz - wz0) * ww + (ix - wx0)] = v;
+  };
+  while (h.ntr > 0 && !h.err) {
+    const int lx = h.bx(1), lz = h.bz(1);
+    if (L->T[lz * ww + lx] >= J.tstop) break;
+    const int iz = lz + wz0, ix = lx + wx0;
+    if ((wz0 > 0 && iz - wz0 < 3) || (wz1 < nnz - 1 && wz1 - iz < 3) || (wx0 > 0 && ix - wx0 < 3) ||
+        (wx1 < nnx - 1 && wx1 - ix < 3))
+      break;
+    L->S[lz * ww + lx] = 0;
+    h.down();
+    for (int s = 0; s < 2; s++) {
+      int i = s == 0 ? ix - 1 : ix + 1;
+      if (0 <= i && i <= nnx - 1) {
+        int li = i - wx0;
+        int st = L->S[lz * ww + li];
+        if (st == -1) {
+          relax_main(iz, i);
+          h.add(lz, li);
+        } else if (st > 0) {
+          relax_main(iz, i);
+          h.upd(lz, li);
+        }
+      }
+    }
+    for (int s = 0; s < 2; s++) {
+      int i = s == 0 ? iz - 1 : iz + 1;
+      if (0 <= i && i <= nnz - 1) {
+        int li = i - wz0;
+        int st = L->S[li * ww + lx];
+        if (st == -1) {
+          relax_main(i, ix);
+          h.add(li, lx);
+        } else if (st > 0) {
+          relax_main(i, ix);
+          h.upd(li, lx);
+        }
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(64) void fmm_init_kernel(DevModel M, InitJob* jobs, int njobs, HandoverOut* out) {
+  __shared__ InitLds lds;
+  InitLds* L = &lds;
+  const int src = blockIdx.x;
+  if (src >= njobs) return;
+  const int lane = threadIdx.x, nl = blockDim.x;
+  InitJob J = jobs[src];
+  const int nnz = M.nz0, nnx = M.nx0;
+  const long isx = J.isx, isz = J.isz;
+  HandoverOut* O = out + src;
+
+  const int sgs[3] = {27, 9, 3}, sizes[3] = {2, 6, 13};
+  int pisz = 0, pisx = 0, pnz = 0, pnx = 0;
+  int err = 0;
+  for (int stg = 0; stg < 3; stg++) {
+    const int sg = sgs[stg], size = sizes[stg];
+    const int left = max(0L, isx - size), right = min((long)nnx - 1, isx + size);
+    const int bottom = max(0L, isz - size), top = min((long)nnz - 1, isz + size);
+    const int nz = sg * (top - bottom) + 1, nx = sg * (right - left) + 1;
+    const int isx_s = sg * (int)(isx - left), isz_s = sg * (int)(isz - bottom);
+    StageCfg c;
+    c.dnx = J.dnx / sg;
+    c.isx = isx_s;
+    c.isz = isz_s;
+    c.max_dist = sg * size;
+    c.quirk = stg == 0;
+    c.mv = MatView{sg, (sg - 1) / 2, bottom, sg, (sg - 1) / 2, left, 1, 0, 0, 0, 1};
+    clear_grid(L, nz * nx, lane, nl);
+    __syncthreads();
+    Heap h{L, nz, nx, 0, 0};
+    if (stg == 0) {
+      // straight rays in the source cell footprint (:1546-1590), coarse material at the source
+      const int side1 = (sg - 1) / 2;
+      MatView ident{1, 0, 0, 1, 0, 0, 1, 0, 0, 0, 0};
+      CellMat cs = cell_mat(M, ident, (int)isz, (int)isx);
+      const int w = 2 * side1 + 1;
+      for (int k = lane; k < w * w; k += nl) {
+        int i = k / w - side1, j = k % w - side1;
+        if (0 <= isz_s + i && isz_s + i <= nz - 1 && 0 <= isx_s + j && isx_s + j <= nx - 1) {
+          double angle = (j == 0) ? 90.0 : atan((double)i / (double)j) * kRad2Deg;
+          double eff = pymod(cs.veln - angle, 180);
+          double velocity = (cs.velpn != 0 || cs.stif == nullptr)
+                                ? table_vel(M.gtab, M.ncol, eff, cs.velpn, cs.vm)
+                                : christoffel_group(cs.stif, eff, cs.vm);
+          double length = c.dnx * sqrt((double)(i * i + j * j));
+          L->T[(isz_s + i) * nx + isx_s + j] = length / velocity;
+          L->S[(isz_s + i) * nx + isx_s + j] = 0;
+        }
+      }
+      __syncthreads();
+      if (lane == 0) {
+        // window edges -> heap, in the reference's order (:1601-1612)
+        const int s1 = side1;
+        if (isz_s - s1 >= 0)
+          for (int i = max(0, isx_s - s1); i <= min(nx - 1, isx_s + s1); i++) h.add(isz_s - s1, i);
+        if (isz_s + s1 <= nz - 1)
+          for (int i = max(0, isx_s - s1); i <= min(nx - 1, isx_s + s1); i++) h.add(isz_s + s1, i);
+        if (isx_s - s1 >= 0)
+          for (int i = max(0, isz_s - s1); i <= min(nz - 1, isz_s + s1); i++) h.add(i, isx_s - s1);
+        if (isx_s + s1 <= nx - 1)
+          for (int i = max(0, isz_s - s1); i <= min(nz - 1, isz_s + s1); i++) h.add(i, isx_s + s1);
+      }
+    } else if (lane == 0) {
+      // hand-over from the decimated previous stage, in row-major order (:1719-1753)
+      int dz = (pnz - 1) / 3 + 1, dx = (pnx - 1) / 3 + 1;
+      for (int k = 0; k < dz * dx; k++) {
+        int i = 3 * (k / dx), j = 3 * (k % dx);
+        int pz = isz_s + (i - pisz) / 3, px = isx_s + (j - pisx) / 3;
+        L->T[pz * nx + px] = L->decT[k];
+        signed char cls = L->decC[k];
+        if (cls == 1 || cls == 2) L->S[pz * nx + px] = 0;
+        if (cls >= 2) h.add(pz, px);
+      }
+    }
+    if (lane == 0) {
+      stage_loop(h, M, c);
+      err |= h.err;
+    }
+    __syncthreads();
+    decimate(L, nz, nx, lane, nl);
+    __syncthreads();
+    pisz = isz_s;
+    pisx = isx_s;
+    pnz = nz;
+    pnx = nx;
+  }
+  if (J.exact_r > 0) {
+    // ---- exact heap-ordered prefix of the main loop (:2055-2102) in an LDS window ----
+    // The reference's pop order (quirky heap included) decides the field near the source, where
+    // the wavefront hits grid edges and close hand-over nodes get overwritten.  Run it exactly
+    // until the root's T reaches exact_r*dnx/vmax (or the root comes within 3 nodes of a window
+    // edge that is not a grid edge), then hand the heap's state to the band kernel.
+    const int W = J.exact_r + 6;
+    const int wz0 = (int)max(0L, isz - W), wz1 = (int)min((long)nnz - 1, isz + W);
+    const int wx0 = (int)max(0L, isx - W), wx1 = (int)min((long)nnx - 1, isx + W);
+    const int wh = wz1 - wz0 + 1, ww = wx1 - wx0 + 1;
+    if (wh * ww > kInitMaxN) {
+      err = 1;
+    } else {
+      clear_grid(L, wh * ww, lane, nl);
+      __syncthreads();
+      Heap h{L, wh, ww, 0, 0};
+      if (lane == 0) {
+        int dz = (pnz - 1) / 3 + 1, dx = (pnx - 1) / 3 + 1;
+        for (int k = 0; k < dz * dx; k++) {
+          int i = 3 * (k / dx), j = 3 * (k % dx);
+          int pz = (int)(isz + (i - pisz) / 3) - wz0, px = (int)(isx + (j - pisx) / 3) - wx0;
+          L->T[pz * ww + px] = L->decT[k];
+          signed char cls = L->decC[k];
+          if (cls == 1 || cls == 2) L->S[pz * ww + px] = 0;
+          if (cls >= 2) h.add(pz, px);
+        }
+        main_prefix(h, M, J, wz0, wx0, wz1, wx1);
+        err |= h.err;
+      }
+      __syncthreads();
+      // emit every touched window node: known (1) / close (3)
+      if (lane == 0) {
+        int n = 0;
+        for (int k = 0; k < wh * ww; k++) {
+          int st = L->S[k];
+          if (st < 0) continue;
+          int z = wz0 + k / ww, x = wx0 + k % ww;
+          O->cell[n] = z * nnx + x;
+          O->ttn[n] = L->T[k];
+          O->cls[n] = st == 0 ? 1 : 3;
+          n++;
+        }
+        O->n = n;
+        O->err = err;
+      }
+      return;
+    }
+  }
+  // emit the decimated stage-3 nodes for the main-grid hand-over (:2006-2040)
+  if (lane == 0) {
+    int dz = (pnz - 1) / 3 + 1, dx = (pnx - 1) / 3 + 1;
+    int n = 0;
+    for (int k = 0; k < dz * dx; k++) {
+      signed char cls = L->decC[k];
+      if (cls == 0) continue;
+      int i = 3 * (k / dx), j = 3 * (k % dx);
+      long pz = isz + (i - pisz) / 3, px = isx + (j - pisx) / 3;
+      O->cell[n] = (int)(pz * nnx + px);
+      O->ttn[n] = L->decT[k];
+      O->cls[n] = cls;
+      n++;
+    }
+    O->n = n;
+    O->err = err;
+  }
+}
+
+}  // namespace af
+
+extern "C" hipError_t af_launch_init(const af::DevModel* M, af::InitJob* jobs, int njobs, af::HandoverOut* out,
+                                     hipStream_t stream) {
+  hipLaunchKernelGGL(af::fmm_init_kernel, dim3(njobs), dim3(64), 0, stream, *M, jobs, njobs, out);
+  return hipGetLastError();
+}

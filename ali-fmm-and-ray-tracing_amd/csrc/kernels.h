@@ -1,0 +1,94 @@
+// kernels.h — parameter blocks and launchers shared by the kernels and the C-ABI host code.
+#pragma once
+#include "device_common.h"
+#include "fmm_shared.h"
+
+namespace af {
+
+struct BandSrc {
+  double* T;      // field (main grid)
+  int* S;         // status
+  int* L0;        // close list (ping)
+  int* L1;        // close list (pong)
+  int* A;         // accepted cells of the step
+  int* C;         // candidates of the step
+  double* V;      // candidate values
+  double* Ts[2];  // stage grids (mode 1)
+  int* Ss[2];
+  long long steps[4];
+  long long nupd;  // relax evaluations (cell-sweeps) in the main run
+  int err;
+  int pad;
+};
+
+struct BandParams {
+  DevModel M;
+  int nsrc;
+  int mode;      // 0: travel (subgrid 1, init from fmm_init_kernel); 1: travel_finer_grid
+  int sg;        // subgrid size (mode 1)
+  int nz, nx;    // main grid (fine grid in mode 1)
+  double dnx, dnz;
+  double cdelta, vmax, r0;
+  int capL, capC, capS;  // list capacities, stage-grid capacity (cells)
+  BandSrc* src;
+  const HandoverOut* ho;  // mode 0
+  const double* scx;
+  const double* scz;
+  double gox, goz;
+};
+
+struct RayJob {
+  const double* ttf;  // receiver travel-time field on the fine grid (row-major, fnz x fnx)
+  double sx, sy;      // source (fine-grid x, z)
+  double rx, ry;      // receiver (fine-grid x, z)
+};
+
+struct RayParams {
+  DevModel M;  // coarse model (veln f64, velpn, vel_map f64, stiffness)
+  int fnz, fnx;
+  int sg;
+  double dnx;
+  int nrays;
+  int max_pts;
+  const RayJob* jobs;
+  double* ray_x;  // [nrays][max_pts]
+  double* ray_y;
+  int* ray_len;
+  double* times;
+  int* flags;     // bit0 early exit ("Travel time to receiver increasing"), bit1 capacity, bit2 empty plane
+};
+
+struct LocalOpsParams {
+  int op;  // 0 update(), 1 fouds18_A()
+  long n;
+  int pz, px;
+  const double* ttn;  // [n][pz][px]
+  const int* nsts;
+  const int* iz;
+  const int* ix;
+  const double* dnx;
+  const double* dnz;
+  const int* nnz_arg;
+  const int* nnx_arg;
+  const double* cveln;  // material at the target cell, per case
+  const int* cvelpn;
+  const double* cvm;
+  const double* cstif;  // [n][5] or nullptr (None)
+  const double* tab;    // (361, ncol): phase table for update(), group table for fouds18_A()
+  int ncol;
+  double* out;
+};
+
+}  // namespace af
+
+extern "C" {
+hipError_t af_launch_init(const af::DevModel* M, af::InitJob* jobs, int njobs, af::HandoverOut* out, hipStream_t stream);
+hipError_t af_launch_band(const af::BandParams* P, hipStream_t stream);
+hipError_t af_launch_scale(double* T, long n, double sg, hipStream_t stream);
+hipError_t af_launch_rays(const af::RayParams* P, hipStream_t stream);
+hipError_t af_launch_pack_rays(const double* rx, const double* ry, const int* len, const long long* off, int nrays,
+                               int max_pts, double* packed, hipStream_t stream);
+hipError_t af_launch_local_ops(const af::LocalOpsParams* P, hipStream_t stream);
+hipError_t af_launch_tbp(const af::DevModel* M, int n, const double* x1, const double* x2, const double* y1,
+                         const double* y2, double dnx, int sg, double* out, hipStream_t stream);
+}

@@ -1,0 +1,612 @@
+// local_ops.h — the reference's local operators as templated device functions.
+//
+//   update()   — ALI locally-interpolated wavefront update, Anis_TTF_rays.py:904-1410
+//   fouds18()  — multi-stencil quadratic fallback, Anis_TTF_rays.py:240-901
+//
+// F is a field accessor with  int st(long z, long x)  (node status; rows past the array read -1,
+// the reference's padded stage-1 semantics) and  double tt(long z, long x).  Validity in update()
+// is st >= 0 (alive or close), "known" in fouds18() is st == 0, exactly as in the reference.
+// Material is read only at the target cell (CellMat), as in the reference.
+#pragma once
+#include "device_common.h"
+
+namespace af {
+
+template <class F>
+AF_DEV double fouds18(const F& f, const DevModel& M, const CellMat& cm, long iz, long ix, double dnx, double dnz,
+                      long nnx, long nnz) {
+#define N_(z, x) f.st((z), (x))
+#define T_(z, x) f.tt((z), (x))
+    double veln = cm.veln;
+    /* ---- 0 deg stencil (:281-459) ---- */
+    int tsw1 = 0;
+    double travm = 0;
+    /* the four stencil families' slownesses (group velocity at 0, 45, -27, +27 deg), computed
+       unconditionally in the reference; evaluated here in one loop (one inlined instance) */
+    double slo0 = 0, slo1 = 0, slo2 = 0, slo3 = 0;
+#pragma unroll 1
+    for (int q = 0; q < 4; q++) {
+        double e = q == 0 ? pymod(0 - veln, 180)
+                 : q == 1 ? (double)pyround(pymod(45 - veln, 180))
+                 : q == 2 ? pymod(-27.0 - veln, 180) : pymod(27.0 - veln, 180);
+        double g = 1.0 / group_vel_cell(M, cm, e);
+        if (q == 0) slo0 = g;
+        else if (q == 1) slo1 = g;
+        else if (q == 2) slo2 = g;
+        else slo3 = g;
+    }
+    double slown = slo0;
+    for (int jj_ = 0; jj_ < 2; jj_++) {
+        long j = jj_ == 0 ? ix - 1 : ix + 1;
+        if (0 <= j && j <= nnx - 1) {
+            int swj = -1;
+            long j2;
+            if (j == ix - 1) {
+                j2 = j - 1;
+                if (j2 >= 0 && N_(iz, j2) == 0) swj = 0;
+            } else {
+                j2 = j + 1;
+                if (j2 <= nnx - 1 && N_(iz, j2) == 0) swj = 0;
+            }
+            if (N_(iz, j) == 0 && swj == 0) {
+                swj = -1;
+                if (T_(iz, j) >= T_(iz, j2)) swj = 0;
+            } else {
+                swj = -1;
+            }
+            for (int kk_ = 0; kk_ < 2; kk_++) {
+                long k = kk_ == 0 ? iz - 1 : iz + 1;
+                if (0 <= k && k <= nnz - 1) {
+                    int swk = -1;
+                    long k2;
+                    if (k == iz - 1) {
+                        k2 = k - 1;
+                        if (k2 >= 0 && N_(k2, ix) == 0) swk = 0;
+                    } else {
+                        k2 = k + 1;
+                        if (k2 <= nnz - 1 && N_(k2, ix) == 0) swk = 0;
+                    }
+                    if (N_(k, ix) == 0 && swk == 0) {
+                        swk = -1;
+                        if (T_(k, ix) >= T_(k2, ix)) swk = 0;
+                    } else {
+                        swk = -1;
+                    }
+                    int swsol = 0;
+                    double a = 0, b = 0, c = 0, tref = 0, tdiv = 1, u, v;
+                    (void)v;
+                    if (swj == 0) {
+                        swsol = 1;
+                        if (swk == 0) {
+                            u = 2.0 * dnx;
+                            a = 18;
+                            b = -6 * (4.0 * T_(iz, j) - T_(iz, j2) + 4.0 * T_(k, ix) - T_(k2, ix));
+                            double p = 4.0 * T_(iz, j) - T_(iz, j2), q = 4.0 * T_(k, ix) - T_(k2, ix);
+                            c = p * p + q * q - 4 * (u * u) * (slown * slown);
+                            tref = 0.0; tdiv = 1.0;
+                        } else if (N_(k, ix) == 0) {
+                            u = dnz; v = 2.0 * dnx;
+                            a = 18;
+                            b = -6.0 * (3.0 * T_(k, ix) + 4.0 * T_(iz, j) - T_(iz, j2));
+                            double p = 3.0 * T_(k, ix), q = 4.0 * T_(iz, j) - T_(iz, j2);
+                            c = p * p + q * q - 4 * (v * v) * (slown * slown);
+                            tref = 0.0; tdiv = 1.0;
+                        } else {
+                            u = 2.0 * dnx;
+                            a = 1.0; b = 0.0;
+                            c = -(u * u) * (slown * slown);
+                            tref = 4.0 * T_(iz, j) - T_(iz, j2);
+                            tdiv = 1.0; /* tdiv=3.0 is overwritten by tdiv=1.0 (:389,:395) */
+                        }
+                    } else if (N_(iz, j) == 0) {
+                        swsol = 1;
+                        if (swk == 0) {
+                            u = dnx;
+                            double em = 3.0 * T_(iz, j) + 4.0 * T_(k, ix) - T_(k2, ix);
+                            a = 18; b = -6.0 * em;
+                            double p = 3.0 * T_(iz, j), q = 4.0 * T_(k, ix) - T_(k2, ix);
+                            c = p * p + q * q - 3 * 4 * (u * u) * (slown * slown);
+                            tref = 0.0; tdiv = 1.0;
+                        } else if (N_(k, ix) == 0) {
+                            u = dnx; v = dnz;
+                            a = 2;
+                            b = -2 * (T_(k, ix) + T_(iz, j));
+                            double w = u * slown;
+                            c = T_(k, ix) * T_(k, ix) + T_(iz, j) * T_(iz, j) - w * w;
+                            tref = 0.0; tdiv = 1.0;
+                        } else {
+                            a = 1.0; b = 0.0;
+                            double w = T_(iz, j) + slown * dnx;
+                            c = -(w * w);
+                            tref = 0.0; tdiv = 1.0;
+                        }
+                    } else {
+                        if (swk == 0) {
+                            swsol = 1;
+                            u = 2.0 * dnz;
+                            a = 1.0; b = 0.0;
+                            c = -(u * u) * (slown * slown);
+                            tref = 4.0 * T_(k, ix) - T_(k2, ix);
+                            tdiv = 3.0;
+                        } else if (N_(k, ix) == 0) {
+                            swsol = 1;
+                            a = 1.0; b = 0.0;
+                            double w = T_(k, ix) + slown * dnz;
+                            c = -(w * w);
+                            tref = 0.0; tdiv = 1.0;
+                        }
+                    }
+                    if (swsol == 1) {
+                        double rd1 = b * b - 4.0 * a * c;
+                        if (rd1 < 0) rd1 = 0;
+                        double tdsh = (-b + sqrt(rd1)) / (2.0 * a);
+                        double trav = (tref + tdsh) / tdiv;
+                        if (tsw1 == 1) travm = (travm < trav) ? travm : trav;
+                        else { travm = trav; tsw1 = 1; }
+                    }
+                }
+            }
+        }
+    }
+    /* ---- 45 deg stencil (:467-696) ---- */
+    int tsw2 = 0;
+    double travmd = 0;
+    slown = slo1;
+    double mf2 = sqrt(2.0);
+    for (int jj_ = 0; jj_ < 2; jj_++) {
+        long j = (jj_ == 0) ? ix - 1 : ix + 1;
+        long k = (j == ix - 1) ? iz + 1 : iz - 1;
+        if (0 <= j && j <= nnx - 1 && 0 <= k && k <= nnz - 1) {
+            int swdiag = -1;
+            long j2 = 0, k2 = 0;
+            if (j == ix - 1) {
+                j2 = j - 1; k2 = k + 1;
+                if (j2 >= 0 && k2 <= nnz - 1 && N_(k2, j2) == 0) swdiag = 0;
+            } else {
+                j2 = j + 1; k2 = k - 1;
+                if (j2 <= nnx - 1 && k2 >= 0 && N_(k2, j2) == 0) swdiag = 0;
+            }
+            if (N_(k, j) == 0 && swdiag == 0) {
+                swdiag = -1;
+                if (T_(k, j) >= T_(k2, j2)) swdiag = 0;
+            } else {
+                swdiag = -1;
+            }
+            for (int q_ = 0; q_ < 2; q_++) {
+                long jj = (q_ == 0) ? ix - 1 : ix + 1;
+                long kk = (jj == ix - 1) ? iz - 1 : iz + 1;
+                if (0 <= jj && jj <= nnx - 1 && 0 <= kk && kk <= nnz - 1) {
+                    int swskew = -1;
+                    long jj2, kk2;
+                    if (jj == ix - 1) {
+                        jj2 = jj - 1; kk2 = kk - 1;
+                        if (jj2 >= 0 && kk2 >= 0 && N_(kk2, jj2) == 0) swskew = 0;
+                    } else {
+                        jj2 = jj + 1; kk2 = kk + 1;
+                        if (jj2 <= nnx - 1 && kk2 <= nnz - 1 && N_(kk2, jj2) == 0) swskew = 0;
+                    }
+                    if (N_(kk, jj) == 0 && swskew == 0) {
+                        swskew = -1;
+                        if (T_(kk, jj) >= T_(kk2, jj2)) swskew = 0;
+                    } else {
+                        swskew = -1;
+                    }
+                    int swsol = 0;
+                    double a = 0, b = 0, c = 0, tref = 0, tdiv = 1, u, v;
+                    (void)v;
+                    if (swdiag == 0) {
+                        swsol = 1;
+                        if (swskew == 0) {
+                            u = 2.0 * mf2 * dnx;
+                            a = 18.0;
+                            b = -6.0 * (4.0 * T_(k, j) - T_(k2, j2) + 4.0 * T_(kk, jj) - T_(kk2, jj2));
+                            double p = 4.0 * T_(k, j) - T_(k2, j2), q = 4.0 * T_(kk, jj) - T_(kk2, jj2);
+                            c = p * p + q * q - 4 * (u * u) * (slown * slown);
+                            tref = 0; tdiv = 1.0;
+                        } else if (N_(kk, jj) == 0) {
+                            u = mf2 * dnz; v = 2.0 * mf2 * dnx;
+                            a = 18;
+                            b = -6.0 * (3.0 * T_(kk, jj) + 4.0 * T_(k, j) - T_(k2, j2));
+                            double p = 3.0 * T_(kk, jj), q = 4.0 * T_(k, j) - T_(k2, j2);
+                            c = p * p + q * q - 4 * (v * v) * (slown * slown);
+                            tref = 0.0; tdiv = 1.0;
+                        } else {
+                            u = mf2 * 2.0 * dnx;
+                            a = 1.0; b = 0.0;
+                            double w = u * slown;
+                            c = -1.0 * (w * w);
+                            tref = 4.0 * T_(k, j) - T_(k2, j2);
+                            tdiv = 3.0;
+                        }
+                    } else if (N_(k, j) == 0) {
+                        swsol = 1;
+                        if (swskew == 0) {
+                            u = mf2 * dnx; v = mf2 * 2.0 * dnz;
+                            double em = 3.0 * T_(k, j) + 4.0 * T_(kk, jj) - T_(kk2, jj2);
+                            a = 18; b = -6.0 * em;
+                            double p = 3.0 * T_(k, j), q = 4.0 * T_(kk, jj) - T_(kk2, jj2);
+                            c = p * p + q * q - 3 * 4 * (u * u) * (slown * slown);
+                            tref = 0.0; tdiv = 1.0;
+                        } else if (N_(kk, jj) == 0) {
+                            u = mf2 * dnx; v = mf2 * dnz;
+                            a = 2;
+                            b = -2 * (T_(kk, jj) + T_(k, j));
+                            double w = u * slown;
+                            c = T_(kk, jj) * T_(kk, jj) + T_(k, j) * T_(k, j) - 4.0 / 9.0 * (w * w);
+                            tref = 0.0; tdiv = 1.0;
+                        } else {
+                            u = mf2 * dnx;
+                            a = 1.0; b = 0.0;
+                            double w = T_(k, j) + slown * u;
+                            c = -(w * w);
+                            tref = 0; tdiv = 1.0;
+                        }
+                    } else {
+                        if (swskew == 0) {
+                            swsol = 1;
+                            u = 2.0 * mf2 * dnz;
+                            a = 1.0; b = 0.0;
+                            c = -(u * u) * (slown * slown);
+                            tref = 4.0 * T_(kk, jj) - T_(kk2, jj2);
+                            tdiv = 3.0;
+                        } else if (N_(kk, jj) == 0) {
+                            swsol = 1;
+                            u = mf2 * dnx;
+                            a = 1.0; b = 0.0;
+                            c = -(slown * slown) * (u * u);
+                            tref = T_(kk, jj);
+                            tdiv = 1.0;
+                        }
+                    }
+                    if (swsol == 1) {
+                        double rd1 = b * b - 4.0 * a * c;
+                        if (rd1 > 0) {
+                            double tdsh = (-b + sqrt(rd1)) / (2.0 * a);
+                            double trav = (tref + tdsh) / tdiv;
+                            if (tsw2 == 1) travmd = (travmd < trav) ? travmd : trav;
+                            else { travmd = trav; tsw2 = 1; }
+                        }
+                    }
+                }
+            }
+        }
+    }
+    if (travmd != 0) travmd = (travm < travmd) ? travm : travmd;
+    else travmd = travm;
+
+    /* ---- atan(1/2) stencils (:698-897) ---- */
+    double travmt = 0, travms = 0;
+    for (int pass = 0; pass < 2; pass++) {
+        slown = pass == 0 ? slo2 : slo3;
+        double m5 = sqrt(5.0);
+        /* j_vec/k_vec of :740-741 (pass 0) and :839-840 (pass 1) as offsets (no indexed arrays) */
+#define JV(l) (ix + (pass == 0 ? ((l) % 4 == 0 ? -1 : (l) == 1 ? 2 : (l) == 2 ? 1 : -2) \
+                               : ((l) % 4 == 0 ? 1 : (l) == 1 ? 2 : (l) == 2 ? -1 : -2)))
+#define KV(l) (iz + (pass == 0 ? ((l) % 4 == 0 ? -2 : (l) == 1 ? -1 : (l) == 2 ? 2 : 1) \
+                               : ((l) % 4 == 0 ? -2 : (l) == 1 ? 1 : (l) == 2 ? 2 : -1)))
+        int tsw = 0;
+        double tm = 0;
+        for (int lp = 0; lp < 4; lp++) {
+            long j = JV(lp), k = KV(lp), jj = JV(lp + 1), kk = KV(lp + 1);
+            if (0 <= j && j <= nnx - 1 && 0 <= k && k <= nnz - 1 && 0 <= jj && jj <= nnx - 1 && 0 <= kk &&
+                kk <= nnz - 1) {
+                int swsol = 0;
+                double a = 0, b = 0, c = 0, tref = 0, u;
+                if (N_(k, j) == 0) {
+                    swsol = 1;
+                    if (N_(kk, jj) == 0) {
+                        u = m5 * dnx;
+                        a = 2;
+                        b = -2 * (T_(kk, jj) + T_(k, j));
+                        double w = u * slown;
+                        c = T_(kk, jj) * T_(kk, jj) + T_(k, j) * T_(k, j) - 2 * (w * w);
+                        tref = 0.0;
+                    } else {
+                        u = m5 * dnx;
+                        a = 1; b = 0;
+                        double w = slown * u;
+                        c = -(w * w);
+                        tref = T_(k, j);
+                    }
+                } else if (N_(kk, jj) == 0) {
+                    swsol = 1;
+                    u = m5 * dnx;
+                    a = 1; b = 0;
+                    double w = slown * u;
+                    c = -(w * w);
+                    tref = T_(kk, jj);
+                }
+                if (swsol == 1) {
+                    double rd1 = b * b - 4 * a * c;
+                    if (rd1 < 0) rd1 = 0;
+                    double tdsh = (-b + sqrt(rd1)) / (2.0 * a);
+                    double trav = tref + tdsh;
+                    if (tsw == 1) tm = (trav < tm) ? trav : tm;
+                    else { tm = trav; tsw = 1; }
+                }
+            }
+        }
+        if (pass == 0) {
+            travmt = tm;
+            if (travmt != 0) travmt = (travmt < travmd) ? travmt : travmd;
+            else travmt = travmd;
+        } else {
+            travms = tm;
+            if (travms != 0) travms = (travmt < travms) ? travmt : travms;
+            else travms = travmt;
+        }
+    }
+#undef JV
+#undef KV
+    double cur = f.tt(iz, ix);
+    if (cur != 0) travms = (travms < cur) ? travms : cur;
+    return travms;
+#undef N_
+#undef T_
+}
+
+
+template <class F>
+AF_DEV double update(const F& f, const DevModel& M, const CellMat& cm, long iz, long ix, double dnx, long nnz,
+                     long nnx) {
+#define N_(z, x) f.st((z), (x))
+#define T_(z, x) f.tt((z), (x))
+    int sp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (ix > 1) { if (N_(iz, ix - 2) >= 0) sp[3]++; }
+    if (ix > 0) {
+        if (N_(iz, ix - 1) >= 0) { sp[4]++; sp[7]++; }
+        if (iz > 0) { if (N_(iz - 1, ix - 1) >= 0) { sp[0]++; sp[3]++; sp[4]++; } }
+        if (iz < nnz - 1) { if (N_(iz + 1, ix - 1) >= 0) { sp[2]++; sp[3]++; sp[7]++; } }
+    }
+    if (ix < nnx - 2) { if (N_(iz, ix + 2) >= 0) sp[1]++; }
+    if (ix < nnx - 1) {
+        if (N_(iz, ix + 1) >= 0) { sp[5]++; sp[6]++; }
+        if (iz > 0) { if (N_(iz - 1, ix + 1) >= 0) { sp[0]++; sp[1]++; sp[5]++; } }
+        if (iz < nnz - 1) { if (N_(iz + 1, ix + 1) >= 0) { sp[1]++; sp[2]++; sp[6]++; } }
+    }
+    if (iz > 1) { if (N_(iz - 2, ix) >= 0) sp[0]++; }
+    if (iz > 0) { if (N_(iz - 1, ix) >= 0) { sp[4]++; sp[5]++; } }
+    if (iz < nnz - 2) { if (N_(iz + 2, ix) >= 0) sp[2]++; }
+    if (iz < nnz - 1) { if (N_(iz + 1, ix) >= 0) { sp[6]++; sp[7]++; } }
+
+    int sno = -1;
+    double min_diff = 1000000.0, diff;
+    if (sp[0] == 3) { diff = fabs(T_(iz - 1, ix - 1) - T_(iz - 1, ix + 1)); if (diff < min_diff) { sno = 0; min_diff = diff; } }
+    if (sp[1] == 3) { diff = fabs(T_(iz - 1, ix + 1) - T_(iz + 1, ix + 1)); if (diff < min_diff) { sno = 1; min_diff = diff; } }
+    if (sp[2] == 3) { diff = fabs(T_(iz + 1, ix - 1) - T_(iz + 1, ix + 1)); if (diff < min_diff) { sno = 2; min_diff = diff; } }
+    if (sp[3] == 3) { diff = fabs(T_(iz - 1, ix - 1) - T_(iz + 1, ix - 1)); if (diff < min_diff) { sno = 3; min_diff = diff; } }
+    if (sp[4] == 3) { diff = fabs(T_(iz, ix - 1) - T_(iz - 1, ix)); if (diff < min_diff) { sno = 4; min_diff = diff; } }
+    if (sp[5] == 3) { diff = fabs(T_(iz - 1, ix) - T_(iz, ix + 1)); if (diff < min_diff) { sno = 5; min_diff = diff; } }
+    if (sp[6] == 3) { diff = fabs(T_(iz + 1, ix) - T_(iz, ix + 1)); if (diff < min_diff) { sno = 6; min_diff = diff; } }
+    if (sp[7] == 3) { diff = fabs(T_(iz, ix - 1) - T_(iz + 1, ix)); if (diff < min_diff) { sno = 7; min_diff = diff; } }
+
+    double angle = 0.0, dist = -1.0, wt = 0.0;
+    /* wavefront_angle_dist is evaluated once, after stencil selection, on the parameters of the
+       stencil that the reference's last wavefront_angle_dist call would use (same result, one
+       inlined instance instead of 32: keeps the kernels free of register spills) */
+    bool have_w = false;
+    long wx1 = 0, wx2 = 0, wx3 = 0, wz1 = 0, wz2 = 0, wz3 = 0;
+    double wy1 = 0, wy2 = 0, wy3 = 0;
+#define SETW(a1, a2, a3, b1, b2, b3, c1, c2, c3) \
+    do { wx1 = (a1); wx2 = (a2); wx3 = (a3); wz1 = (b1); wz2 = (b2); wz3 = (b3); \
+         wy1 = (c1); wy2 = (c2); wy3 = (c3); have_w = true; } while (0)
+    if (sno != -1) {
+        /* square stencils :1039-1143 (both nsts sub-branches of stencils 0-3 are identical) */
+        switch (sno) {
+        case 0:
+            if (T_(iz - 1, ix - 1) < T_(iz - 1, ix + 1)) {
+                SETW(ix, ix - 1, ix + 1, iz - 2, iz - 1, iz - 1, T_(iz - 2, ix), T_(iz - 1, ix - 1), T_(iz - 1, ix + 1));
+                wt = T_(iz - 1, ix - 1);
+            } else {
+                SETW(ix, ix + 1, ix - 1, iz - 2, iz - 1, iz - 1, T_(iz - 2, ix), T_(iz - 1, ix + 1), T_(iz - 1, ix - 1));
+                wt = T_(iz - 1, ix + 1);
+            }
+            break;
+        case 1:
+            if (T_(iz - 1, ix + 1) < T_(iz + 1, ix + 1)) {
+                SETW(ix + 2, ix + 1, ix + 1, iz, iz - 1, iz + 1, T_(iz, ix + 2), T_(iz - 1, ix + 1), T_(iz + 1, ix + 1));
+                wt = T_(iz - 1, ix + 1);
+            } else {
+                SETW(ix + 2, ix + 1, ix + 1, iz, iz + 1, iz - 1, T_(iz, ix + 2), T_(iz + 1, ix + 1), T_(iz - 1, ix + 1));
+                wt = T_(iz + 1, ix + 1);
+            }
+            break;
+        case 2:
+            if (T_(iz + 1, ix - 1) < T_(iz + 1, ix + 1)) {
+                SETW(ix, ix - 1, ix + 1, iz + 2, iz + 1, iz + 1, T_(iz + 2, ix), T_(iz + 1, ix - 1), T_(iz + 1, ix + 1));
+                wt = T_(iz + 1, ix - 1);
+            } else {
+                SETW(ix, ix + 1, ix - 1, iz + 2, iz + 1, iz + 1, T_(iz + 2, ix), T_(iz + 1, ix + 1), T_(iz + 1, ix - 1));
+                wt = T_(iz + 1, ix + 1);
+            }
+            break;
+        case 3:
+            if (T_(iz - 1, ix - 1) < T_(iz + 1, ix - 1)) {
+                SETW(ix - 2, ix - 1, ix - 1, iz, iz - 1, iz + 1, T_(iz, ix - 2), T_(iz - 1, ix - 1), T_(iz + 1, ix - 1));
+                wt = T_(iz - 1, ix - 1);
+            } else {
+                SETW(ix - 2, ix - 1, ix - 1, iz, iz + 1, iz - 1, T_(iz, ix - 2), T_(iz + 1, ix - 1), T_(iz - 1, ix - 1));
+                wt = T_(iz + 1, ix - 1);
+            }
+            break;
+        case 4:
+            if (T_(iz, ix - 1) < T_(iz - 1, ix)) {
+                SETW(ix - 1, ix - 1, ix, iz - 1, iz, iz - 1, T_(iz - 1, ix - 1), T_(iz, ix - 1), T_(iz - 1, ix));
+                wt = T_(iz, ix - 1);
+            } else {
+                SETW(ix - 1, ix, ix - 1, iz - 1, iz - 1, iz, T_(iz - 1, ix - 1), T_(iz - 1, ix), T_(iz, ix - 1));
+                wt = T_(iz - 1, ix);
+            }
+            break;
+        case 5:
+            if (T_(iz - 1, ix) < T_(iz, ix + 1)) {
+                SETW(ix + 1, ix, ix + 1, iz - 1, iz - 1, iz, T_(iz - 1, ix + 1), T_(iz - 1, ix), T_(iz, ix + 1));
+                wt = T_(iz - 1, ix);
+            } else {
+                SETW(ix + 1, ix + 1, ix, iz - 1, iz, iz - 1, T_(iz - 1, ix + 1), T_(iz, ix + 1), T_(iz - 1, ix));
+                wt = T_(iz, ix + 1);
+            }
+            break;
+        case 6:
+            if (T_(iz + 1, ix) < T_(iz, ix + 1)) {
+                SETW(ix + 1, ix, ix + 1, iz + 1, iz + 1, iz, T_(iz + 1, ix + 1), T_(iz + 1, ix), T_(iz, ix + 1));
+                wt = T_(iz + 1, ix);
+            } else {
+                SETW(ix + 1, ix + 1, ix, iz + 1, iz, iz + 1, T_(iz + 1, ix + 1), T_(iz, ix + 1), T_(iz + 1, ix));
+                wt = T_(iz, ix + 1);
+            }
+            break;
+        case 7:
+            if (T_(iz, ix - 1) < T_(iz + 1, ix)) {
+                SETW(ix - 1, ix - 1, ix, iz + 1, iz, iz + 1, T_(iz + 1, ix - 1), T_(iz, ix - 1), T_(iz + 1, ix));
+                wt = T_(iz, ix - 1);
+            } else {
+                SETW(ix - 1, ix, ix - 1, iz + 1, iz + 1, iz, T_(iz + 1, ix - 1), T_(iz + 1, ix), T_(iz, ix - 1));
+                wt = T_(iz + 1, ix);
+            }
+            break;
+        }
+    }
+
+    if (sno == -1 || ix == 0 || ix == nnx - 1 || iz == 0 || iz == nnz - 1) {
+        /* triangular stencils :1146-1366 */
+        int tp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (ix > 1) { if (N_(iz, ix - 2) >= 0) { tp[4]++; tp[7]++; } }
+        if (ix > 0) {
+            if (N_(iz, ix - 1) >= 0) { tp[4]++; tp[7]++; }
+            if (iz > 0) { if (N_(iz - 1, ix - 1) >= 0) { tp[2]++; tp[7]++; } }
+            if (iz < nnz - 1) { if (N_(iz + 1, ix - 1) >= 0) { tp[3]++; tp[4]++; } }
+        }
+        if (ix < nnx - 2) { if (N_(iz, ix + 2) >= 0) { tp[5]++; tp[6]++; } }
+        if (ix < nnx - 1) {
+            if (N_(iz, ix + 1) >= 0) { tp[5]++; tp[6]++; }
+            if (iz > 0) { if (N_(iz - 1, ix + 1) >= 0) { tp[1]++; tp[6]++; } }
+            if (iz < nnz - 1) { if (N_(iz + 1, ix + 1) >= 0) { tp[0]++; tp[5]++; } }
+        }
+        if (iz > 1) { if (N_(iz - 2, ix) >= 0) { tp[1]++; tp[2]++; } }
+        if (iz > 0) { if (N_(iz - 1, ix) >= 0) { tp[1]++; tp[2]++; } }
+        if (iz < nnz - 2) { if (N_(iz + 2, ix) >= 0) { tp[0]++; tp[3]++; } }
+        if (iz < nnz - 1) { if (N_(iz + 1, ix) >= 0) { tp[0]++; tp[3]++; } }
+
+        if (sno == -1) min_diff = 1000000.0;
+        sno = -2;
+        const double s2m1 = sqrt(2.0) - 1, tms2 = 2 - sqrt(2.0);
+#define TRI(id, ca, cb, cc)                                                                   \
+    if (tp[id] == 3) {                                                                        \
+        double A_ = (ca), B_ = (cb), C_ = (cc);                                               \
+        if (A_ < ((B_ < C_) ? B_ : C_)) {                                                     \
+            diff = fabs(s2m1 * A_ + tms2 * B_ - C_);                                          \
+            if (diff < min_diff) { sno = id; min_diff = diff; }                               \
+        }                                                                                     \
+    }
+        TRI(0, T_(iz + 2, ix), T_(iz + 1, ix), T_(iz + 1, ix + 1))
+        TRI(1, T_(iz - 2, ix), T_(iz - 1, ix), T_(iz - 1, ix + 1))
+        TRI(2, T_(iz - 2, ix), T_(iz - 1, ix), T_(iz - 1, ix - 1))
+        TRI(3, T_(iz + 2, ix), T_(iz + 1, ix), T_(iz + 1, ix - 1))
+        TRI(4, T_(iz, ix - 2), T_(iz, ix - 1), T_(iz + 1, ix - 1))
+        TRI(5, T_(iz, ix + 2), T_(iz, ix + 1), T_(iz + 1, ix + 1))
+        TRI(6, T_(iz, ix + 2), T_(iz, ix + 1), T_(iz - 1, ix + 1))
+        TRI(7, T_(iz, ix - 2), T_(iz, ix - 1), T_(iz - 1, ix - 1))
+#undef TRI
+        /* NOTE: the reference's min(b, c) for the guard: numba min(b,c) -> b if not (c < b) */
+        if (sno != -2) {
+            switch (sno) {
+            case 0:
+                if (T_(iz + 1, ix) < T_(iz + 1, ix + 1)) {
+                    if (ix == 0) { angle = 90.; dist = 1.; have_w = false; }
+                    else SETW(ix, ix, ix + 1, iz + 2, iz + 1, iz + 1, T_(iz + 2, ix), T_(iz + 1, ix), T_(iz + 1, ix + 1));
+                } else {
+                    SETW(ix, ix + 1, ix, iz + 2, iz + 1, iz + 1, T_(iz + 2, ix), T_(iz + 1, ix + 1), T_(iz + 1, ix));
+                }
+                wt = T_(iz + 1, ix + 1); /* SURVEY B-D15 */
+                break;
+            case 1:
+                if (T_(iz - 1, ix) < T_(iz - 1, ix + 1)) {
+                    if (ix == 0) { angle = 90.; dist = 1.; have_w = false; }
+                    else SETW(ix, ix, ix + 1, iz - 2, iz - 1, iz - 1, T_(iz - 2, ix), T_(iz - 1, ix), T_(iz - 1, ix + 1));
+                    wt = T_(iz - 1, ix);
+                } else {
+                    SETW(ix, ix + 1, ix, iz - 2, iz - 1, iz - 1, T_(iz - 2, ix), T_(iz - 1, ix + 1), T_(iz - 1, ix));
+                    wt = T_(iz - 1, ix + 1);
+                }
+                break;
+            case 2:
+                if (T_(iz - 1, ix) < T_(iz - 1, ix - 1)) {
+                    if (ix == nnx - 1) { angle = 90.; dist = 1.; have_w = false; }
+                    else SETW(ix, ix, ix - 1, iz - 2, iz - 1, iz - 1, T_(iz - 2, ix), T_(iz - 1, ix), T_(iz - 1, ix - 1));
+                    wt = T_(iz - 1, ix);
+                } else {
+                    SETW(ix, ix - 1, ix, iz - 2, iz - 1, iz - 1, T_(iz - 2, ix), T_(iz - 1, ix - 1), T_(iz - 1, ix));
+                    wt = T_(iz - 1, ix - 1);
+                }
+                break;
+            case 3:
+                if (T_(iz + 1, ix) < T_(iz + 1, ix - 1)) {
+                    if (ix == nnx - 1) { angle = 90.; dist = 1.; have_w = false; }
+                    else SETW(ix, ix, ix - 1, iz + 2, iz + 1, iz + 1, T_(iz + 2, ix), T_(iz + 1, ix), T_(iz + 1, ix - 1));
+                    wt = T_(iz + 1, ix);
+                } else {
+                    SETW(ix, ix - 1, ix, iz + 2, iz + 1, iz + 1, T_(iz + 2, ix), T_(iz + 1, ix - 1), T_(iz + 1, ix));
+                    wt = T_(iz + 1, ix - 1);
+                }
+                break;
+            case 4:
+                if (T_(iz, ix - 1) < T_(iz + 1, ix - 1)) {
+                    if (iz == 0) { angle = 0.; dist = 1.; have_w = false; }
+                    else SETW(ix - 2, ix - 1, ix - 1, iz, iz, iz + 1, T_(iz, ix - 2), T_(iz, ix - 1), T_(iz + 1, ix - 1));
+                    wt = T_(iz, ix - 1);
+                } else {
+                    SETW(ix - 2, ix - 1, ix - 1, iz, iz + 1, iz, T_(iz, ix - 2), T_(iz + 1, ix - 1), T_(iz, ix - 1));
+                    wt = T_(iz + 1, ix - 1);
+                }
+                break;
+            case 5:
+                if (T_(iz, ix + 1) < T_(iz + 1, ix + 1)) {
+                    if (iz == 0) { angle = 0.; dist = 1.; have_w = false; }
+                    else SETW(ix + 2, ix + 1, ix + 1, iz, iz, iz + 1, T_(iz, ix + 2), T_(iz, ix + 1), T_(iz + 1, ix + 1));
+                    wt = T_(iz, ix + 1);
+                } else {
+                    SETW(ix + 2, ix + 1, ix + 1, iz, iz + 1, iz, T_(iz, ix + 2), T_(iz + 1, ix + 1), T_(iz, ix + 1));
+                    wt = T_(iz + 1, ix + 1);
+                }
+                break;
+            case 6:
+                if (T_(iz, ix + 1) < T_(iz - 1, ix + 1)) {
+                    if (iz == nnz - 1) { angle = 0.; dist = 1.; have_w = false; }
+                    else SETW(ix + 2, ix + 1, ix + 1, iz, iz, iz - 1, T_(iz, ix + 2), T_(iz, ix + 1), T_(iz - 1, ix + 1));
+                    wt = T_(iz, ix + 1);
+                } else {
+                    SETW(ix + 2, ix + 1, ix + 1, iz, iz - 1, iz, T_(iz, ix + 2), T_(iz - 1, ix + 1), T_(iz, ix + 1));
+                    wt = T_(iz - 1, ix + 1);
+                }
+                break;
+            case 7:
+                if (T_(iz, ix - 1) < T_(iz - 1, ix - 1)) {
+                    if (iz == nnz - 1) { angle = 0.; dist = 1.; have_w = false; }
+                    else SETW(ix - 2, ix - 1, ix - 1, iz, iz, iz - 1, T_(iz, ix - 2), T_(iz, ix - 1), T_(iz - 1, ix - 1));
+                    wt = T_(iz, ix - 1);
+                } else {
+                    SETW(ix - 2, ix - 1, ix - 1, iz, iz - 1, iz, T_(iz, ix - 2), T_(iz - 1, ix - 1), T_(iz, ix - 1));
+                    wt = T_(iz - 1, ix - 1);
+                }
+                break;
+            }
+            sno += 8;
+        }
+    }
+    if (have_w) wad(ix, iz, wx1, wx2, wx3, wz1, wz2, wz3, wy1, wy2, wy3, angle, dist);
+#undef SETW
+    if (dist != -1.0) {
+        double effa = pymod(cm.veln - angle, 180);
+        double velocity;
+        if (cm.velpn != 0 || cm.stif == nullptr) velocity = table_vel(M.ptab, M.ncol, effa, cm.velpn, cm.vm);
+        else velocity = christoffel_phase(cm.stif, effa, cm.vm);
+        return wt + (dist * dnx / velocity);
+    }
+    return -1.0;
+#undef N_
+#undef T_
+}
+
+
+}  // namespace af

@@ -1,0 +1,240 @@
+// rays.hip — plane-search ray back-trace find_ray (Anis_TTF_rays.py:3104-3465) on gfx950.
+//
+// One 64-lane wavefront per ray.  Each step is wave-uniform except the candidate evaluation:
+// lane i evaluates candidate i of the plane (6*sg+3 candidates on axis planes, <= 5*sg+3 on
+// diagonal planes), i.e. rec_TTF at the candidate plus the straight-segment time
+// time_between_points (:2835-2989, a DDA over coarse cells).  The parabolic local-minimum search
+// (:3192-3218) is a lexicographic (value, order) wave reduction, which selects exactly the
+// candidate the reference's sequential strict-'<' scan selects.  ray_time (:2992-3022) is
+// accumulated segment by segment as the ray grows, i.e. in the reference's summation order, so
+// times match the CPU to the last bit
+// except where ocml's atan/tan/sin/cos differ from glibc.  All arithmetic is double precision.
+#include "kernels.h"
+
+namespace af {
+
+
+
+constexpr int kRayWaves = 4;
+constexpr int kMaxCand = 256;
+
+struct Key {
+  double v;
+  int order;
+  double pos;
+};
+AF_DEV bool key_less(const Key& a, const Key& b) { return a.v < b.v || (a.v == b.v && a.order < b.order); }
+
+__global__ __launch_bounds__(64 * kRayWaves) void find_ray_kernel(RayParams P) {
+  __shared__ double TTs[kRayWaves][kMaxCand];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int ray = blockIdx.x * kRayWaves + w;
+  if (ray >= P.nrays) return;
+  const RayJob J = P.jobs[ray];
+  const int sg = P.sg;
+  const long sd = 3L * sg + 1, sd2 = 2L * sg + 1;
+  const long nnx = P.fnz, nnz = P.fnx;  // reference naming (:3151-3152)
+  double* rxo = P.ray_x + (long)ray * P.max_pts;
+  double* ryo = P.ray_y + (long)ray * P.max_pts;
+  double* TT = TTs[w];
+  long cap = 5L * (P.M.nz0 + P.M.nx0);
+  if (cap > P.max_pts) cap = P.max_pts;
+  const double recx = J.rx, recy = J.ry;
+  double last_x = J.sx, last_y = J.sy;
+  double lvx = recx - J.sx, lvy = recy - J.sy;
+  long ray_len = 1;
+  int flags = 0;
+  double tt = 0.0;  // ray_time :2992-3022, accumulated segment by segment in the reference's order
+  if (lane == 0) {
+    rxo[0] = J.sx;
+    ryo[0] = J.sy;
+  }
+#define RT(r, c) J.ttf[(long)(r) * P.fnx + (long)(c)]
+  while ((last_x - recx) * (last_x - recx) + (last_y - recy) * (last_y - recy) > (1.6 * sg) * (1.6 * sg)) {
+    if ((last_x - recx) * (last_x - recx) + (last_y - recy) * (last_y - recy) < (double)(4 * sg) * (4 * sg)) {
+      lvx = recx - last_x;
+      lvy = recy - last_y;
+    }
+    if (ray_len + 1 >= cap) {
+      flags |= 2;
+      break;
+    }
+    double cand[4] = {fabs(lvx), fabs(lvx + lvy) / sqrt(2.0), fabs(lvy), fabs(lvx - lvy) / sqrt(2.0)};
+    int dir = 0;
+    for (int q = 1; q < 4; q++)
+      if (cand[q] > cand[dir]) dir = q;
+    long rlx = pyround(last_x), rly = pyround(last_y);
+    long c_value = 0, base0 = 0, n = 0;
+    bool stop = false;
+    if (dir == 0) {
+      c_value = rlx + (lvx > 0 ? sg : -sg);
+      if (c_value < 0 || c_value >= nnz) stop = true;
+      long mn = max(0L, rly - sd), mx = min(nnx - 1, rly + sd);
+      base0 = mn;
+      n = mx - mn + 1;
+    } else if (dir == 1) {
+      c_value = rlx + rly;
+      long mn, mx;
+      if (lvx > 0) {
+        c_value += sg;
+        mn = max(max(0L, c_value - (nnx - 1)), rlx - sd2);
+        mx = min(min(nnz - 1, c_value), c_value - rly + sd2);
+      } else {
+        c_value -= sg;
+        mn = max(max(0L, c_value - (nnx - 1)), c_value - rly - sd2);
+        mx = min(min(nnz - 1, c_value), rlx + sd2);
+      }
+      base0 = mn;
+      n = mx - mn + 1;
+    } else if (dir == 2) {
+      c_value = rly + (lvy > 0 ? sg : -sg);
+      if (c_value < 0 || c_value >= nnx) stop = true;
+      long mn = max(0L, rlx - sd), mx = min(nnz - 1, rlx + sd);
+      base0 = mn;
+      n = mx - mn + 1;
+    } else {
+      c_value = rly - rlx;
+      long mn, mx;
+      if (lvx < 0) {
+        c_value += sg;
+        mn = max(max(0L, -c_value), rly - c_value - sd2);
+        mx = min(min(nnz - 1, (nnx - 1) - c_value), rlx + sd2);
+      } else {
+        c_value -= sg;
+        mn = max(max(0L, -c_value), rlx - sd2);
+        mx = min(min(nnz - 1, (nnx - 1) - c_value), rly - c_value + sd2);
+      }
+      base0 = mn;
+      n = mx - mn + 1;
+    }
+    if (stop) break;
+    if (n <= 0 || n > kMaxCand) {
+      flags |= 4;
+      break;
+    }
+    // candidates across lanes
+    for (long i0 = 0; i0 < n; i0 += 64) {
+      long i = i0 + lane;
+      if (i < n) {
+        double t;
+        if (dir == 0) {
+          long xv = i + base0;
+          t = RT(xv, c_value) + tbp(P.M, last_x, (double)c_value, last_y, (double)xv, P.dnx, sg);
+        } else if (dir == 1) {
+          long xc = base0 + i, yc = -xc + c_value;
+          t = RT(yc, xc) + tbp(P.M, last_x, (double)xc, last_y, (double)yc, P.dnx, sg);
+        } else if (dir == 2) {
+          long yv = i + base0;
+          t = RT(c_value, yv) + tbp(P.M, last_x, (double)yv, last_y, (double)c_value, P.dnx, sg);
+        } else {
+          long xc = base0 + i, yc = xc + c_value;
+          t = RT(yc, xc) + tbp(P.M, last_x, (double)xc, last_y, (double)yc, P.dnx, sg);
+        }
+        TT[i] = t;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    // local minima (:3192-3218): init key (order 0) + each strict parabola minimum (order j)
+    Key best;
+    if (TT[0] < TT[n - 1]) best = Key{TT[0], 0, 0.0};
+    else best = Key{TT[n - 1], 0, (double)(n - 1)};
+    for (long j0 = 1; j0 < n - 1; j0 += 64) {
+      long j = j0 + lane;
+      if (j < n - 1) {
+        double t1 = TT[j - 1], t2 = TT[j], t3 = TT[j + 1];
+        if (t1 >= t2 && t2 <= t3) {
+          double a = (t1 + t3 - 2 * t2) / 2;
+          double b = (t3 - t1) / 2;
+          double c = t2;
+          double pos, lmv;
+          if (a != 0) {
+            pos = -b / (2 * a);
+            lmv = a * (pos * pos) + b * pos + c;
+            pos += (double)j;
+          } else {
+            pos = (double)j;
+            lmv = t2;
+          }
+          Key k{lmv, (int)j, pos};
+          if (key_less(k, best)) best = k;
+        }
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      Key other{__shfl_xor(best.v, o), __shfl_xor(best.order, o), __shfl_xor(best.pos, o)};
+      if (key_less(other, best)) best = other;
+    }
+    const double min_i = best.pos;
+    double nx_, ny_;
+    if (dir == 0) {
+      nx_ = (double)c_value;
+      ny_ = min_i + (double)base0;
+    } else if (dir == 1) {
+      nx_ = (double)base0 + min_i;
+      ny_ = (double)c_value - nx_;
+    } else if (dir == 2) {
+      nx_ = min_i + (double)base0;
+      ny_ = (double)c_value;
+    } else {
+      nx_ = (double)base0 + min_i;
+      ny_ = nx_ + (double)c_value;
+    }
+    if (RT(pyround(last_y), pyround(last_x)) < RT(pyround(ny_), pyround(nx_))) {
+      flags |= 1;  // "Travel time to receiver increasing: Finishing ray early" (:3406-3407)
+      break;
+    }
+    if (lane == 0) {
+      rxo[ray_len] = nx_;
+      ryo[ray_len] = ny_;
+    }
+    tt += tbp(P.M, last_x, nx_, last_y, ny_, P.dnx, sg);  // wave-uniform
+    lvx = nx_ - last_x;
+    last_x = nx_;
+    lvy = ny_ - last_y;
+    last_y = ny_;
+    ray_len += 1;
+    __builtin_amdgcn_wave_barrier();
+  }
+#undef RT
+  if (lane == 0) {
+    rxo[ray_len] = recx;
+    ryo[ray_len] = recy;
+  }
+  const long npts = ray_len + 1;
+  tt += tbp(P.M, last_x, recx, last_y, recy, P.dnx, sg);
+  if (lane == 0) {
+    P.times[ray] = tt;
+    P.ray_len[ray] = (int)npts;
+    P.flags[ray] = flags;
+  }
+}
+
+}  // namespace af
+
+namespace af {
+// pack per-ray point slots into one interleaved (x, z) buffer at host-computed offsets
+__global__ void pack_rays_kernel(const double* rx, const double* ry, const int* len, const long long* off, int max_pts,
+                                 double* packed) {
+  const int ray = blockIdx.x;
+  const int n = len[ray];
+  const long long o = off[ray];
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    packed[2 * (o + i)] = rx[(long)ray * max_pts + i];
+    packed[2 * (o + i) + 1] = ry[(long)ray * max_pts + i];
+  }
+}
+}  // namespace af
+
+extern "C" hipError_t af_launch_pack_rays(const double* rx, const double* ry, const int* len, const long long* off,
+                                          int nrays, int max_pts, double* packed, hipStream_t stream) {
+  if (nrays <= 0) return hipSuccess;
+  hipLaunchKernelGGL(af::pack_rays_kernel, dim3(nrays), dim3(256), 0, stream, rx, ry, len, off, max_pts, packed);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t af_launch_rays(const af::RayParams* P, hipStream_t stream) {
+  int blocks = (P->nrays + af::kRayWaves - 1) / af::kRayWaves;
+  hipLaunchKernelGGL(af::find_ray_kernel, dim3(blocks), dim3(64 * af::kRayWaves), 0, stream, *P);
+  return hipGetLastError();
+}

@@ -1,0 +1,65 @@
+// utils.hip — batched evaluation of single device functions (module-level API of the drop-in
+// Anis_TTF_rays.py and device-level parity tests):
+//   update() / fouds18_A() on independent caller-supplied neighbourhoods (:904-1410, :240-901)
+//   time_between_points() on the resident model (:2835-2989)
+#include "kernels.h"
+#include "local_ops.h"
+
+namespace af {
+
+struct PatchField {  // caller patch; rows past pz read as nsts=-1 / ttn=0 (padded semantics)
+  const double* T;
+  const int* S;
+  int nz, nx;
+  AF_DEV int st(long z, long x) const { return z >= nz ? -1 : S[z * nx + x]; }
+  AF_DEV double tt(long z, long x) const { return z >= nz ? 0.0 : T[z * nx + x]; }
+};
+
+__global__ void local_ops_kernel(LocalOpsParams P) {
+  long k = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= P.n) return;
+  const long pn = (long)P.pz * P.px;
+  PatchField F{P.ttn + k * pn, P.nsts + k * pn, P.pz, P.px};
+  DevModel M;
+  M.nz0 = 1;
+  M.nx0 = 1;
+  M.veln = P.cveln + k;
+  M.velpn = P.cvelpn + k;
+  M.vm = P.cvm + k;
+  M.sidx = nullptr;
+  M.stab = nullptr;
+  M.gtab = P.tab;
+  M.ptab = P.tab;
+  M.ncol = P.ncol;
+  CellMat cm;
+  cm.veln = P.cveln[k];
+  cm.vm = P.cvm[k];
+  cm.velpn = P.cvelpn[k];
+  cm.stif = P.cstif ? P.cstif + 5 * k : nullptr;
+  double v;
+  if (P.op == 0)
+    v = update(F, M, cm, P.iz[k], P.ix[k], P.dnx[k], P.nnz_arg[k], P.nnx_arg[k]);
+  else
+    v = fouds18(F, M, cm, P.iz[k], P.ix[k], P.dnx[k], P.dnz[k], P.nnx_arg[k], P.nnz_arg[k]);
+  P.out[k] = v;
+}
+
+__global__ void tbp_kernel(DevModel M, int n, const double* x1, const double* x2, const double* y1, const double* y2,
+                           double dnx, int sg, double* out) {
+  int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  out[k] = tbp(M, x1[k], x2[k], y1[k], y2[k], dnx, sg);
+}
+
+}  // namespace af
+
+extern "C" hipError_t af_launch_local_ops(const af::LocalOpsParams* P, hipStream_t stream) {
+  hipLaunchKernelGGL(af::local_ops_kernel, dim3((P->n + 63) / 64), dim3(64), 0, stream, *P);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t af_launch_tbp(const af::DevModel* M, int n, const double* x1, const double* x2, const double* y1,
+                                    const double* y2, double dnx, int sg, double* out, hipStream_t stream) {
+  hipLaunchKernelGGL(af::tbp_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, *M, n, x1, x2, y1, y2, dnx, sg, out);
+  return hipGetLastError();
+}

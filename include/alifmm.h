@@ -1,0 +1,109 @@
+/* alifmm.h — C-ABI of libalifmm.so, the MI355X (gfx950) ALI-FMM travel-time-field solver and
+ * ray tracer.  Drop-in boundary for the hot path of the reference module Anis_TTF_rays.py
+ * (WiPi-UoS/ALI-FMM-and-ray-tracing); each entry point names the reference interface it replaces.
+ *
+ * Conventions: every function returns 0 on success and a negative code on failure, with the
+ * message available from alifmm_last_error(ctx).  Host buffers are caller-owned, C-contiguous,
+ * row-major [iz][ix] (the reference's numpy layout).  Device memory is library-owned.  Calls are
+ * synchronous (they return after their device work and any device->host copy completed).
+ * One context drives one GPU; a context is not re-entrant (one host thread per context).
+ */
+#ifndef ALIFMM_H
+#define ALIFMM_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct alifmm_ctx alifmm_ctx;
+
+enum {
+  ALIFMM_OK = 0,
+  ALIFMM_E_HIP = -1,      /* HIP runtime error (device missing, out of memory, launch failure) */
+  ALIFMM_E_ARG = -2,      /* invalid argument (shape, source outside the grid, no model) */
+  ALIFMM_E_CAPACITY = -3, /* a device work list overflowed even after the automatic retry */
+  ALIFMM_E_KERNEL = -4    /* a kernel reported an internal error (init heap overflow, ...) */
+};
+
+const char* alifmm_version(void);
+int alifmm_device_count(int* n);
+
+/* Create a context on HIP device `device` (index into the visible devices). */
+int alifmm_ctx_create(int device, alifmm_ctx** out);
+int alifmm_ctx_destroy(alifmm_ctx* ctx);
+const char* alifmm_last_error(alifmm_ctx* ctx);
+
+/* Upload the model (replaces the model arrays handed to travel()/travel_finer_grid()/find_ray():
+ * Anis_TTF_rays.py:1464, :2121, :3105; stored by ALI_FMM.__init__ :3793-3862).
+ *   veln     (nnz, nnx) float64  orientation [deg]
+ *   velpn    (nnz, nnx) int64    material column; 0 selects the per-cell stiffness
+ *   vel_map  (nnz, nnx) float64  velocity scale
+ *   stif_den (nnz, nnx, 5) int64 c22, c23, c33, c44 [MPa], density [kg/m^3]; NULL = None
+ *   group_tab, phase_tab (361, ncol) float64  velocity tables (ALI_FMM.velocity_dat / phase_vel)
+ *   dnx, dnz grid spacing [m]; gox, goz origin [m]                                            */
+int alifmm_set_model(alifmm_ctx* ctx, int nnz, int nnx, const double* veln, const int64_t* velpn,
+                     const double* vel_map, const int64_t* stif_den, const double* group_tab,
+                     const double* phase_tab, int ncol, double dnx, double dnz, double gox, double goz);
+
+/* Tuning: "cdelta" (band width in units of dnx/vmax, default 0.5), "r0" (near-source band
+ * schedule radius in cells, default 40), "exact_r" (radius in cells of the exact heap-ordered
+ * main-loop prefix for subgrid 1, 0..48, default 40), "batch" (sources per launch, default 256). */
+int alifmm_set_option(alifmm_ctx* ctx, const char* name, double value);
+
+/* Shape of a travel-time field for subgrid size sg: (sg*(nnz-1)+1, sg*(nnx-1)+1). */
+int alifmm_field_shape(alifmm_ctx* ctx, int subgrid, int* fnz, int* fnx);
+
+/* First-arrival travel-time fields for nsrc sources (scx, scz in metres).
+ * Replaces travel() :1463-2117 (subgrid == 1) and travel_finer_grid() :2120-2832 (subgrid > 1,
+ * odd; the result is already divided by subgrid as at :2832).  The fields stay resident on the
+ * device in slots first_slot .. first_slot+nsrc-1 (for alifmm_find_rays); if out != NULL they are
+ * also copied to out (nsrc x fnz x fnx float64).  Field semantics: SURVEY/DESIGN parity contract. */
+int alifmm_travel(alifmm_ctx* ctx, int subgrid, int nsrc, const double* scx, const double* scz,
+                  int first_slot, double* out);
+
+/* Copy a resident field to the host; release all resident fields. */
+int alifmm_get_field(alifmm_ctx* ctx, int slot, double* out);
+int alifmm_release_fields(alifmm_ctx* ctx);
+
+/* Trace npairs rays (replaces find_ray() :3104-3465 incl. ray_time() :2992-3022).
+ *   field_slot[k]        resident field of the RECEIVER of ray k (its subgrid is used)
+ *   src_xy[2k], rec_xy[2k]  source / receiver (x, z) on that field's fine grid
+ *   times[k]             ray travel time [s]
+ *   ray_len[k]           number of points (>= 2)
+ *   flags[k]             bit0: reference's early exit ("Travel time to receiver increasing"),
+ *                        bit1: point capacity reached, bit2: empty candidate plane
+ *   ray_xy (nullable)    packed points: ray k's x at ray_xy[2*off[k] + 2*i], z at +1,
+ *                        off[k] = sum of ray_len[0..k-1]; capacity ray_xy_cap points.      */
+int alifmm_find_rays(alifmm_ctx* ctx, int npairs, const int32_t* field_slot, const double* src_xy,
+                     const double* rec_xy, double* times, int32_t* ray_len, int32_t* flags,
+                     double* ray_xy, int64_t ray_xy_cap);
+
+/* Diagnostics of the last alifmm_travel(): per slot band steps [stage1, stage2, stage3|-, main]
+ * and main-grid cell-sweeps (local-operator evaluations); device time of the last call's kernels. */
+int alifmm_source_stats(alifmm_ctx* ctx, int slot, int64_t* steps4, int64_t* cell_sweeps);
+int alifmm_last_timing(alifmm_ctx* ctx, double* init_ms, double* band_ms, double* total_ms);
+
+/* Upload a host travel-time field (fine grid of `subgrid`) into a slot, e.g. for find_ray() on a
+ * field computed elsewhere (find_ray's rec_TTF argument, :3105). */
+int alifmm_put_field(alifmm_ctx* ctx, int slot, int subgrid, const double* data);
+
+/* n straight-segment times on the resident model (time_between_points() :2835-2989; the
+ * coordinates are fine-grid indices of `subgrid`).  ray_time() (:2992-3022) = ordered sum. */
+int alifmm_time_between_points(alifmm_ctx* ctx, int n, const double* x1, const double* x2, const double* y1,
+                               const double* y2, int subgrid, double* out);
+
+/* Evaluate the local operators on n independent neighbourhoods (pz x px patches; rows past pz
+ * read as nsts=-1/ttn=0, the reference's padded stage-1 semantics).  op 0: update() :904-1410
+ * with the phase table; op 1: fouds18_A() :240-901 with the group table.  Material is given at
+ * the target cell only (the operators read nothing else); cell_stif (n x 5) NULL = None. */
+int alifmm_local_ops(alifmm_ctx* ctx, int op, int n, int pz, int px, const double* ttn, const int32_t* nsts,
+                     const int32_t* iz, const int32_t* ix, const double* dnx, const double* dnz,
+                     const int32_t* nnz_arg, const int32_t* nnx_arg, const double* cell_veln,
+                     const int64_t* cell_velpn, const double* cell_vm, const int64_t* cell_stif,
+                     const double* tab, int ncol, double* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ALIFMM_H */

@@ -859,6 +859,7 @@ typedef struct {
     const table_t *av, *ph;
     double dnx, dnz_fouds;
     int stage, isx_s, isz_s, max_dist, quirk_nnz;
+    double tstop; /* > 0: stop before popping a node with ttn >= tstop (band model prefix only) */
 } loopcfg_t;
 
 static void relax(fstate_t *f, const mat_t *m, const loopcfg_t *c, long iz, long ix, int is_xclose_quirk) {
@@ -873,6 +874,7 @@ static int fmm_loop(fstate_t *f, const mat_t *m, const loopcfg_t *c) {
     long nnx = f->nnx, nnz = f->nnz;
     while (f->ntr > 0 && !finished) {
         long ix = f->btg[3], iz = f->btg[2];
+        if (c->tstop > 0 && f->ttn[iz * nnx + ix] >= c->tstop) break;
         f->nsts[iz * nnx + ix] = 0;
         downtree(f);
         for (int s = 0; s < 2; s++) {
@@ -1035,7 +1037,7 @@ static int travel_impl(double scx, double scz, const mat_t *base, const table_t 
     long max_dist1 = sg1 * size1;
     straight_rays(&f1, isz_1, isx_1, side1, dnx1, base, (int)isz, (int)isx, av, 0);
     add_edges(&f1, isz_1, isx_1, side1);
-    loopcfg_t c1 = {av, ph, dnx1, dnx1, 1, (int)isx_1, (int)isz_1, (int)max_dist1, 1};
+    loopcfg_t c1 = {av, ph, dnx1, dnx1, 1, (int)isx_1, (int)isz_1, (int)max_dist1, 1, 0.0};
     if (fmm_loop(&f1, &v1.m, &c1)) rc = -1;
 
     /* ---- stage 2: 13x13 coarse window x9 ---- */

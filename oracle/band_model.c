@@ -68,48 +68,50 @@ static long band_run(bstate_t *b, const mat_t *m, const loopcfg_t *c, double del
                 b->L2[nL2++] = (int32_t)idx;
             }
         }
-        /* claim candidates (dedupe); window-edge finish test (reference :1651-1652, :1673-1674) */
-        long nC = 0;
-        for (long a = 0; a < nA; a++) {
-            long idx = b->A[a], iz = idx / nx, ix = idx % nx;
-            long nb[4][2] = {{iz, ix - 1}, {iz, ix + 1}, {iz - 1, ix}, {iz + 1, ix}};
-            for (int q = 0; q < 4; q++) {
-                long z = nb[q][0], x = nb[q][1];
-                if (z < 0 || z >= nz || x < 0 || x >= nx) {
-                    if (c->stage) {
-                        if (q < 2 && labs(c->isx_s - x) == c->max_dist + 1) finished = 1;
-                        if (q >= 2 && labs(c->isz_s - z) == c->max_dist + 1) finished = 1;
+        /* neighbours are visited in the reference's order (x-1, x+1, z-1, z+1; :2065-2102).  seq=1:
+           one sub-phase per direction, each committed before the next, so an update sees the
+           values its siblings of the same pop received earlier (sequential semantics for one pop);
+           seq=0: all four directions evaluated Jacobi-style against the post-acceptance state. */
+        int ndirph = sweeps >= 10 ? 4 : 1;
+        for (int ph = 0; ph < ndirph; ph++) {
+            long nC = 0;
+            for (long a = 0; a < nA; a++) {
+                long idx = b->A[a], iz = idx / nx, ix = idx % nx;
+                long nb[4][2] = {{iz, ix - 1}, {iz, ix + 1}, {iz - 1, ix}, {iz + 1, ix}};
+                for (int q = 0; q < 4; q++) {
+                    if (ndirph == 4 && q != ph) continue;
+                    long z = nb[q][0], x = nb[q][1];
+                    if (z < 0 || z >= nz || x < 0 || x >= nx) {
+                        if (c->stage) {
+                            if (q < 2 && labs(c->isx_s - x) == c->max_dist + 1) finished = 1;
+                            if (q >= 2 && labs(c->isz_s - z) == c->max_dist + 1) finished = 1;
+                        }
+                        continue;
                     }
-                    continue;
+                    long r = z * nx + x;
+                    int32_t s = f->nsts[r];
+                    if (b->accstep[r] == -2 - (int32_t)steps) continue; /* already updated this step */
+                    if (s == S_FAR) { f->nsts[r] = S_FARC; b->C[nC++] = (int32_t)r; }
+                    else if (s == S_CLOSE) { f->nsts[r] = S_CLOSEC; b->C[nC++] = (int32_t)r; }
                 }
-                long r = z * nx + x;
-                int32_t s = f->nsts[r];
-                if (s == S_FAR) { f->nsts[r] = S_FARC; b->C[nC++] = (int32_t)r; }
-                else if (s == S_CLOSE) { f->nsts[r] = S_CLOSEC; b->C[nC++] = (int32_t)r; }
             }
-        }
-        for (int sw = 0; sw < sweeps; sw++) {
             for (long k = 0; k < nC; k++) {
                 long r = b->C[k], iz = r / nx, ix = r % nx;
                 int quirk = 0;
-                if (c->quirk_nnz && (sw == 0 ? f->nsts[r] == S_CLOSEC : 1)) {
-                    /* stage-1 quirk (:1645): a close cell re-evaluated because an x-neighbour was popped */
+                if (c->quirk_nnz && f->nsts[r] == S_CLOSEC) {
                     if ((ix > 0 && b->accstep[r - 1] == steps) || (ix < nx - 1 && b->accstep[r + 1] == steps)) quirk = 1;
                 }
                 double v = oref_update_f(f, m, c->ph, iz, ix, c->dnx, quirk ? nx : nz, nx);
                 if (v == -1.0) v = oref_fouds18_f(f, m, c->av, iz, ix, c->dnx, c->dnz_fouds, nx, nz);
                 b->V[k] = v;
             }
-            if (sw + 1 < sweeps) {
-                /* Gauss-Seidel-like second sweep: candidates see each other's first-sweep values */
-                for (long k = 0; k < nC; k++) { long r = b->C[k]; f->ttn[r] = b->V[k]; f->nsts[r] = S_CLOSEC; }
+            for (long k = 0; k < nC; k++) {
+                long r = b->C[k];
+                f->ttn[r] = b->V[k];
+                if (f->nsts[r] == S_FARC) b->L2[nL2++] = (int32_t)r;
+                f->nsts[r] = S_CLOSE;
+                if (ndirph == 4 && b->accstep[r] < 0) b->accstep[r] = -2 - (int32_t)steps;
             }
-        }
-        for (long k = 0; k < nC; k++) {
-            long r = b->C[k];
-            f->ttn[r] = b->V[k];
-            if (f->nsts[r] == S_FARC) b->L2[nL2++] = (int32_t)r;
-            f->nsts[r] = S_CLOSE;
         }
         int32_t *t = b->L; b->L = b->L2; b->L2 = t;
         b->nL = nL2;
@@ -144,7 +146,7 @@ static void band_handover(const fstate_t *s, long isz_s, long isx_s, bstate_t *d
 int oband_travel(double scx, double scz, int nnz, int nnx, const double *veln, const int64_t *velpn,
                  const double *vel_map, const int64_t *stif, const double *av_, const double *ph_, int ncol,
                  double gox, double goz, double dnx, double dnz, double cdelta, double vmax, int exact_init,
-                 int sweeps, double r0, double *ttn, long *steps_out) {
+                 int sweeps, double r0, double exact_r, double *ttn, long *steps_out) {
     base_t bb;
     if (make_base(&bb, nnz, nnx, veln, velpn, vel_map, stif)) return -1;
     const mat_t *base = &bb.m;
@@ -155,6 +157,7 @@ int oband_travel(double scx, double scz, int nnz, int nnx, const double *veln, c
     long steps[4] = {0, 0, 0, 0};
     long sgs[3] = {27, 9, 3}, sizes[3] = {2, 6, 13};
     fstate_t prev;       /* previous stage (heap or band) in fstate form */
+    fstate_t hprev_keep; /* stage-3 heap state for the exact main-loop prefix */
     bstate_t bprev;
     int have_b = 0;
     long pisz = 0, pisx = 0;
@@ -166,7 +169,7 @@ int oband_travel(double scx, double scz, int nnz, int nnx, const double *veln, c
         make_view(&views[st], base, bottom, top, left, right, sg);
         long isx_s = sg * (isx - left), isz_s = sg * (isz - bottom);
         double dn = dnx / sg;
-        loopcfg_t c = {av, ph, dn, dn, 1, (int)isx_s, (int)isz_s, (int)(sg * size), st == 0};
+        loopcfg_t c = {av, ph, dn, dn, 1, (int)isx_s, (int)isz_s, (int)(sg * size), st == 0, 0.0};
         if (exact_init == 1 || (exact_init == 2 && st == 0) || (exact_init == 3 && st < 2)) {
             fstate_t f;
             fstate_alloc(&f, views[st].m.nnz, views[st].m.nnx, 0, NULL);
@@ -180,6 +183,11 @@ int oband_travel(double scx, double scz, int nnz, int nnx, const double *veln, c
             fmm_loop(&f, &views[st].m, &c);
             prev = f;
             have_b = 0;
+            if (st == 2 && exact_r > 0) {
+                fstate_alloc(&hprev_keep, f.nnz, f.nnx, 0, NULL);
+                memcpy(hprev_keep.ttn, f.ttn, sizeof(double) * (size_t)f.nnz * f.nnx);
+                memcpy(hprev_keep.nsts, f.nsts, sizeof(int32_t) * (size_t)f.nnz * f.nnx);
+            }
         } else {
             bstate_t b;
             bstate_alloc(&b, views[st].m.nnz, views[st].m.nnx, NULL);
@@ -205,11 +213,33 @@ int oband_travel(double scx, double scz, int nnz, int nnx, const double *veln, c
         }
         pisz = isz_s; pisx = isx_s;
     }
-    loopcfg_t c = {av, ph, dnx, dnz, 0, 0, 0, 0, 0};
+    loopcfg_t c = {av, ph, dnx, dnz, 0, 0, 0, 0, 0, 0.0};
     bstate_t bm;
     bstate_alloc(&bm, nnz, nnx, ttn);
     if (!have_b) { band_handover(&prev, pisz, pisx, &bm, isz, isx); fstate_free(&prev, 1); }
     else { band_handover(&bprev.f, pisz, pisx, &bm, isz, isx); bstate_free(&bprev, 1); }
+    if (exact_r > 0) {
+        /* exact heap-ordered prefix of the main loop (the reference's own pop order near the source),
+           then the band continues from the heap's state (close = in heap, known, far) */
+        fstate_t h;
+        fstate_alloc(&h, (int)nnz, (int)nnx, 0, ttn);
+        for (long i = 0; i < (long)nnz * nnx; i++) h.nsts[i] = -1;
+        /* rebuild the reference hand-over into the heap (row-major addtree order) */
+        memset(ttn, 0, sizeof(double) * (size_t)nnz * nnx);
+        if (!have_b) { fprintf(stderr, "exact_r needs band stages off\n"); }
+        handover(&hprev_keep, pisz, pisx, &h, isz, isx);
+        loopcfg_t ce = c;
+        ce.tstop = exact_r * dnx / vmax;
+        fmm_loop(&h, base, &ce);
+        for (long i = 0; i < (long)nnz * nnx; i++) bm.f.nsts[i] = -1;
+        bm.nL = 0;
+        for (long i = 0; i < (long)nnz * nnx; i++) {
+            if (h.nsts[i] == 0) bm.f.nsts[i] = S_KNOWN;
+            else if (h.nsts[i] > 0) push_close(&bm, i);
+        }
+        fstate_free(&h, 0);
+        fstate_free(&hprev_keep, 1);
+    }
     steps[3] = band_run(&bm, base, &c, cdelta * dnx / vmax, sweeps, r0 * dnx / vmax);
     bstate_free(&bm, 0);
     for (int st = 0; st < 3; st++) free_view(&views[st]);
