@@ -1,0 +1,154 @@
+"""Benchmark: grid-cell updates/s + sources/s on the 4096^2 anisotropic weld-like grid (BASELINE.json).
+
+One process per GPU (python -m torch.distributed.run ... bench.py --gpus N).  A "step" is one
+pass of the hot path over one batch: first-arrival travel-time fields for the rank's sources
+(BASELINE C4: 128 sources on the top surface per GPU, subgrid 1), inputs resident in HBM, fields
+left resident in HBM (the ray tracer reads them there).  Sources are independent: each rank
+computes its own shard (weak scaling), no data-path collective; torch.distributed (gloo) only
+provides the barrier and the max-over-ranks of the step time.
+
+Reported: value = all ranks' (cells x sources) / max-over-ranks wall time of the timed steps;
+roofline of the dominant kernel (fmm_band_kernel) from in-library HIP events; cpu_baseline = the
+CPU restatement of the reference (oracle/, one source per thread) on a bounded sample, rank 0, N=1.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "ali-fmm-and-ray-tracing_amd"))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+# algorithmic bytes per cell-sweep (one local-operator evaluation on the band front), DESIGN.md §5:
+# T f64 read+write 16, status int32 read+write 8, material (veln f64, vel_map f64, velpn i32, stiffness idx i32) 24
+BYTES_PER_SWEEP = 48
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--n", type=int, default=4096, help="grid side (4096 = BASELINE C4)")
+    ap.add_argument("--sources", type=int, default=128, help="sources per GPU (BASELINE C4: 128)")
+    ap.add_argument("--cpu-sample", type=int, default=16, help="sources in the CPU-baseline sample (0: skip)")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cdelta", type=float, default=None)
+    ap.add_argument("--exact-r", type=float, default=None)
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    import _alifmm
+    import workloads as W
+
+    n = args.n
+    veln, velpn, vel_map, stif = W.weldlike_model(n)
+    dnx = W.weldlike_dnx()
+    vt = W.default_table()
+    ctx = _alifmm.Context(local)
+    if args.cdelta is not None:
+        ctx.set_option("cdelta", args.cdelta)
+    if args.exact_r is not None:
+        ctx.set_option("exact_r", args.exact_r)
+    ctx.set_model(veln, velpn, vel_map, stif, vt, vt, dnx)
+    # rank r: x = 16 + 32k + 4 (r mod 8), z = 0  (rank 0 = exactly BASELINE C4's sources)
+    k = np.arange(args.sources) % (n // 32)
+    scx = dnx * (16 + 32 * k + 4 * (rank % 8)).astype(np.float64)
+    scz = np.zeros(args.sources)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        ctx.travel(scx, scz, subgrid=1, first_slot=0, copy_out=False)
+    barrier()
+    t0 = time.perf_counter()
+    band_ms = init_ms = 0.0
+    for _ in range(args.steps):
+        ctx.travel(scx, scz, subgrid=1, first_slot=0, copy_out=False)
+        ti, tb, _ = ctx.last_timing()
+        init_ms += ti
+        band_ms += tb
+    barrier()
+    dt = time.perf_counter() - t0
+    sweeps = sum(ctx.source_stats(i)[1] for i in range(args.sources))
+    steps_main = [int(ctx.source_stats(i)[0][3]) for i in range(args.sources)]
+    if dist is not None:
+        import torch
+
+        tt = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    cells = float(n) * n
+    total_src = args.sources * world
+    value = cells * total_src * args.steps / dt
+    band_avg_s = band_ms / args.steps / 1e3
+    achieved = BYTES_PER_SWEEP * sweeps / band_avg_s / 1e9 if band_avg_s > 0 else None
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu and args.cpu_sample > 0:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle as O
+
+        ns = args.cpu_sample
+        th = min(args.cpu_threads, ns)
+        t1 = time.perf_counter()
+        O.travel_batch(scx[:ns], scz[:ns], veln, velpn, vel_map, stif, vt, vt, dnx=dnx, n_threads=th)
+        tc = time.perf_counter() - t1
+        cpu = {"value": cells * ns / tc, "unit": "grid-cell updates/s", "cores": th, "kind": "port",
+               "sample": "%d C4 sources (4096^2, z=0) on %d threads, one source per thread, oracle/alifmm_oracle.c "
+                         "(bit-exact restatement of the reference's heap FMM); %.1f s wall" % (ns, th, tc)}
+    if rank == 0:
+        out = {
+            "metric": "grid-cell updates/sec + sources/sec on 4096^2 anisotropic grid",
+            "value": value,
+            "unit": "grid-cell updates/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: weld-like model built from the reference's weld_*.npy (edge-padded, 8x nearest), "
+                    "stiffness row of the notebook",
+            "config": {"workload": "C4: %dx%d weld-like, %d top-surface Tx sources per GPU, subgrid 1" % (n, n, args.sources),
+                       "sources_per_gpu": args.sources, "total_sources": total_src, "grid": [n, n], "subgrid": 1},
+            "sources_per_s": total_src * args.steps / dt,
+            "kernel_ms_per_step": {"fmm_init_kernel": init_ms / args.steps, "fmm_band_kernel": band_ms / args.steps},
+            "band_steps_main_mean": float(np.mean(steps_main)),
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
+                         "kernel": "fmm_band_kernel", "bytes_per_cell_sweep": BYTES_PER_SWEEP,
+                         "cell_sweeps_per_launch": int(sweeps)},
+            "cpu_baseline": cpu,
+        }
+        if cpu:
+            out["speedup_vs_cpu_baseline"] = value / cpu["value"]
+        print(json.dumps(out))
+    if dist is not None:
+        dist.destroy_process_group()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
