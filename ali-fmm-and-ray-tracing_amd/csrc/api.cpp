@@ -438,6 +438,14 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
     P.mode = 1;
     P.scx = a.dscx;
     P.scz = a.dscz;
+    // exact heap walk: both stage grids plus the fine-grid main loop out to exact_r fine nodes
+    // beyond the stage-2 window (field units before the final / subgrid: coarse dnx per fine node)
+    const long size2 = 2L * sg + (sg - 1) / 2 + 3L * sg;
+    P.tstop = (double)(size2 + ctx->exact_r) * ctx->dnx / ctx->vmax;
+    P.capL = (int)capL;
+    P.capS = (int)capS;
+    P.src = a.srcs;
+    HIPCHK(af_launch_exact(&P, ctx->stream));
   }
   HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
   HIPCHK(af_launch_band(&P, ctx->stream));
@@ -482,7 +490,7 @@ int alifmm_travel(alifmm_ctx* ctx, int subgrid, int nsrc, const double* scx, con
   for (int s0 = 0; s0 < nsrc; s0 += ctx->batch) {
     int n = std::min(ctx->batch, nsrc - s0);
     int rc;
-    for (int attempt = 0;; attempt++) {
+    for (;;) {
       rc = travel_chunk(ctx, subgrid, n, scx + s0, scz + s0, first_slot + s0, fz, fx, &ms_init, &ms_band);
       if (rc != ALIFMM_E_CAPACITY || ctx->cap_scale * 4 > 64) break;
       ctx->cap_scale *= 4;  // retry the chunk with larger work lists

@@ -1,0 +1,67 @@
+// fields.h — global-memory field accessors for the local operators (update() / fouds18_A()).
+#pragma once
+#include "device_common.h"
+
+namespace af {
+
+struct GField {
+  const double* T;
+  const int* S;
+  int nz, nx;
+  AF_DEV int st(long z, long x) const { return z >= nz ? -1 : S[z * nx + x]; }
+  AF_DEV double tt(long z, long x) const { return z >= nz ? 0.0 : T[z * nx + x]; }
+};
+
+// Register copy of the 12 cells update() reads around (iz, ix): (0,+-1) (+-1,0) (+-1,+-1) (0,+-2)
+// (+-2,0).  All 24 loads are issued together (one memory round trip instead of a chain of
+// branch-dependent gathers).  Same values as GField: rows >= nz read status -1 / time 0 (the
+// reference's padded stage-1 reads); other out-of-grid positions are never read by update().
+struct NbField {
+  long iz, ix;
+  unsigned vm;  // bit k: status >= 0
+  double t0, t1, t2, t3, t4, t5, t6, t7, t8, t9, t10, t11;
+  AF_DEV static int slot(long dz, long dx) {
+    return dz == 0 ? (dx == -2 ? 0 : dx == -1 ? 1 : dx == 1 ? 2 : 3)
+         : dx == 0 ? (dz == -2 ? 4 : dz == -1 ? 5 : dz == 1 ? 6 : 7)
+         : dz < 0 ? (dx < 0 ? 8 : 9) : (dx < 0 ? 10 : 11);
+  }
+  AF_DEV int st(long z, long x) const { return (vm >> slot(z - iz, x - ix)) & 1u ? 0 : -1; }
+  AF_DEV double tt(long z, long x) const {
+    const int k = slot(z - iz, x - ix);
+    return k == 0 ? t0 : k == 1 ? t1 : k == 2 ? t2 : k == 3 ? t3 : k == 4 ? t4 : k == 5 ? t5 : k == 6 ? t6
+         : k == 7 ? t7 : k == 8 ? t8 : k == 9 ? t9 : k == 10 ? t10 : t11;
+  }
+  AF_DEV void load(const double* T, const int* S, int nz, int nx, int z, int x) {
+    iz = z;
+    ix = x;
+    const long n = (long)nz * nx;
+    long f[12];
+    bool in[12];
+    const int dz[12] = {0, 0, 0, 0, -2, -1, 1, 2, -1, -1, 1, 1};
+    const int dx[12] = {-2, -1, 1, 2, 0, 0, 0, 0, -1, 1, -1, 1};
+    int s[12];
+    double t[12];
+#pragma unroll
+    for (int k = 0; k < 12; k++) {
+      long c = (long)(z + dz[k]) * nx + (x + dx[k]);
+      in[k] = z + dz[k] < nz;
+      f[k] = c < 0 ? 0 : c >= n ? n - 1 : c;
+    }
+#pragma unroll
+    for (int k = 0; k < 12; k++) {
+      s[k] = S[f[k]];
+      t[k] = T[f[k]];
+    }
+    unsigned m = 0;
+#pragma unroll
+    for (int k = 0; k < 12; k++) {
+      if (in[k] && s[k] >= 0) m |= 1u << k;
+      if (!in[k]) t[k] = 0.0;
+    }
+    vm = m;
+    t0 = t[0]; t1 = t[1]; t2 = t[2]; t3 = t[3]; t4 = t[4]; t5 = t[5];
+    t6 = t[6]; t7 = t[7]; t8 = t[8]; t9 = t[9]; t10 = t[10]; t11 = t[11];
+  }
+};
+
+}  // namespace af

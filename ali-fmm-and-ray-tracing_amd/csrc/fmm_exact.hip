@@ -1,0 +1,324 @@
+// fmm_exact.hip — the source stages of travel_finer_grid() (Anis_TTF_rays.py:2187-2504) and the
+// first part of its fine-grid main loop (:2775-2817), solved exactly as the reference does, on gfx950.
+//
+// Near the source the reference's heap (round-half-even parent, SURVEY B-D3) pops nodes out of
+// time order, and the hand-over nodes and grid edges make the field depend on that order; a
+// time-ordered (band) solver differs there by up to a few per cent.  This kernel replays the
+// reference's heap walk: x9 stage grid, x3 stage grid, then the fine main grid until the heap
+// root reaches P.tstop.  The stage grids (up to 397 x 397 for subgrid 9) and the main grid live
+// in HBM; the heap itself (cells + keys, i.e. copies of ttn at insertion/update) lives in LDS, so
+// every sift is LDS-only and each pop costs the <= 4 neighbour evaluations (one round trip of
+// 24 prefetched loads each, NbField).  One workgroup (one wave) per source; the walk is serial
+// (lane 0), the other lanes clear grids and fill the straight-ray footprint.
+//
+// Output for the band kernel: main-grid statuses known 0 / close 1 / far -1 and the close cells
+// in L0 (count in BandSrc::nl0).
+#include "kernels.h"
+#include "local_ops.h"
+#include "fields.h"
+
+namespace af {
+
+constexpr int kXHeap = 8192;
+
+struct XLds {
+  double key[kXHeap];
+  int cell[kXHeap];
+};
+
+// addtree / updtree / downtree (:94-237) over a global nsts array, heap slots in LDS
+struct XHeap {
+  XLds* H;
+  int* S;
+  const double* T;
+  int ntr;
+  int err;
+  AF_DEV static int parent(int t) { return (int)rint((double)t / 2.0); }  // half-even (:123)
+  AF_DEV void swap(int a, int b) {
+    int c = H->cell[a];
+    H->cell[a] = H->cell[b];
+    H->cell[b] = c;
+    double k = H->key[a];
+    H->key[a] = H->key[b];
+    H->key[b] = k;
+  }
+  AF_DEV void sift_up(int c, int tpc) {
+    int tpp = parent(tpc);
+    const double tv = H->key[tpc];
+    while (tpp > 0) {
+      if (tv < H->key[tpp]) {
+        S[c] = tpp;
+        S[H->cell[tpp]] = tpc;
+        swap(tpc, tpp);
+        tpc = tpp;
+        tpp = parent(tpc);
+      } else {
+        tpp = 0;
+      }
+    }
+  }
+  AF_DEV void add(int c) {
+    ntr += 1;
+    if (ntr >= kXHeap) {
+      err = 3;
+      ntr = kXHeap - 1;
+      return;
+    }
+    S[c] = ntr;
+    H->cell[ntr] = c;
+    H->key[ntr] = T[c];
+    sift_up(c, ntr);
+  }
+  AF_DEV void upd(int c) {
+    const int tpc = S[c];
+    H->key[tpc] = T[c];
+    sift_up(c, tpc);
+  }
+  AF_DEV void down() {
+    if (ntr == 1) {
+      ntr -= 1;
+      return;
+    }
+    S[H->cell[ntr]] = 1;
+    H->cell[1] = H->cell[ntr];
+    H->key[1] = H->key[ntr];
+    ntr -= 1;
+    int tpp = 1, tpc = 2;
+    while (tpc < ntr) {
+      if (H->key[tpc] > H->key[tpc + 1]) tpc = tpc + 1;
+      if (H->key[tpc] < H->key[tpp]) {
+        S[H->cell[tpp]] = tpc;
+        S[H->cell[tpc]] = tpp;
+        swap(tpc, tpp);
+        tpp = tpc;
+        tpc = 2 * tpp;
+      } else {
+        tpc = ntr + 1;
+      }
+    }
+    if (tpc == ntr) {
+      if (H->key[tpc] < H->key[tpp]) {
+        S[H->cell[tpp]] = tpc;
+        S[H->cell[tpc]] = tpp;
+        swap(tpc, tpp);
+      }
+    }
+  }
+};
+
+struct XGrid {
+  double* T;
+  int* S;
+  int nz, nx;
+  MatView mv;
+  double dnx, dnz;  // update() spacing, fouds18 dnz
+};
+
+// update() then fouds18_A() (:2326-2329 / :2790-2793)
+AF_DEV double xrelax(const DevModel& M, const XGrid& g, int iz, int ix) {
+  CellMat cm = cell_mat(M, g.mv, iz, ix);
+  NbField nb;
+  nb.load(g.T, g.S, g.nz, g.nx, iz, ix);
+  double v = update(nb, M, cm, iz, ix, g.dnx, g.nz, g.nx);
+  if (v == -1.0) {
+    GField F{g.T, g.S, g.nz, g.nx};
+    v = fouds18(F, M, cm, iz, ix, g.dnx, g.dnz, g.nx, g.nz);
+  }
+  return v;
+}
+
+// the reference's FMM loop (oracle fmm_loop): stage grids stop when a neighbour step leaves the
+// window at max_dist + 1 from the source; the main grid stops when the root reaches tstop
+AF_DEV long long xloop(XHeap& h, const DevModel& M, const XGrid& g, bool stage, int isx_s, int isz_s, int max_dist,
+                       double tstop) {
+  long long pops = 0;
+  bool finished = false;
+  const int nz = g.nz, nx = g.nx;
+  while (h.ntr > 0 && !finished && !h.err) {
+    const int c = h.H->cell[1];
+    if (tstop > 0 && h.H->key[1] >= tstop) break;
+    const int iz = c / nx, ix = c - iz * nx;
+    g.S[c] = 0;
+    h.down();
+    pops++;
+    for (int s = 0; s < 2; s++) {
+      const int i = s == 0 ? ix - 1 : ix + 1;
+      if (0 <= i && i <= nx - 1) {
+        const int r = iz * nx + i;
+        const int st = g.S[r];
+        if (st == -1) {
+          g.T[r] = xrelax(M, g, iz, i);
+          h.add(r);
+        } else if (st > 0) {
+          g.T[r] = xrelax(M, g, iz, i);
+          h.upd(r);
+        }
+      } else if (stage && abs(isx_s - i) == max_dist + 1) {
+        finished = true;
+      }
+    }
+    for (int s = 0; s < 2; s++) {
+      const int i = s == 0 ? iz - 1 : iz + 1;
+      if (0 <= i && i <= nz - 1) {
+        const int r = i * nx + ix;
+        const int st = g.S[r];
+        if (st == -1) {
+          g.T[r] = xrelax(M, g, i, ix);
+          h.add(r);
+        } else if (st > 0) {
+          g.T[r] = xrelax(M, g, i, ix);
+          h.upd(r);
+        }
+      } else if (stage && abs(isz_s - i) == max_dist + 1) {
+        finished = true;
+      }
+    }
+  }
+  return pops;
+}
+
+// hand-over of every 3rd node of a stage grid into the next grid, in row-major order (:2391-2425,
+// :2725-2759): ttn copied, known nodes stay known, "outer" known nodes and close nodes -> heap
+AF_DEV void xhandover(XHeap& h, const XGrid& s, int isz_s, int isx_s, const XGrid& d, int isz_d, int isx_d) {
+  for (int i = 0; i < s.nz + 1; i += 3) {
+    for (int j = 0; j < s.nx + 1; j += 3) {
+      const int pz = isz_d + (i - isz_s) / 3, px = isx_d + (j - isx_s) / 3;
+      const int dc = pz * d.nx + px;
+      d.T[dc] = s.T[i * s.nx + j];
+      const int st = s.S[i * s.nx + j];
+      if (st == 0) {
+        d.S[dc] = 0;
+        bool outer = false;
+        if (i - 3 >= 0) { if (s.S[(i - 3) * s.nx + j] == -1) outer = true; } else outer = true;
+        if (i + 3 <= s.nz - 1) { if (s.S[(i + 3) * s.nx + j] == -1) outer = true; } else outer = true;
+        if (j - 3 >= 0) { if (s.S[i * s.nx + j - 3] == -1) outer = true; } else outer = true;
+        if (j + 3 <= s.nx - 1) { if (s.S[i * s.nx + j + 3] == -1) outer = true; } else outer = true;
+        if (outer) h.add(dc);
+      }
+      if (st > 0) h.add(dc);
+    }
+  }
+}
+
+AF_DEV void xclear(double* T, int* S, int n) {
+  for (int k = threadIdx.x; k < n; k += blockDim.x) {
+    T[k] = 0.0;
+    S[k] = -1;
+  }
+}
+
+__global__ __launch_bounds__(64) void fmm_exact_kernel(BandParams P) {
+  __shared__ XLds lds;
+  const int src = blockIdx.x;
+  if (src >= P.nsrc) return;
+  BandSrc* B = P.src + src;
+  const int lane = threadIdx.x;
+  const DevModel& M = P.M;
+  const int sg = P.sg, sgside = (sg - 1) / 2;
+  const long isx = (long)sg * (long)rint((P.scx[src] - P.gox) / P.dnx);
+  const long isz = (long)sg * (long)rint((P.scz[src] - P.goz) / P.dnz);
+  const int nnz = P.nz, nnx = P.nx;
+  int err = 0;
+  XGrid prev{nullptr, nullptr, 0, 0, MatView{}, 0, 0};
+  int pisz = 0, pisx = 0;
+  const int scales[2] = {9, 3};
+  const int size1 = 2 * sg + (sg - 1) / 2, size2 = size1 + 3 * sg;
+  for (int stg = 0; stg < 2 && !err; stg++) {
+    const int scale = scales[stg], size = stg == 0 ? size1 : size2;
+    const int left = (int)max(0L, isx - size), right = (int)min((long)nnx - 1, isx + size);
+    const int bottom = (int)max(0L, isz - size), top = (int)min((long)nnz - 1, isz + size);
+    XGrid g;
+    g.nz = scale * (top - bottom) + 1;
+    g.nx = scale * (right - left) + 1;
+    if ((long)g.nz * g.nx > P.capS) {
+      err = 4;
+      break;
+    }
+    g.T = B->Ts[stg];
+    g.S = B->Ss[stg];
+    g.mv = MatView{scale, (scale - 1) / 2, bottom, scale, (scale - 1) / 2, left, sg, sgside, 0, 0, 1};
+    g.dnx = g.dnz = P.dnx / scale;
+    const int isx_s = scale * (int)(isx - left), isz_s = scale * (int)(isz - bottom);
+    xclear(g.T, g.S, g.nz * g.nx);
+    __syncthreads();
+    XHeap h{&lds, g.S, g.T, 0, 0};
+    if (stg == 0) {
+      // straight rays (:2223-2267; veln + angle, SURVEY B-D5), material of the source's fine cell
+      const int side1 = (9 - 1) / 2 + 9 * ((sg - 1) / 2);
+      const MatView fine{sg, sgside, 0, sg, sgside, 0, 1, 0, 0, 0, 1};
+      const CellMat cs = cell_mat(M, fine, (int)isz, (int)isx);
+      const int w = 2 * side1 + 1;
+      for (int k = lane; k < w * w; k += blockDim.x) {
+        const int i = k / w - side1, j = k % w - side1;
+        if (0 <= isz_s + i && isz_s + i <= g.nz - 1 && 0 <= isx_s + j && isx_s + j <= g.nx - 1) {
+          double angle = (j == 0) ? 90.0 : atan((double)i / (double)j) * kRad2Deg;
+          double eff = pymod(cs.veln + angle, 180);
+          double velocity = (cs.velpn != 0 || cs.stif == nullptr) ? table_vel(M.gtab, M.ncol, eff, cs.velpn, cs.vm)
+                                                                  : christoffel_group(cs.stif, eff, cs.vm);
+          double length = g.dnx * sqrt((double)(i * i + j * j));
+          g.T[(isz_s + i) * g.nx + isx_s + j] = length / velocity;
+          g.S[(isz_s + i) * g.nx + isx_s + j] = 0;
+        }
+      }
+      __syncthreads();
+      if (lane == 0) {
+        // window edges -> heap in the reference's order (:2277-2288)
+        const int s1 = side1;
+        if (isz_s - s1 >= 0)
+          for (int i = max(0, isx_s - s1); i <= min(g.nx - 1, isx_s + s1); i++) h.add((isz_s - s1) * g.nx + i);
+        if (isz_s + s1 <= g.nz - 1)
+          for (int i = max(0, isx_s - s1); i <= min(g.nx - 1, isx_s + s1); i++) h.add((isz_s + s1) * g.nx + i);
+        if (isx_s - s1 >= 0)
+          for (int i = max(0, isz_s - s1); i <= min(g.nz - 1, isz_s + s1); i++) h.add(i * g.nx + isx_s - s1);
+        if (isx_s + s1 <= g.nx - 1)
+          for (int i = max(0, isz_s - s1); i <= min(g.nz - 1, isz_s + s1); i++) h.add(i * g.nx + isx_s + s1);
+      }
+    } else if (lane == 0) {
+      xhandover(h, prev, pisz, pisx, g, isz_s, isx_s);
+    }
+    if (lane == 0) {
+      B->steps[stg] = xloop(h, M, g, true, isx_s, isz_s, scale * size, 0.0);
+      err = h.err;
+    }
+    err = __shfl(err, 0);
+    __syncthreads();
+    prev = g;
+    pisz = isz_s;
+    pisx = isx_s;
+  }
+  // fine main grid (memset by the host: T 0, S -1): hand-over, then the exact prefix
+  if (lane == 0) {
+    int nl = 0;
+    if (!err) {
+      XGrid g;
+      g.T = B->T;
+      g.S = B->S;
+      g.nz = nnz;
+      g.nx = nnx;
+      g.mv = MatView{sg, sgside, 0, sg, sgside, 0, 1, 0, 0, 0, 1};
+      g.dnx = P.dnx;  // the coarse spacing on the fine grid (:2790; field divided by sg at the end)
+      g.dnz = P.dnz;
+      XHeap h{&lds, g.S, g.T, 0, 0};
+      xhandover(h, prev, pisz, pisx, g, (int)isz, (int)isx);
+      B->steps[2] = xloop(h, M, g, false, 0, 0, 0, P.tstop);
+      err = h.err;
+      // heap -> band close list (statuses: heap index > 0 -> close 1)
+      for (int k = 1; k <= h.ntr && k <= P.capL; k++) {
+        const int c = lds.cell[k];
+        B->S[c] = kClose;
+        B->L0[k - 1] = c;
+      }
+      nl = h.ntr;
+      if (nl > P.capL) err = 2;
+    }
+    B->nl0 = nl;
+    B->err = err;
+  }
+}
+
+}  // namespace af
+
+extern "C" hipError_t af_launch_exact(const af::BandParams* P, hipStream_t stream) {
+  hipLaunchKernelGGL(af::fmm_exact_kernel, dim3(P->nsrc), dim3(64), 0, stream, *P);
+  return hipGetLastError();
+}

@@ -18,7 +18,7 @@ struct BandSrc {
   long long steps[4];
   long long nupd;  // relax evaluations (cell-sweeps) in the main run
   int err;
-  int pad;
+  int nl0;  // close cells handed to the band kernel in L0 (mode 1: fmm_exact_kernel)
 };
 
 struct BandParams {
@@ -29,6 +29,7 @@ struct BandParams {
   int nz, nx;    // main grid (fine grid in mode 1)
   double dnx, dnz;
   double cdelta, vmax, r0;
+  double tstop;  // mode 1: the exact main-loop prefix stops when the heap root reaches it (fmm_exact_kernel)
   int capL, capC, capS;  // list capacities, stage-grid capacity (cells)
   BandSrc* src;
   const HandoverOut* ho;  // mode 0
@@ -83,6 +84,7 @@ struct LocalOpsParams {
 
 extern "C" {
 hipError_t af_launch_init(const af::DevModel* M, af::InitJob* jobs, int njobs, af::HandoverOut* out, hipStream_t stream);
+hipError_t af_launch_exact(const af::BandParams* P, hipStream_t stream);
 hipError_t af_launch_band(const af::BandParams* P, hipStream_t stream);
 hipError_t af_launch_scale(double* T, long n, double sg, hipStream_t stream);
 hipError_t af_launch_rays(const af::RayParams* P, hipStream_t stream);
