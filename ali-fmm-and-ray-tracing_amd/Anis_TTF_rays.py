@@ -27,6 +27,7 @@ import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import _alifmm  # noqa: E402
+import sharding  # noqa: E402
 
 # Parameter used to enable/disable progress bars (reference :22-24; kept for API compatibility)
 tqdm_disable = False
@@ -103,8 +104,28 @@ def finer_grid_n_2(data, scale):
     return data[iz][:, ix].astype(np.int64)
 
 
+def _sincos(x):
+    """sin(x), cos(x) from libm's sincos(): numba (LLVM) fuses the reference's sin(2 pa) / cos(2 pa)
+    pair into one sincos() call, which can differ from separate sin() by an ulp."""
+    import ctypes
+    import ctypes.util
+
+    global _libm
+    if _libm is None:
+        _libm = ctypes.CDLL(ctypes.util.find_library("m"))
+        _libm.sincos.argtypes = [ctypes.c_double, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
+        _libm.sincos.restype = None
+    s, c = ctypes.c_double(), ctypes.c_double()
+    _libm.sincos(x, ctypes.byref(s), ctypes.byref(c))
+    return s.value, c.value
+
+
+_libm = None
+
+
 def group_vel(angle, c_22, c_23, c_33, c_44, sigma, vel_scale=1):
-    """Closed-form 2D orthotropic Christoffel group velocity (reference :3521-3558)."""
+    """Closed-form 2D orthotropic Christoffel group velocity (reference :3521-3558, a numba
+    function: sin/cos of the same argument go through sincos(), as numba compiles them)."""
     if angle % 90 < 0.01 or angle % 90 > 90 - 0.01:
         if abs((angle % 180) - 90) < 1:
             lambda_val = c_33
@@ -119,8 +140,8 @@ def group_vel(angle, c_22, c_23, c_33, c_44, sigma, vel_scale=1):
         phase_angle_rad = math.atan((-B - math.sqrt(B ** 2 + A ** 2 - C ** 2)) / (C - A)) % math.pi
     else:
         phase_angle_rad = math.atan((-B + math.sqrt(B ** 2 + A ** 2 - C ** 2)) / (C - A)) % math.pi
-    lambda_val = 0.5 * (math.cos(2 * phase_angle_rad) * (c_22 - c_44) + math.sin(2 * phase_angle_rad) * (c_23 + c_44) *
-                        tan_ang + c_22 + c_44)
+    s2, c2 = _sincos(2 * phase_angle_rad)
+    lambda_val = 0.5 * (c2 * (c_22 - c_44) + s2 * (c_23 + c_44) * tan_ang + c_22 + c_44)
     return 1000 * vel_scale * math.sqrt(lambda_val / sigma) / math.cos(math.radians(angle) - phase_angle_rad)
 
 
@@ -300,7 +321,7 @@ class ALI_FMM:
     def _fields(self, veln, velpn, vel_map, stif_den, subgrid_size, idx, devices, copy_out=True, slot_of=None):
         """Fields of the sources `idx`, block-distributed over `devices` (one host thread per GPU)."""
         idx = list(idx)
-        parts = [idx[k::len(devices)] for k in range(len(devices))]
+        parts = sharding.deal(idx, len(devices))
         results = {}
         errors = []
 

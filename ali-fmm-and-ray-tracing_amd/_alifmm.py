@@ -10,7 +10,7 @@ import threading
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libalifmm.so")
+LIB_PATH = os.environ.get("ALIFMM_LIB") or os.path.join(HERE, "lib", "libalifmm.so")  # override: experiments
 
 _d, _i, _l, _p = ctypes.c_double, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p
 _lib = None
@@ -45,6 +45,7 @@ def _load():
             "alifmm_find_rays": (_i, [_p, _i, _p, _p, _p, _p, _p, _p, _p, _l]),
             "alifmm_source_stats": (_i, [_p, _i, _p, _p]),
             "alifmm_last_timing": (_i, [_p, _p, _p, _p]),
+            "alifmm_band_profile": (_i, [_p, _i, _p]),
             "alifmm_put_field": (_i, [_p, _i, _i, _p]),
             "alifmm_time_between_points": (_i, [_p, _i, _p, _p, _p, _p, _i, _p]),
             "alifmm_local_ops": (_i, [_p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i,
@@ -208,6 +209,11 @@ class Context:
         sw = ctypes.c_int64(0)
         self._chk(lib().alifmm_source_stats(self._h, int(slot), _ptr(steps), ctypes.byref(sw)), "source_stats")
         return steps, sw.value
+
+    def band_profile(self, slot):
+        out = np.zeros(14, dtype=np.int64)
+        self._chk(lib().alifmm_band_profile(self._h, int(slot), _ptr(out)), "band_profile")
+        return out
 
     def last_timing(self):
         a, b, c = ctypes.c_double(0), ctypes.c_double(0), ctypes.c_double(0)

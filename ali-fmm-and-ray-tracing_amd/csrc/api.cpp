@@ -26,14 +26,16 @@ struct Field {
   int sg = 0, nz = 0, nx = 0;
   int64_t steps[4] = {0, 0, 0, 0};
   int64_t sweeps = 0;
+  int64_t prof[14] = {};  // band profile: 6 phase ticks, 3 list sums, max close, 4 sub-phase ticks
 };
 
 struct Arena {  // per-chunk scratch, reused across calls
   int nsrc = 0;
   long cells = 0, capL = 0, capC = 0, capS = 0;
   int* S = nullptr;
-  int* lists = nullptr;  // L0 | L1 | A | C per source
-  double* V = nullptr;
+  int* own = nullptr;
+  int* lists = nullptr;    // L0 | L1 | A | C | Cp per source
+  double* dlists = nullptr;  // Lt0 | Lt1 | V per source
   double* Ts = nullptr;  // stage grids (travel_finer_grid), 2 per source
   int* Ss = nullptr;
   af::BandSrc* srcs = nullptr;
@@ -59,12 +61,17 @@ struct alifmm_ctx {
   int* d_velpn = nullptr;
   int* d_sidx = nullptr;
   double* d_stab = nullptr;
+  int nstab = 0;
+  int* d_mid = nullptr;
+  af::MatRec* d_mtab = nullptr;
+  int nmat = 0;
   double* d_gtab = nullptr;
   double* d_ptab = nullptr;
   // options
   double cdelta = 0.5, r0 = 40.0;
   int exact_r = 40;
   int batch = 256;
+  int prof = 0;
   long cap_scale = 1;
   // state
   std::vector<Field> fields;
@@ -97,7 +104,7 @@ static void dfree(void* p) {
 }
 
 static void free_arena(Arena& a) {
-  dfree(a.S); dfree(a.lists); dfree(a.V); dfree(a.Ts); dfree(a.Ss); dfree(a.srcs); dfree(a.ho); dfree(a.jobs);
+  dfree(a.S); dfree(a.own); dfree(a.lists); dfree(a.dlists); dfree(a.Ts); dfree(a.Ss); dfree(a.srcs); dfree(a.ho); dfree(a.jobs);
   dfree(a.dscx); dfree(a.dscz);
   a = Arena();
 }
@@ -126,6 +133,9 @@ static double christoffel_group_host(const double* s, double eff, double vm) {
   double lam = 0.5 * (std::cos(2 * pa) * (s[0] - s[3]) + std::sin(2 * pa) * (s[1] + s[3]) * tan_ang + s[0] + s[3]);
   return 1000 * vm * std::sqrt(lam / s[4]) / std::cos(eff * M_PI / 180.0 - pa);
 }
+
+// material-id table capacity (the band kernel stages <= kMatLds of them in LDS)
+static const int kMaxMatIds = 4096;
 
 extern "C" {
 
@@ -157,7 +167,10 @@ int alifmm_ctx_create(int device, alifmm_ctx** out) {
 
 static void free_model(alifmm_ctx* c) {
   dfree(c->d_veln); dfree(c->d_vm); dfree(c->d_velpn); dfree(c->d_sidx); dfree(c->d_stab); dfree(c->d_gtab);
-  dfree(c->d_ptab);
+  dfree(c->d_ptab); dfree(c->d_mid); dfree(c->d_mtab);
+  c->d_mid = nullptr;
+  c->d_mtab = nullptr;
+  c->nmat = 0;
   c->d_veln = c->d_vm = c->d_stab = c->d_gtab = c->d_ptab = nullptr;
   c->d_velpn = c->d_sidx = nullptr;
   c->have_model = false;
@@ -191,6 +204,7 @@ int alifmm_set_option(alifmm_ctx* ctx, const char* name, double value) {
   if (!strcmp(name, "cdelta") && value > 0) ctx->cdelta = value;
   else if (!strcmp(name, "r0") && value >= 0) ctx->r0 = value;
   else if (!strcmp(name, "batch") && value >= 1) ctx->batch = (int)value;
+  else if (!strcmp(name, "prof")) ctx->prof = value != 0;
   else if (!strcmp(name, "exact_r") && value >= 0 && value <= 48) ctx->exact_r = (int)value;
   else return fail(ctx, ALIFMM_E_ARG, "unknown option or bad value: %s=%g", name, value);
   return ALIFMM_OK;
@@ -273,6 +287,47 @@ int alifmm_set_model(alifmm_ctx* ctx, int nnz, int nnx, const double* veln, cons
     HIPCHK(hipMemcpy(ctx->d_sidx, sidx.data(), n * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(ctx->d_stab, stab.data(), stab.size() * 8, hipMemcpyHostToDevice));
   }
+  // distinct (veln, vel_map, velpn, stiffness row) records -> per-cell material ids
+  {
+    std::map<std::array<int64_t, 4>, int> uniq;
+    std::vector<af::MatRec> recs;
+    std::vector<int> mid(n);
+    std::array<int64_t, 4> last{};
+    int last_id = -1;
+    bool ok = true;
+    for (size_t i = 0; i < n && ok; i++) {
+      std::array<int64_t, 4> key;
+      memcpy(&key[0], &veln[i], 8);
+      memcpy(&key[1], &vel_map[i], 8);
+      key[2] = vp[i];
+      key[3] = stif_den ? sidx[i] : -1;
+      if (last_id >= 0 && key == last) {
+        mid[i] = last_id;
+        continue;
+      }
+      auto it = uniq.find(key);
+      int id;
+      if (it == uniq.end()) {
+        id = (int)recs.size();
+        if (id >= kMaxMatIds) { ok = false; break; }
+        uniq.emplace(key, id);
+        recs.push_back(af::MatRec{veln[i], vel_map[i], vp[i], stif_den ? sidx[i] : -1});
+      } else {
+        id = it->second;
+      }
+      mid[i] = id;
+      last = key;
+      last_id = id;
+    }
+    if (ok) {
+      HIPCHK(dalloc(&ctx->d_mid, n));
+      HIPCHK(dalloc(&ctx->d_mtab, recs.size()));
+      HIPCHK(hipMemcpy(ctx->d_mid, mid.data(), n * 4, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(ctx->d_mtab, recs.data(), recs.size() * sizeof(af::MatRec), hipMemcpyHostToDevice));
+      ctx->nmat = (int)recs.size();
+    }
+  }
+  ctx->nstab = (int)stab.size() / 5;
   ctx->nz0 = nnz;
   ctx->nx0 = nnx;
   ctx->ncol = ncol;
@@ -302,6 +357,10 @@ static af::DevModel dev_model(const alifmm_ctx* c) {
   M.vm = c->d_vm;
   M.sidx = c->d_sidx;
   M.stab = c->d_stab;
+  M.nstab = c->nstab;
+  M.mid = c->d_mid;
+  M.mtab = c->d_mtab;
+  M.nmat = c->nmat;
   M.gtab = c->d_gtab;
   M.ptab = c->d_ptab;
   M.ncol = c->ncol;
@@ -318,8 +377,9 @@ static int ensure_arena(alifmm_ctx* ctx, int nsrc, long cells, long capL, long c
   a.capC = capC;
   a.capS = capS;
   HIPCHK(dalloc(&a.S, (size_t)nsrc * cells));
-  HIPCHK(dalloc(&a.lists, (size_t)nsrc * (3 * capL + capC)));
-  HIPCHK(dalloc(&a.V, (size_t)nsrc * capC));
+  HIPCHK(dalloc(&a.own, (size_t)nsrc * cells));
+  HIPCHK(dalloc(&a.lists, (size_t)nsrc * (3 * capL + 2 * capC)));
+  HIPCHK(dalloc(&a.dlists, (size_t)nsrc * (2 * capL + capC)));
   if (capS > 0) {
     HIPCHK(dalloc(&a.Ts, (size_t)nsrc * 2 * capS));
     HIPCHK(dalloc(&a.Ss, (size_t)nsrc * 2 * capS));
@@ -375,20 +435,26 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
     memset(&b, 0, sizeof b);
     b.T = ctx->fields[slot].d;
     b.S = a.S + (size_t)i * a.cells;
-    int* base = a.lists + (size_t)i * (3 * a.capL + a.capC);
+    b.own = a.own + (size_t)i * a.cells;
+    int* base = a.lists + (size_t)i * (3 * a.capL + 2 * a.capC);
     b.L0 = base;
     b.L1 = base + a.capL;
     b.A = base + 2 * a.capL;
     b.C = base + 3 * a.capL;
-    b.V = a.V + (size_t)i * a.capC;
+    b.Cp = base + 3 * a.capL + a.capC;
+    double* dbase = a.dlists + (size_t)i * (2 * a.capL + a.capC);
+    b.Lt0 = dbase;
+    b.Lt1 = dbase + a.capL;
+    b.V = dbase + 2 * a.capL;
     if (capS > 0) {
       b.Ts[0] = a.Ts + (size_t)i * 2 * a.capS;
       b.Ts[1] = b.Ts[0] + a.capS;
       b.Ss[0] = a.Ss + (size_t)i * 2 * a.capS;
       b.Ss[1] = b.Ss[0] + a.capS;
     }
-    HIPCHK(hipMemsetAsync(b.T, 0, (size_t)cells * 8, ctx->stream));
-    HIPCHK(hipMemsetAsync(b.S, 0xFF, (size_t)cells * 4, ctx->stream));  // kFar = -1
+    HIPCHK(hipMemsetAsync(b.T, 0xFF, (size_t)cells * 8, ctx->stream));  // far: NaN (fields.h)
+    HIPCHK(hipMemsetAsync(b.S, 0xFF, (size_t)cells * 4, ctx->stream));    // kFar = -1
+    HIPCHK(hipMemsetAsync(b.own, 0xFF, (size_t)cells * 4, ctx->stream));  // claim stamps -1
   }
   HIPCHK(hipMemcpyAsync(a.srcs, hs.data(), sizeof(af::BandSrc) * n, hipMemcpyHostToDevice, ctx->stream));
   af::DevModel M = dev_model(ctx);
@@ -410,6 +476,7 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
   P.src = a.srcs;
   P.gox = ctx->gox;
   P.goz = ctx->goz;
+  P.prof = ctx->prof;
   HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
   if (sg == 1) {
     std::vector<af::InitJob> jobs(n);
@@ -464,6 +531,10 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
     Field& f = ctx->fields[first_slot + i];
     for (int k = 0; k < 4; k++) f.steps[k] = hs[i].steps[k];
     f.sweeps = hs[i].nupd;
+    for (int k = 0; k < 6; k++) f.prof[k] = hs[i].ph[k];
+    for (int k = 0; k < 3; k++) f.prof[6 + k] = hs[i].lsum[k];
+    f.prof[9] = hs[i].lmax;
+    for (int k = 0; k < 4; k++) f.prof[10 + k] = hs[i].sub[k];
     if (hs[i].err == 2) cap_err = 1;
     else if (hs[i].err == 3) return fail(ctx, ALIFMM_E_KERNEL, "source %d: init heap overflow", i);
     else if (hs[i].err == 4) return fail(ctx, ALIFMM_E_KERNEL, "source %d: stage grid capacity", i);
@@ -533,6 +604,12 @@ int alifmm_source_stats(alifmm_ctx* ctx, int slot, int64_t* steps4, int64_t* cel
   if (steps4)
     for (int k = 0; k < 4; k++) steps4[k] = ctx->fields[slot].steps[k];
   if (cell_sweeps) *cell_sweeps = ctx->fields[slot].sweeps;
+  return ALIFMM_OK;
+}
+
+int alifmm_band_profile(alifmm_ctx* ctx, int slot, int64_t* out14) {
+  if (!ctx || slot < 0 || slot >= (int)ctx->fields.size() || !out14) return fail(ctx, ALIFMM_E_ARG, "band_profile: bad slot");
+  for (int k = 0; k < 14; k++) out14[k] = ctx->fields[slot].prof[k];
   return ALIFMM_OK;
 }
 

@@ -12,11 +12,34 @@
 
 namespace af {
 
+// Global-memory accesses through pointers the compiler cannot prove global (pointers stored in
+// device-side structs, e.g. BandSrc) would otherwise compile to flat_* instructions, whose
+// completion also counts on lgkmcnt and so serialises them against every LDS access.
+#define AF_GLOBAL __attribute__((address_space(1)))
+template <class T>
+AF_DEV T gld(const T* p) {
+  return *(const AF_GLOBAL T*)p;
+}
+template <class T>
+AF_DEV void gst(T* p, T v) {
+  *(AF_GLOBAL T*)p = v;
+}
+AF_DEV int gatomic_max(int* p, int v) { return __atomic_fetch_max((AF_GLOBAL int*)p, v, __ATOMIC_RELAXED); }
+
 constexpr double kDeg2Rad = M_PI / 180.0;
 constexpr double kRad2Deg = 180.0 / M_PI;
 
 // Python float '%' (CPython float_divmod; numba real_divmod_func_body).
+// Fast paths for |a| < 2b (every call site: angles mod 180/90/pi) give the same bits as the
+// generic fmod route: fmod(a, b) is exact, and a -/+ b is exact there by Sterbenz's lemma; the
+// only rounding is the final '+ b' of negative remainders, which the reference performs too.
 AF_DEV double pymod(double a, double b) {
+  if (b > 0) {
+    if (a >= 0 && a < b) return a == 0 ? 0.0 : a;  // -0.0 -> +0.0 as copysign(0, b)
+    if (a >= b && a < 2 * b) return a - b;
+    if (a < 0 && a >= -b) return a + b;            // a == -b: fmod gives -0.0 -> +0.0, as here
+    if (a < -b && a > -2 * b) return (a + b) + b;
+  }
   double m = fmod(a, b);
   if (m != 0.0) {
     if ((b < 0) != (m < 0)) m += b;
@@ -29,6 +52,13 @@ AF_DEV double pymod(double a, double b) {
 AF_DEV long pyround(double x) { return (long)rint(x); }
 
 // ---------------------------------------------------------------------------------------------
+// Distinct per-cell material (veln, vel_map, velpn, stiffness row): the band kernel stages the
+// table in LDS and reads one 4-byte id per cell instead of four arrays.
+struct MatRec {
+  double veln, vm;
+  int velpn, sidx;  // sidx -1: stif_den is None
+};
+
 // Model resident in HBM (uploaded once per set_model, shared by every source on the GPU).
 struct DevModel {
   int nz0, nx0;          // coarse grid
@@ -37,9 +67,13 @@ struct DevModel {
   const double* vm;      // velocity scale
   const int* sidx;       // stiffness row index per cell, or nullptr when stif_den is None
   const double* stab;    // unique stiffness rows [n][5] (exact int64 values as doubles)
+  int nstab;             // number of unique stiffness rows
   const double* gtab;    // group velocity table (361, ncol)
   const double* ptab;    // phase velocity table (361, ncol)
   int ncol;
+  const int* mid;        // material id per cell (into mtab), or nullptr when there are too many
+  const MatRec* mtab;
+  int nmat;
 };
 
 // Logical grid -> coarse cell: f = lo1 + (a + side1)/s1 ; c = lo2 + (f + side2)/s2
@@ -67,12 +101,12 @@ struct CellMat {
 AF_DEV CellMat cell_mat(const DevModel& M, const MatView& v, int iz, int ix) {
   long c = mv_cell(M, v, iz, ix);
   CellMat r;
-  double a = M.veln[c];
-  double b = M.vm[c];
+  double a = gld(M.veln + c);
+  double b = gld(M.vm + c);
   r.veln = v.quant ? (double)(int)a : a;
   r.vm = v.quant ? (double)(float)b : b;
-  r.velpn = M.velpn[c];
-  r.stif = M.sidx ? M.stab + 5 * (long)M.sidx[c] : nullptr;
+  r.velpn = gld(M.velpn + c);
+  r.stif = M.sidx ? M.stab + 5 * (long)gld(M.sidx + c) : nullptr;
   return r;
 }
 

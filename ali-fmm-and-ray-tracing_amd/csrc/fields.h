@@ -4,12 +4,17 @@
 
 namespace af {
 
+// Far cells of the HBM grids hold NaN (kFarT) instead of the reference's 0 so that validity can
+// be read from T alone (NbFieldT); every value read through an accessor maps NaN back to 0, the
+// reference's ttn of a never-relaxed node.
+AF_DEV double far0(double v) { return v == v ? v : 0.0; }
+
 struct GField {
   const double* T;
   const int* S;
   int nz, nx;
-  AF_DEV int st(long z, long x) const { return z >= nz ? -1 : S[z * nx + x]; }
-  AF_DEV double tt(long z, long x) const { return z >= nz ? 0.0 : T[z * nx + x]; }
+  AF_DEV int st(long z, long x) const { return z >= nz ? -1 : gld(S + z * nx + x); }
+  AF_DEV double tt(long z, long x) const { return z >= nz ? 0.0 : far0(gld(T + z * nx + x)); }
 };
 
 // Register copy of the 12 cells update() reads around (iz, ix): (0,+-1) (+-1,0) (+-1,+-1) (0,+-2)
@@ -49,8 +54,8 @@ struct NbField {
     }
 #pragma unroll
     for (int k = 0; k < 12; k++) {
-      s[k] = S[f[k]];
-      t[k] = T[f[k]];
+      s[k] = gld(S + f[k]);
+      t[k] = gld(T + f[k]);
     }
     unsigned m = 0;
 #pragma unroll
@@ -58,6 +63,60 @@ struct NbField {
       if (in[k] && s[k] >= 0) m |= 1u << k;
       if (!in[k]) t[k] = 0.0;
     }
+    vm = m;
+    t0 = t[0]; t1 = t[1]; t2 = t[2]; t3 = t[3]; t4 = t[4]; t5 = t[5];
+    t6 = t[6]; t7 = t[7]; t8 = t[8]; t9 = t[9]; t10 = t[10]; t11 = t[11];
+  }
+};
+
+// As NbField, for update() (validity = nsts >= 0, i.e. known or close) on an HBM grid whose far
+// cells hold NaN: 12 loads of T, no status loads.
+struct NbFieldT {
+  int iz, ix;
+  unsigned vm;  // bit k: valid
+  double t0, t1, t2, t3, t4, t5, t6, t7, t8, t9, t10, t11;
+  AF_DEV int st(long z, long x) const { return (vm >> NbField::slot(z - iz, x - ix)) & 1u ? 0 : -1; }
+  AF_DEV double tt(long z, long x) const {
+    const int k = NbField::slot(z - iz, x - ix);
+    return k == 0 ? t0 : k == 1 ? t1 : k == 2 ? t2 : k == 3 ? t3 : k == 4 ? t4 : k == 5 ? t5 : k == 6 ? t6
+         : k == 7 ? t7 : k == 8 ? t8 : k == 9 ? t9 : k == 10 ? t10 : t11;
+  }
+  // 8 loads: rows z-2 and z+2 one double each; rows z-1, z+1 (x-1, x) as one 16-byte load plus
+  // (x+1); row z (x-2, x-1) and (x+1, x+2) as 16-byte loads.  Addresses are clamped into the
+  // grid; values at out-of-grid columns are never read by update() (it bounds-checks first).
+  AF_DEV void load(const double* T, int nz, int nx, int z, int x) {
+    iz = z;
+    ix = x;
+    const int n = nz * nx;
+    const int p = z * nx + x;
+    auto cl = [n](int c, int w) { return c < 0 ? 0 : c > n - w ? n - w : c; };
+    auto ld2 = [&](int c, double& a, double& b) {
+      if (c >= 0 && c <= n - 2) {
+        double v[2];
+        __builtin_memcpy(v, (const AF_GLOBAL char*)(T + c), 16);
+        a = v[0];
+        b = v[1];
+      } else {  // grid corners: element-wise, so clamping never shifts a value into a valid slot
+        a = gld(T + cl(c, 1));
+        b = gld(T + cl(c + 1, 1));
+      }
+    };
+    // slots: 0 (0,-2) 1 (0,-1) 2 (0,+1) 3 (0,+2) 4 (-2,0) 5 (-1,0) 6 (+1,0) 7 (+2,0)
+    //        8 (-1,-1) 9 (-1,+1) 10 (+1,-1) 11 (+1,+1)
+    double t[12];
+    ld2(p - 2, t[0], t[1]);
+    ld2(p + 1, t[2], t[3]);
+    ld2(p - nx - 1, t[8], t[5]);
+    t[9] = gld(T + cl(p - nx + 1, 1));
+    ld2(p + nx - 1, t[10], t[6]);
+    t[11] = gld(T + cl(p + nx + 1, 1));
+    t[4] = gld(T + cl(p - 2 * nx, 1));
+    t[7] = gld(T + cl(p + 2 * nx, 1));
+    const int dz[12] = {0, 0, 0, 0, -2, -1, 1, 2, -1, -1, 1, 1};
+    unsigned m = 0;
+#pragma unroll
+    for (int k = 0; k < 12; k++)
+      if (z + dz[k] < nz && t[k] == t[k]) m |= 1u << k;
     vm = m;
     t0 = t[0]; t1 = t[1]; t2 = t[2]; t3 = t[3]; t4 = t[4]; t5 = t[5];
     t6 = t[6]; t7 = t[7]; t8 = t[8]; t9 = t[9]; t10 = t[10]; t11 = t[11];

@@ -1,54 +1,80 @@
 // fmm_band.hip — band-synchronous ("Delta-stepping") FMM on gfx950.
 //
 // Replaces the reference's heap-ordered main loop (travel :2055-2102, travel_finer_grid
-// :2775-2817).  One persistent 1024-thread workgroup per source; all synchronisation is
+// :2775-2817).  One persistent 512-thread workgroup per source; all synchronisation is
 // workgroup-local (s_barrier), so sources never wait on each other.  Per step:
-//   1  Tmin over the close list (wave DPP min + LDS)                       [T gather]
-//   2  accept every close cell with T <= Tmin + delta(Tmin) -> known, compact the rest
-//   3  for each (accepted cell, direction): claim the neighbour with one atomicCAS on its
-//      status (far->far_cand / close->close_cand; claims never change update() validity),
-//      evaluate the reference's update() (fallback fouds18_A()) against the post-acceptance
-//      state, Jacobi-style, into the candidate list
-//   4  commit: T <- new value, status -> close, new close cells appended to the list
-// Lists are appended with one LDS atomic per wave (ballot + mbcnt).  delta = cdelta*dn/vmax,
-// narrowed in proportion to Tmin while Tmin < r0*dnx/vmax (near-source schedule).
-// The same routine runs the refined stage grids of travel_finer_grid (mode 1).
+//   1  Tmin over the close set — LDS only: the close set is an LDS slot array of (cell, T);
+//      a close cell keeps its slot until accepted (nsts = 1 + slot, the reference's "heap index
+//      > 0" convention), freed slots go to a free stack
+//   2  accept every close cell with T <= Tmin + delta(Tmin) -> known (nsts 0)
+//   3a claim: the neighbours of the accepted cells are deduplicated in an LDS hash set; each
+//      distinct neighbour's nsts is read once (known: dropped; close: its slot; far: fresh)
+//   3b evaluate the reference's update() (fallback fouds18_A()) for every claimed neighbour,
+//      Jacobi-style against the post-acceptance state (far cells hold NaN: fields.h NbFieldT)
+//   4  commit: T <- new value; far cells take a free slot (nsts = 1 + slot), close cells update
+//      their slot's T
+// Lists live in LDS and spill to global arrays of the same index past the LDS capacity.
+// delta = cdelta*dn/vmax, narrowed in proportion to Tmin while Tmin < r0*dnx/vmax.
 #include "kernels.h"
 #include "local_ops.h"
 #include "fields.h"
 
 namespace af {
 
-
-
-constexpr int kThreads = 512;
+#ifndef AF_THREADS
+#define AF_THREADS 512
+#endif
+#ifndef AF_EVAL2
+#define AF_EVAL2 0
+#endif
+#ifndef AF_FOUDS_NOINLINE
+#define AF_FOUDS_NOINLINE 0
+#endif
+constexpr int kThreads = AF_THREADS;
 constexpr int kWaves = kThreads / 64;
-// LDS-resident heads of the per-step lists; entries past the cap spill to the global arrays of
-// the same index (BandSrc L0/L1, A, C, V), so LDS bounds only speed, never capacity.
-constexpr int kLcap = 6144, kAcap = 4096, kEcap = 6144;
+#ifndef AF_LCAP
+#define AF_LCAP 3584
+#endif
+#ifndef AF_HASH_LOG2
+#define AF_HASH_LOG2 13
+#endif
+#ifndef AF_HASH_ITEMS
+#define AF_HASH_ITEMS 6144
+#endif
+constexpr int kLcap = AF_LCAP, kAcap = 2048, kEcap = 2816;
+constexpr int kHash = 1 << AF_HASH_LOG2;    // LDS hash set of claimed cells
+constexpr int kHashItems = AF_HASH_ITEMS;  // (load <= 0.75) steps with more claim items use the global stamps
+constexpr int kStabLds = 64;    // stiffness rows staged in LDS (more rows: global)
+constexpr int kPtabLds = 722;   // phase-table doubles staged in LDS (361 x ncol <= 2 columns)
+constexpr int kMatLds = 256;    // material records staged in LDS (DevModel::mtab)
 
 struct BandLds {
   double red[kWaves];
-  double Vl[kEcap];
-  int cnt[2][3];  // [parity][A, L2, E]
-  int finished;
+  double Lt[kLcap];  // close set: T of the slot (+inf: free)
+  double Vl[kEcap];  // evaluated values
+  double stab[kStabLds * 5];
+  double ptab[kPtabLds];
+  MatRec mat[kMatLds];
+  int Ll[kLcap];     // close set: cell of the slot
+  int Fs[kLcap];     // free slots
+  int Al[kAcap];     // accepted cells
+  int El[kEcap];     // claimed cells
+  int Ep[kEcap];     // slot of a claimed close cell, -1 for a far cell
+  alignas(16) int H[kHash];  // hash set of this step's claimed cells (cell + 1; 0 empty)
+  int nA, nE, nF, hi, taken;
   int err;
-  int Ll[2][kLcap];
-  int Al[kAcap];
-  int El[kEcap];
 };
 
-template <int CAP>
+template <class T, int CAP>
 struct HList {
-  int* l;  // LDS head
-  int* g;  // global array (same indexing)
-  AF_DEV int get(int i) const { return i < CAP ? l[i] : g[i]; }
-  AF_DEV void put(int i, int v) const {
+  T* l;  // LDS head
+  T* g;  // global array (same indexing)
+  AF_DEV T get(int i) const { return i < CAP ? l[i] : gld(g + i); }
+  AF_DEV void put(int i, T v) const {
     if (i < CAP) l[i] = v;
-    else g[i] = v;
+    else gst(g + i, v);
   }
 };
-typedef HList<kLcap> LList;
 
 AF_DEV int lane_id() { return threadIdx.x & 63; }
 
@@ -76,185 +102,274 @@ AF_DEV double wave_min(double v) {
   return v;
 }
 
+AF_DEV int nb_cell(int c, int d, int nz, int nx) {
+  const int iz = c / nx, ix = c - iz * nx;
+  const int z = iz + (d == 2 ? -1 : d == 3 ? 1 : 0);
+  const int x = ix + (d == 0 ? -1 : d == 1 ? 1 : 0);
+  return (z < 0 || z >= nz || x < 0 || x >= nx) ? -1 : z * nx + x;
+}
+
 struct RunCfg {
   int nz, nx;
   double dnx, dnz;  // update() spacing and fouds18 dnz
   MatView mv;
-  int stage;        // window-edge finish test enabled
-  int isx, isz, max_dist;
   double delta, t0;
 };
 
-AF_DEV LList band_list(BandLds* sh, BandSrc* B, int k) { return LList{sh->Ll[k], k ? B->L1 : B->L0}; }
+// fouds18_A() fallback out of line: rare, and inlined its live ranges (~180 VGPRs) would set
+// the whole kernel's register budget
+#if AF_FOUDS_NOINLINE
+__device__ __noinline__
+#else
+AF_DEV
+#endif
+double fouds18_global(const GField& F, const DevModel& M, const CellMat& cm, int z, int x, double dnx, double dnz,
+                      int nx, int nz) {
+  return fouds18(F, M, cm, z, x, dnx, dnz, nx, nz);
+}
 
-// one band run; returns steps.  T/S in global memory, list heads and counts in LDS.
-// lc: index (0/1) of the list holding the nL close cells on entry and on return.
-AF_DEV long long band_run(const BandParams& P, BandLds* sh, BandSrc* B, double* T, int* S, int& lc, int& nL,
-                          const RunCfg& R, long long* nupd) {
+// material of main-grid cell (z, x): LDSMAT = one id load + the LDS record; else four arrays
+template <bool LDSMAT>
+AF_DEV CellMat band_mat(const DevModel& M, const BandLds* sh, const MatView& v, int z, int x) {
+  if (!LDSMAT) return cell_mat(M, v, z, x);
+  const MatRec m = sh->mat[gld(M.mid + mv_cell(M, v, z, x))];
+  CellMat r;
+  r.velpn = m.velpn;
+  r.veln = v.quant ? (double)(int)m.veln : m.veln;
+  r.vm = v.quant ? (double)(float)m.vm : m.vm;
+  r.stif = m.sidx >= 0 ? sh->stab + 5 * m.sidx : nullptr;
+  return r;
+}
+
+AF_DEV unsigned hash_slot(int key) { return ((unsigned)key * 2654435761u) >> (32 - AF_HASH_LOG2); }
+
+// one band run over the main grid; returns steps.  T/S in global memory, sets and lists in LDS.
+// On entry the close set holds slots [0, sh->hi) with sh->nF free slots in sh->Fs.
+template <bool LDSMAT>
+AF_DEV long long band_run(const BandParams& P, BandLds* sh, BandSrc* B, const RunCfg& R) {
   const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
   const int nz = R.nz, nx = R.nx;
-  const long ncell = (long)nz * nx;
+  double* T = B->T;
+  int* S = B->S;
+  int* own = B->own;  // claim stamps (host-initialised to -1)
   const GField F{T, S, nz, nx};
-  const HList<kAcap> AL{sh->Al, B->A};
-  const HList<kEcap> EL{sh->El, B->C};
-  long long steps = 0;
-  long long myupd = 0;
-  if (tid == 0) {
-    sh->finished = 0;
-    for (int p = 0; p < 2; p++)
-      for (int q = 0; q < 3; q++) sh->cnt[p][q] = 0;
+  DevModel M = P.M;
+  if (LDSMAT) M.ptab = sh->ptab;
+  const HList<int, kLcap> L{sh->Ll, B->L0};
+  const HList<double, kLcap> Lt{sh->Lt, B->Lt0};
+  const HList<int, kLcap> FS{sh->Fs, B->L1};
+  const HList<int, kAcap> AL{sh->Al, B->A};
+  const HList<int, kEcap> EL{sh->El, B->C};
+  const HList<int, kEcap> EP{sh->Ep, B->Cp};
+  const HList<double, kEcap> VL{sh->Vl, B->V};
+  long long steps = 0, myupd = 0;
+  const bool prof = P.prof && tid == 0;
+  long long ph[6] = {0, 0, 0, 0, 0, 0}, ls[3] = {0, 0, 0}, lmax = 0, tk = prof ? wall_clock64() : 0;
+  long long sub[4] = {0, 0, 0, 0}, ts = 0;
+#define AF_SUB(k)                      \
+  if (prof) {                          \
+    __builtin_amdgcn_s_waitcnt(0);     \
+    long long t_ = wall_clock64();     \
+    sub[k] += t_ - ts;                 \
+    ts = t_;                           \
   }
-  __syncthreads();
+#define AF_TICK(k)                 \
+  if (prof) {                      \
+    long long t_ = wall_clock64(); \
+    ph[k] += t_ - tk;              \
+    tk = t_;                       \
+  }
   while (true) {
-    const int par = (int)(steps & 1);
-    const LList L = band_list(sh, B, lc), L2 = band_list(sh, B, lc ^ 1);
-    // ---- phase 1: Tmin over the close list (4 gathers in flight per lane) ----
+    const int hi = sh->hi;
+    const int live = hi - sh->nF;
+    // ---- phase 1: Tmin over the close set (LDS); clear the hash set ----
     double tmin = INFINITY;
-    for (int e0 = tid; e0 < nL; e0 += 4 * kThreads) {
-      int c[4];
-      double t[4];
-#pragma unroll
-      for (int u = 0; u < 4; u++) {
-        int e = e0 + u * kThreads;
-        c[u] = e < nL ? L.get(e) : -1;
-      }
-#pragma unroll
-      for (int u = 0; u < 4; u++) t[u] = T[c[u] < 0 ? 0 : c[u]];
-#pragma unroll
-      for (int u = 0; u < 4; u++)
-        if (c[u] >= 0) tmin = fmin(tmin, t[u]);
-    }
+    for (int e = tid; e < hi; e += kThreads) tmin = fmin(tmin, Lt.get(e));
+    for (int k = tid * 4; k < kHash; k += kThreads * 4) *(int4*)&sh->H[k] = make_int4(0, 0, 0, 0);
     tmin = wave_min(tmin);
     if (lane == 0) sh->red[wv] = tmin;
+    if (tid == 0) {
+      sh->nA = 0;
+      sh->nE = 0;
+      sh->taken = 0;
+    }
     __syncthreads();
+    AF_TICK(0)
+    if (live <= 0) break;
     tmin = sh->red[0];
     for (int w = 1; w < kWaves; w++) tmin = fmin(tmin, sh->red[w]);
-    if (nL == 0) break;
     double dl = R.delta;
     if (R.t0 > 0 && tmin < R.t0) dl = R.delta * (tmin / R.t0);
     const double thr = tmin + dl;
-    int* cA = &sh->cnt[par][0];
-    int* cL2 = &sh->cnt[par][1];
-    int* cE = &sh->cnt[par][2];
-    // ---- phase 2: accept / compact ----
-    for (int e0 = wv * 64; e0 < nL; e0 += 2 * kThreads) {
-      int c[2];
-      double t[2];
-#pragma unroll
-      for (int u = 0; u < 2; u++) {
-        int e = e0 + u * kThreads + lane;
-        c[u] = e < nL ? L.get(e) : -1;
+    // ---- phase 2: accept (-> known, slot freed) ----
+    for (int e0 = wv * 64; e0 < hi; e0 += kThreads) {
+      const int e = e0 + lane;
+      const double t = e < hi ? Lt.get(e) : INFINITY;
+      const bool acc = t <= thr;
+      const int sa = wave_push(&sh->nA, acc, P.capL, &sh->err);
+      if (sa >= 0) {
+        const int c = L.get(e);
+        AL.put(sa, c);
+        gst(S + c, (int)kKnown);
+        Lt.put(e, INFINITY);
       }
-#pragma unroll
-      for (int u = 0; u < 2; u++) t[u] = T[c[u] < 0 ? 0 : c[u]];
-#pragma unroll
-      for (int u = 0; u < 2; u++) {
-        bool valid = c[u] >= 0;
-        bool acc = valid && t[u] <= thr;
-        if (acc) S[c[u]] = kKnown;
-        int sa = wave_push(cA, acc, P.capL, &sh->err);
-        if (sa >= 0) AL.put(sa, c[u]);
-        int sl = wave_push(cL2, valid && !acc, P.capL, &sh->err);
-        if (sl >= 0) L2.put(sl, c[u]);
-      }
+      const int sf = wave_push(&sh->nF, acc, P.capL, &sh->err);
+      if (sf >= 0) FS.put(sf, e);
     }
     __syncthreads();
-    const int nA = min(*cA, P.capL);
-    if (tid == 0) {  // reset the other parity's counters (read by everyone before this step's barrier)
-      sh->cnt[par ^ 1][0] = 0;
-      sh->cnt[par ^ 1][1] = 0;
-      sh->cnt[par ^ 1][2] = 0;
-    }
-    // ---- phase 3a: claim the neighbours of the accepted cells (far->far_cand, close->close_cand) ----
+    AF_TICK(1)
+    const int nA = min(sh->nA, P.capL);
+    // ---- phase 3a: claim.  Each distinct neighbour of the accepted cells is owned by one item.
+    // Steps with <= kHashItems items dedupe in the LDS hash set; larger steps (long fronts) stamp
+    // own[cell] with the step number by a global atomicMax (winner: previous stamp < step).
     const int nItems = 4 * nA;
-    for (int q0 = wv * 64; q0 < nItems; q0 += kThreads) {
-      int q = q0 + lane;
-      bool won = false;
-      int r = 0;
-      if (q < nItems) {
-        int a = AL.get(q >> 2), dir = q & 3;
-        int iz = a / nx, ix = a - iz * nx;
-        int z = iz + (dir == 2 ? -1 : dir == 3 ? 1 : 0);
-        int x = ix + (dir == 0 ? -1 : dir == 1 ? 1 : 0);
-        if (z < 0 || z >= nz || x < 0 || x >= nx) {
-          if (R.stage) {
-            // window-edge finish test (:1651-1652, :1673-1674)
-            if (dir < 2 ? (abs(R.isx - x) == R.max_dist + 1) : (abs(R.isz - z) == R.max_dist + 1))
-              sh->finished = 1;
+    const bool use_hash = nItems <= kHashItems;
+    const int stamp = (int)steps;
+    for (int q0 = wv * 64 * 8; q0 < nItems; q0 += kThreads * 8) {
+      int r[8], s[8], o[8];
+      if (prof) ts = wall_clock64();
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int q = q0 + u * 64 + lane;
+        int c = q < nItems ? nb_cell(AL.get(q >> 2), q & 3, nz, nx) : -1;
+        if (use_hash && c >= 0) {  // insert c + 1; the inserting item owns the cell
+          unsigned h = hash_slot(c);
+          for (int probe = 0;; probe++) {
+            const int prev = atomicCAS(&sh->H[h], 0, c + 1);
+            if (prev == 0) break;
+            if (prev == c + 1 || probe >= kHash) {
+              if (probe >= kHash) sh->err = 5;
+              c = -1;
+              break;
+            }
+            h = (h + 1) & (kHash - 1);
           }
-        } else {
-          r = z * nx + x;
-          int s = S[r];
-          bool fresh = false;
-          if (s == kFar) fresh = won = atomicCAS(&S[r], kFar, kFarCand) == kFar;
-          else if (s == kClose) won = atomicCAS(&S[r], kClose, kCloseCand) == kClose;
-          if (fresh) r = -(r + 1);  // far -> close: remembered here, never re-read from S (L1 may be stale)
+        }
+        r[u] = c;
+      }
+      AF_SUB(0)
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        s[u] = r[u] >= 0 ? gld(S + r[u]) : (int)kKnown;
+        o[u] = (!use_hash && r[u] >= 0) ? gatomic_max(own + r[u], stamp) : -1;
+      }
+      AF_SUB(1)
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const bool won = s[u] != kKnown && o[u] < stamp;
+        const int se = wave_push(&sh->nE, won, P.capC, &sh->err);
+        if (se >= 0) {
+          EL.put(se, r[u]);
+          EP.put(se, s[u] > 0 ? s[u] - 1 : -1);
         }
       }
-      int se = wave_push(cE, won, P.capC, &sh->err);
-      if (se >= 0) EL.put(se, r);
+      AF_SUB(2)
     }
     __syncthreads();
-    const int nE = min(*cE, P.capC);
-    // ---- phase 3b: evaluate (Jacobi against the post-acceptance state), all lanes busy ----
+    AF_TICK(2)
+    const int nE = min(sh->nE, P.capC);
+    // ---- phase 3b: evaluate ----
+#if AF_EVAL2
+    // two cells per lane per round trip
+    for (int e0 = tid; e0 < nE; e0 += 2 * kThreads) {
+      const int e1 = e0 + kThreads;
+      const bool has1 = e1 < nE;
+      const int r0 = EL.get(e0), r1 = has1 ? EL.get(e1) : r0;
+      const int z0 = r0 / nx, x0 = r0 - z0 * nx, z1 = r1 / nx, x1 = r1 - z1 * nx;
+      const CellMat m0 = band_mat<LDSMAT>(M, sh, R.mv, z0, x0);
+      const CellMat m1 = band_mat<LDSMAT>(M, sh, R.mv, z1, x1);
+      NbFieldT n0, n1;
+      n0.load(T, nz, nx, z0, x0);
+      n1.load(T, nz, nx, z1, x1);
+      VL.put(e0, update(n0, M, m0, z0, x0, R.dnx, nz, nx));
+      if (has1) VL.put(e1, update(n1, M, m1, z1, x1, R.dnx, nz, nx));
+      myupd += has1 ? 2 : 1;
+    }
+#else
     for (int e = tid; e < nE; e += kThreads) {
-      int r = EL.get(e);
-      if (r < 0) r = -r - 1;
-      int z = r / nx, x = r - z * nx;
-      CellMat cm = cell_mat(P.M, R.mv, z, x);
-      NbField nb;
-      nb.load(T, S, nz, nx, z, x);
-      double v = update(nb, P.M, cm, z, x, R.dnx, nz, nx);
-      if (e < kEcap) sh->Vl[e] = v;
-      else B->V[e] = v;
+      const int r = EL.get(e);
+      const int z = r / nx, x = r - z * nx;
+      if (prof) ts = wall_clock64();
+      const CellMat cm = band_mat<LDSMAT>(M, sh, R.mv, z, x);
+      NbFieldT nb;
+      nb.load(T, nz, nx, z, x);
+      AF_SUB(3)
+      VL.put(e, update(nb, M, cm, z, x, R.dnx, nz, nx));
       myupd++;
     }
-    // fouds18_A() fallback (update() found no usable stencil): a loop of its own over the same
-    // entries, so its live ranges never overlap update()'s (no register spills)
+#endif
+    AF_TICK(3)
+    // fouds18_A() fallback (update() found no usable stencil): a loop of its own, so its live
+    // ranges never overlap update()'s
     for (int e = tid; e < nE; e += kThreads) {
-      double v = e < kEcap ? sh->Vl[e] : B->V[e];
-      if (v == -1.0) {
-        int r = EL.get(e);
-        if (r < 0) r = -r - 1;
-        int z = r / nx, x = r - z * nx;
-        CellMat cm = cell_mat(P.M, R.mv, z, x);
-        v = fouds18(F, P.M, cm, z, x, R.dnx, R.dnz, nx, nz);
-        if (e < kEcap) sh->Vl[e] = v;
-        else B->V[e] = v;
+      if (VL.get(e) == -1.0) {
+        const int r = EL.get(e);
+        const int z = r / nx, x = r - z * nx;
+        const CellMat cm = band_mat<LDSMAT>(M, sh, R.mv, z, x);
+        VL.put(e, fouds18_global(F, M, cm, z, x, R.dnx, R.dnz, nx, nz));
       }
     }
     __syncthreads();
-    // ---- phase 4: commit (same lane <-> entry map as 3b) ----
+    AF_TICK(4)
+    // ---- phase 4: commit; far cells take free slots (top of the stack first), then new ones ----
+    const int nF = sh->nF;
     for (int e0 = wv * 64; e0 < nE; e0 += kThreads) {
-      int e = e0 + lane;
+      const int e = e0 + lane;
       bool fresh = false;
       int r = 0;
+      double v = 0.0;
       if (e < nE) {
         r = EL.get(e);
-        fresh = r < 0;
-        if (fresh) r = -r - 1;
-        T[r] = e < kEcap ? sh->Vl[e] : B->V[e];
-        S[r] = kClose;
+        v = VL.get(e);
+        const int p = EP.get(e);
+        gst(T + r, v);
+        if (p >= 0) Lt.put(p, v);
+        else fresh = true;
       }
-      int sl = wave_push(cL2, fresh, P.capL, &sh->err);
-      if (sl >= 0) L2.put(sl, r);
+      const int k = wave_push(&sh->taken, fresh, 1 << 30, &sh->err);
+      if (k >= 0) {
+        const int slot = k < nF ? FS.get(nF - 1 - k) : hi + (k - nF);
+        if (slot >= P.capL) {
+          sh->err = 2;
+        } else {
+          L.put(slot, r);
+          Lt.put(slot, v);
+          gst(S + r, 1 + slot);
+        }
+      }
     }
     __syncthreads();
-    nL = min(*cL2, P.capL);
-    lc ^= 1;
+    AF_TICK(5)
+    if (tid == 0) {
+      const int tk_ = sh->taken;
+      sh->nF = max(0, nF - tk_);
+      sh->hi = hi + max(0, tk_ - nF);
+    }
+    if (prof) {
+      ls[0] += live;
+      ls[1] += nA;
+      ls[2] += nE;
+      lmax = max(lmax, (long long)hi);
+    }
     steps++;
-    if (sh->finished || sh->err) break;
+    __syncthreads();
+    if (sh->err) break;
   }
-  if (nupd) {
-    for (int o = 32; o > 0; o >>= 1) myupd += __shfl_xor(myupd, o);
-    if (lane == 0 && myupd) atomicAdd((unsigned long long*)nupd, (unsigned long long)myupd);
+  for (int o = 32; o > 0; o >>= 1) myupd += __shfl_xor(myupd, o);
+  if (lane == 0 && myupd) atomicAdd((unsigned long long*)&B->nupd, (unsigned long long)myupd);
+  if (prof) {
+    for (int k = 0; k < 6; k++) B->ph[k] += ph[k];
+    for (int k = 0; k < 3; k++) B->lsum[k] += ls[k];
+    for (int k = 0; k < 4; k++) B->sub[k] += sub[k];
+    B->lmax = max(B->lmax, lmax);
   }
+#undef AF_TICK
+#undef AF_SUB
   __syncthreads();
-  (void)ncell;
   return steps;
 }
 
-template <int MODE>
+template <int MODE, bool LDSMAT>
 __global__ __launch_bounds__(kThreads) void fmm_band_kernel(BandParams P) {
   __shared__ BandLds sh;
   const int src = blockIdx.x;
@@ -262,46 +377,55 @@ __global__ __launch_bounds__(kThreads) void fmm_band_kernel(BandParams P) {
   BandSrc* B = P.src + src;
   const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
   if (tid == 0) {
-    for (int p = 0; p < 2; p++)
-      for (int q = 0; q < 3; q++) sh.cnt[p][q] = 0;
+    sh.hi = 0;
+    sh.nF = 0;
     sh.err = 0;
-    sh.finished = 0;
+  }
+  if (LDSMAT) {
+    for (int k = tid; k < 5 * P.M.nstab; k += kThreads) sh.stab[k] = P.M.stab[k];
+    for (int k = tid; k < 361 * P.M.ncol; k += kThreads) sh.ptab[k] = P.M.ptab[k];
+    for (int k = tid; k < P.M.nmat; k += kThreads) sh.mat[k] = P.M.mtab[k];
   }
   __syncthreads();
-  int lc = 0;
-  int nL = 0;
-  const double t0 = P.r0 * P.dnx / P.vmax;
-
+  const HList<int, kLcap> L0{sh.Ll, B->L0};
+  const HList<double, kLcap> Lt0{sh.Lt, B->Lt0};
   if (MODE == 0) {
-    // ---------------- travel(): hand-over of the exact-heap stage 3 (fmm_init_kernel) ----------------
+    // ---------------- travel(): hand-over of the exact-heap init (fmm_init_kernel) ----------------
     const HandoverOut* H = P.ho + src;
     if (tid == 0) sh.err = H->err ? 3 : 0;
     const int n = H->n;
     for (int k0 = wv * 64; k0 < n; k0 += kThreads) {
-      int k = k0 + lane;
+      const int k = k0 + lane;
       bool push = false;
       int c = 0;
+      double t = 0.0;
       if (k < n) {
         c = H->cell[k];
-        B->T[c] = H->ttn[k];
-        B->S[c] = H->cls[k] == 1 ? kKnown : kClose;
-        push = H->cls[k] != 1;
+        t = H->ttn[k];
+        gst(B->T + c, t);
+        if (H->cls[k] == 1) gst(B->S + c, (int)kKnown);
+        else push = true;
       }
-      int s = wave_push(&sh.cnt[1][1], push, P.capL, &sh.err);
-      if (s >= 0) band_list(&sh, B, lc).put(s, c);
+      const int s = wave_push(&sh.hi, push, P.capL, &sh.err);
+      if (s >= 0) {
+        L0.put(s, c);
+        Lt0.put(s, t);
+        gst(B->S + c, 1 + s);
+      }
     }
-    __syncthreads();
-    nL = sh.cnt[1][1];
-    __syncthreads();
-    if (tid == 0) sh.cnt[1][1] = 0;
-    __syncthreads();
   } else {
     // ---------------- travel_finer_grid(): stages + exact prefix ran in fmm_exact_kernel ----------------
-    if (tid == 0 && B->err) sh.err = B->err;
-    nL = B->nl0;
-    for (int k = tid; k < min(nL, kLcap); k += kThreads) sh.Ll[0][k] = B->L0[k];
-    __syncthreads();
+    if (tid == 0) {
+      if (B->err) sh.err = B->err;
+      sh.hi = B->nl0;
+    }
+    for (int k = tid; k < B->nl0; k += kThreads) {
+      const int c = gld(B->L0 + k);
+      if (k < kLcap) sh.Ll[k] = c;
+      Lt0.put(k, gld(B->T + c));
+    }
   }
+  __syncthreads();
   // ---------------- main grid ----------------
   if (!sh.err) {
     RunCfg R;
@@ -313,17 +437,15 @@ __global__ __launch_bounds__(kThreads) void fmm_band_kernel(BandParams P) {
       R.mv = MatView{1, 0, 0, 1, 0, 0, 1, 0, 0, 0, 0};
     else
       R.mv = MatView{P.sg, (P.sg - 1) / 2, 0, P.sg, (P.sg - 1) / 2, 0, 1, 0, 0, 0, 1};
-    R.stage = 0;
-    R.isx = R.isz = R.max_dist = 0;
     R.delta = P.cdelta * P.dnx / P.vmax;
-    R.t0 = t0;
-    long long st = band_run(P, &sh, B, B->T, B->S, lc, nL, R, &B->nupd);
+    R.t0 = P.r0 * P.dnx / P.vmax;
+    const long long st = band_run<LDSMAT>(P, &sh, B, R);
     if (tid == 0) B->steps[3] = st;
   }
   if (tid == 0) B->err = sh.err;
 }
 
-// final scaling of travel_finer_grid (:2832 ttn / subgrid_size) fused with nothing else: one pass
+// final scaling of travel_finer_grid (:2832 ttn / subgrid_size)
 __global__ void scale_kernel(double* T, long n, double inv) {
   long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   long stride = (long)gridDim.x * blockDim.x;
@@ -333,10 +455,17 @@ __global__ void scale_kernel(double* T, long n, double inv) {
 }  // namespace af
 
 extern "C" hipError_t af_launch_band(const af::BandParams* P, hipStream_t stream) {
-  if (P->mode == 0)
-    hipLaunchKernelGGL(af::fmm_band_kernel<0>, dim3(P->nsrc), dim3(af::kThreads), 0, stream, *P);
-  else
-    hipLaunchKernelGGL(af::fmm_band_kernel<1>, dim3(P->nsrc), dim3(af::kThreads), 0, stream, *P);
+  const bool lds = P->M.mid && P->M.nmat <= af::kMatLds && P->M.nstab <= af::kStabLds &&
+                   361 * P->M.ncol <= af::kPtabLds;
+  // (mode 1 hands over fmm_exact_kernel's close list in L0; the band run keeps it there)
+  const dim3 g(P->nsrc), b(af::kThreads);
+  if (P->mode == 0) {
+    if (lds) hipLaunchKernelGGL((af::fmm_band_kernel<0, true>), g, b, 0, stream, *P);
+    else hipLaunchKernelGGL((af::fmm_band_kernel<0, false>), g, b, 0, stream, *P);
+  } else {
+    if (lds) hipLaunchKernelGGL((af::fmm_band_kernel<1, true>), g, b, 0, stream, *P);
+    else hipLaunchKernelGGL((af::fmm_band_kernel<1, false>), g, b, 0, stream, *P);
+  }
   return hipGetLastError();
 }
 

@@ -11,8 +11,8 @@
 // 24 prefetched loads each, NbField).  One workgroup (one wave) per source; the walk is serial
 // (lane 0), the other lanes clear grids and fill the straight-ray footprint.
 //
-// Output for the band kernel: main-grid statuses known 0 / close 1 / far -1 and the close cells
-// in L0 (count in BandSrc::nl0).
+// Output for the band kernel: main-grid statuses known 0 / close 1 + list slot / far -1 and the
+// close cells in L0 (count in BandSrc::nl0).
 #include "kernels.h"
 #include "local_ops.h"
 #include "fields.h"
@@ -202,7 +202,7 @@ AF_DEV void xhandover(XHeap& h, const XGrid& s, int isz_s, int isx_s, const XGri
 
 AF_DEV void xclear(double* T, int* S, int n) {
   for (int k = threadIdx.x; k < n; k += blockDim.x) {
-    T[k] = 0.0;
+    T[k] = __builtin_nan("");  // far (fields.h: far cells of HBM grids hold NaN)
     S[k] = -1;
   }
 }
@@ -305,7 +305,7 @@ __global__ __launch_bounds__(64) void fmm_exact_kernel(BandParams P) {
       // heap -> band close list (statuses: heap index > 0 -> close 1)
       for (int k = 1; k <= h.ntr && k <= P.capL; k++) {
         const int c = lds.cell[k];
-        B->S[c] = kClose;
+        B->S[c] = k;  // close: 1 + close-list slot
         B->L0[k - 1] = c;
       }
       nl = h.ntr;

@@ -7,18 +7,28 @@ namespace af {
 
 struct BandSrc {
   double* T;      // field (main grid)
-  int* S;         // status
-  int* L0;        // close list (ping)
+  int* S;         // status: far -1, known 0, close 1 + close-list slot
+  int* own;       // claim owner ids (main grid)
+  int* L0;        // close list (ping): cells
   int* L1;        // close list (pong)
+  double* Lt0;    // close list (ping): T of the entry
+  double* Lt1;
   int* A;         // accepted cells of the step
-  int* C;         // candidates of the step
-  double* V;      // candidate values
+  int* C;         // claimed cells of the step
+  int* Cp;        // their close-list slot (-1: far)
+  double* V;      // claimed cells' new values
   double* Ts[2];  // stage grids (mode 1)
   int* Ss[2];
   long long steps[4];
   long long nupd;  // relax evaluations (cell-sweeps) in the main run
   int err;
-  int nl0;  // close cells handed to the band kernel in L0 (mode 1: fmm_exact_kernel)
+  int nl0;
+  // band profile (BandParams::prof): wall-clock ticks (100 MHz) per phase [tmin, accept, claim,
+  // evaluate, fallback, commit] and list-size sums [close, accepted, evaluated] and max close
+  long long ph[6];
+  long long lsum[3];
+  long long lmax;
+  long long sub[4];  // thread 0 inside phases: claim [neighbour+dedupe, loads, pushes], evaluate loads  // close cells handed to the band kernel in L0 (mode 1: fmm_exact_kernel)
 };
 
 struct BandParams {
@@ -36,6 +46,7 @@ struct BandParams {
   const double* scx;
   const double* scz;
   double gox, goz;
+  int prof;  // record BandSrc::ph / lsum (thread 0 reads the wall clock after each barrier)
 };
 
 struct RayJob {

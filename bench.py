@@ -56,6 +56,7 @@ def main():
         dist.init_process_group("gloo", rank=rank, world_size=world)
 
     import _alifmm
+    import sharding
     import workloads as W
 
     n = args.n
@@ -68,10 +69,7 @@ def main():
     if args.exact_r is not None:
         ctx.set_option("exact_r", args.exact_r)
     ctx.set_model(veln, velpn, vel_map, stif, vt, vt, dnx)
-    # rank r: x = 16 + 32k + 4 (r mod 8), z = 0  (rank 0 = exactly BASELINE C4's sources)
-    k = np.arange(args.sources) % (n // 32)
-    scx = dnx * (16 + 32 * k + 4 * (rank % 8)).astype(np.float64)
-    scz = np.zeros(args.sources)
+    scx, scz = sharding.bench_sources(rank, args.sources, n, dnx)
 
     def barrier():
         if dist is not None:
@@ -91,12 +89,7 @@ def main():
     dt = time.perf_counter() - t0
     sweeps = sum(ctx.source_stats(i)[1] for i in range(args.sources))
     steps_main = [int(ctx.source_stats(i)[0][3]) for i in range(args.sources)]
-    if dist is not None:
-        import torch
-
-        tt = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
+    dt = sharding.max_over_ranks(dt, dist)
     cells = float(n) * n
     total_src = args.sources * world
     value = cells * total_src * args.steps / dt

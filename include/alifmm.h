@@ -46,7 +46,7 @@ int alifmm_set_model(alifmm_ctx* ctx, int nnz, int nnx, const double* veln, cons
                      const double* vel_map, const int64_t* stif_den, const double* group_tab,
                      const double* phase_tab, int ncol, double dnx, double dnz, double gox, double goz);
 
-/* Tuning: "cdelta" (band width in units of dnx/vmax, default 0.5), "r0" (near-source band
+/* Tuning: "prof" (1: record the band profile, alifmm_band_profile), "cdelta" (band width in units of dnx/vmax, default 0.5), "r0" (near-source band
  * schedule radius in cells, default 40), "exact_r" (radius in cells of the exact heap-ordered
  * main-loop prefix for subgrid 1, 0..48, default 40), "batch" (sources per launch, default 256). */
 int alifmm_set_option(alifmm_ctx* ctx, const char* name, double value);
@@ -83,6 +83,13 @@ int alifmm_find_rays(alifmm_ctx* ctx, int npairs, const int32_t* field_slot, con
  * and main-grid cell-sweeps (local-operator evaluations); device time of the last call's kernels. */
 int alifmm_source_stats(alifmm_ctx* ctx, int slot, int64_t* steps4, int64_t* cell_sweeps);
 int alifmm_last_timing(alifmm_ctx* ctx, double* init_ms, double* band_ms, double* total_ms);
+
+/* Band-kernel profile of a slot's last alifmm_travel() when option "prof" is 1 (zeros otherwise):
+ * out14[0..5] wall-clock ticks (100 MHz) spent by the workgroup in the step phases [Tmin, accept,
+ * claim, evaluate, fallback, commit]; out14[6..8] sums over steps of the close / accepted /
+ * evaluated list sizes; out14[9] the largest close set; out14[10..13] thread 0's ticks inside
+ * phases: claim [neighbour + dedupe, nsts loads, list pushes], evaluate [neighbourhood loads]. */
+int alifmm_band_profile(alifmm_ctx* ctx, int slot, int64_t* out14);
 
 /* Upload a host travel-time field (fine grid of `subgrid`) into a slot, e.g. for find_ray() on a
  * field computed elsewhere (find_ray's rec_TTF argument, :3105). */
