@@ -547,6 +547,8 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
 int alifmm_travel(alifmm_ctx* ctx, int subgrid, int nsrc, const double* scx, const double* scz, int first_slot,
                   double* out) {
   if (!ctx || !ctx->have_model) return fail(ctx, ALIFMM_E_ARG, "travel: no model");
+  if ((long)subgrid * (ctx->nz0 - 1) + 1 >= 32768 || (long)subgrid * (ctx->nx0 - 1) + 1 >= 32768)
+    return fail(ctx, ALIFMM_E_ARG, "travel: field sides must stay below 32768 nodes (packed list keys)");
   if (subgrid < 1 || subgrid % 2 == 0) return fail(ctx, ALIFMM_E_ARG, "travel: subgrid must be odd, got %d", subgrid);
   if (nsrc < 0 || first_slot < 0 || (nsrc > 0 && (!scx || !scz))) return fail(ctx, ALIFMM_E_ARG, "travel: bad args");
   HIPCHK(hipSetDevice(ctx->device));

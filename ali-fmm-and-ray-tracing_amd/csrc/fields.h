@@ -121,6 +121,30 @@ struct NbFieldT {
     t0 = t[0]; t1 = t[1]; t2 = t[2]; t3 = t[3]; t4 = t[4]; t5 = t[5];
     t6 = t[6]; t7 = t[7]; t8 = t[8]; t9 = t[9]; t10 = t[10]; t11 = t[11];
   }
+  // From a status-coded grid in LDS (the init kernel's stage grids / prefix window): validity =
+  // inside rows [z0, z1] and columns [x0, x1] (else never-relaxed: nsts -1) and status >= 0;
+  // the 24 LDS reads are issued together instead of as update()'s chain of dependent reads.
+  AF_DEV void load_lds(const double* T, const short* S, int z0, int x0, int z1, int x1, int w, int z, int x) {
+    iz = z;
+    ix = x;
+    const int dz[12] = {0, 0, 0, 0, -2, -1, 1, 2, -1, -1, 1, 1};
+    const int dx[12] = {-2, -1, 1, 2, 0, 0, 0, 0, -1, 1, -1, 1};
+    double t[12];
+    unsigned m = 0;
+#pragma unroll
+    for (int k = 0; k < 12; k++) {
+      const int zz = z + dz[k], xx = x + dx[k];
+      const bool in = zz >= z0 && zz <= z1 && xx >= x0 && xx <= x1;
+      const int c = in ? (zz - z0) * w + (xx - x0) : 0;
+      t[k] = T[c];
+      const int s = S[c];
+      if (in && s >= 0) m |= 1u << k;
+      if (!in) t[k] = 0.0;
+    }
+    vm = m;
+    t0 = t[0]; t1 = t[1]; t2 = t[2]; t3 = t[3]; t4 = t[4]; t5 = t[5];
+    t6 = t[6]; t7 = t[7]; t8 = t[8]; t9 = t[9]; t10 = t[10]; t11 = t[11];
+  }
 };
 
 }  // namespace af

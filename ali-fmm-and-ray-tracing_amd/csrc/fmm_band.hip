@@ -102,11 +102,31 @@ AF_DEV double wave_min(double v) {
   return v;
 }
 
+// Lists hold cells as packed (z << 16 | x) keys (grids are < 32768 per side): no integer
+// divisions on the hot path; the flat index z * nx + x is formed where memory is addressed.
+AF_DEV int pk(int z, int x) { return (z << 16) | x; }
+AF_DEV int pkz(int k) { return k >> 16; }
+AF_DEV int pkx(int k) { return k & 0xffff; }
+AF_DEV int pk_flat(int k, int nx) { return pkz(k) * nx + pkx(k); }
+
+// neighbour d (0 -x, 1 +x, 2 -z, 3 +z) of packed cell c, or -1 outside the grid
 AF_DEV int nb_cell(int c, int d, int nz, int nx) {
-  const int iz = c / nx, ix = c - iz * nx;
-  const int z = iz + (d == 2 ? -1 : d == 3 ? 1 : 0);
-  const int x = ix + (d == 0 ? -1 : d == 1 ? 1 : 0);
-  return (z < 0 || z >= nz || x < 0 || x >= nx) ? -1 : z * nx + x;
+  const int z = pkz(c) + (d == 2 ? -1 : d == 3 ? 1 : 0);
+  const int x = pkx(c) + (d == 0 ? -1 : d == 1 ? 1 : 0);
+  return (z < 0 || z >= nz || x < 0 || x >= nx) ? -1 : pk(z, x);
+}
+
+// exclusive prefix sum over the wave's lanes, and the wave total
+AF_DEV int wave_excl_scan(int v, int& total) {
+  const int lane = threadIdx.x & 63;
+  int inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(inc, o);
+    if (lane >= o) inc += t;
+  }
+  total = __shfl(inc, 63);
+  return inc - v;
 }
 
 struct RunCfg {
@@ -210,7 +230,7 @@ AF_DEV long long band_run(const BandParams& P, BandLds* sh, BandSrc* B, const Ru
       if (sa >= 0) {
         const int c = L.get(e);
         AL.put(sa, c);
-        gst(S + c, (int)kKnown);
+        gst(S + pk_flat(c, nx), (int)kKnown);
         Lt.put(e, INFINITY);
       }
       const int sf = wave_push(&sh->nF, acc, P.capL, &sh->err);
@@ -250,17 +270,30 @@ AF_DEV long long band_run(const BandParams& P, BandLds* sh, BandSrc* B, const Ru
       AF_SUB(0)
 #pragma unroll
       for (int u = 0; u < 8; u++) {
-        s[u] = r[u] >= 0 ? gld(S + r[u]) : (int)kKnown;
-        o[u] = (!use_hash && r[u] >= 0) ? gatomic_max(own + r[u], stamp) : -1;
+        const int f = r[u] >= 0 ? pk_flat(r[u], nx) : 0;
+        s[u] = r[u] >= 0 ? gld(S + f) : (int)kKnown;
+        o[u] = (!use_hash && r[u] >= 0) ? gatomic_max(own + f, stamp) : -1;
       }
       AF_SUB(1)
+      // one list allocation per wave for all 8 items
+      int nw = 0;
+#pragma unroll
+      for (int u = 0; u < 8; u++) nw += (s[u] != kKnown && o[u] < stamp) ? 1 : 0;
+      int tot;
+      const int off = wave_excl_scan(nw, tot);
+      int base = 0;
+      if (lane == 0 && tot) base = atomicAdd(&sh->nE, tot);
+      base = __shfl(base, 0) + off;
 #pragma unroll
       for (int u = 0; u < 8; u++) {
-        const bool won = s[u] != kKnown && o[u] < stamp;
-        const int se = wave_push(&sh->nE, won, P.capC, &sh->err);
-        if (se >= 0) {
-          EL.put(se, r[u]);
-          EP.put(se, s[u] > 0 ? s[u] - 1 : -1);
+        if (s[u] != kKnown && o[u] < stamp) {
+          if (base < P.capC) {
+            EL.put(base, r[u]);
+            EP.put(base, s[u] > 0 ? s[u] - 1 : -1);
+          } else {
+            sh->err = 2;
+          }
+          base++;
         }
       }
       AF_SUB(2)
@@ -275,7 +308,7 @@ AF_DEV long long band_run(const BandParams& P, BandLds* sh, BandSrc* B, const Ru
       const int e1 = e0 + kThreads;
       const bool has1 = e1 < nE;
       const int r0 = EL.get(e0), r1 = has1 ? EL.get(e1) : r0;
-      const int z0 = r0 / nx, x0 = r0 - z0 * nx, z1 = r1 / nx, x1 = r1 - z1 * nx;
+      const int z0 = pkz(r0), x0 = pkx(r0), z1 = pkz(r1), x1 = pkx(r1);
       const CellMat m0 = band_mat<LDSMAT>(M, sh, R.mv, z0, x0);
       const CellMat m1 = band_mat<LDSMAT>(M, sh, R.mv, z1, x1);
       NbFieldT n0, n1;
@@ -288,7 +321,7 @@ AF_DEV long long band_run(const BandParams& P, BandLds* sh, BandSrc* B, const Ru
 #else
     for (int e = tid; e < nE; e += kThreads) {
       const int r = EL.get(e);
-      const int z = r / nx, x = r - z * nx;
+      const int z = pkz(r), x = pkx(r);
       if (prof) ts = wall_clock64();
       const CellMat cm = band_mat<LDSMAT>(M, sh, R.mv, z, x);
       NbFieldT nb;
@@ -304,7 +337,7 @@ AF_DEV long long band_run(const BandParams& P, BandLds* sh, BandSrc* B, const Ru
     for (int e = tid; e < nE; e += kThreads) {
       if (VL.get(e) == -1.0) {
         const int r = EL.get(e);
-        const int z = r / nx, x = r - z * nx;
+        const int z = pkz(r), x = pkx(r);
         const CellMat cm = band_mat<LDSMAT>(M, sh, R.mv, z, x);
         VL.put(e, fouds18_global(F, M, cm, z, x, R.dnx, R.dnz, nx, nz));
       }
@@ -322,7 +355,7 @@ AF_DEV long long band_run(const BandParams& P, BandLds* sh, BandSrc* B, const Ru
         r = EL.get(e);
         v = VL.get(e);
         const int p = EP.get(e);
-        gst(T + r, v);
+        gst(T + pk_flat(r, nx), v);
         if (p >= 0) Lt.put(p, v);
         else fresh = true;
       }
@@ -334,7 +367,7 @@ AF_DEV long long band_run(const BandParams& P, BandLds* sh, BandSrc* B, const Ru
         } else {
           L.put(slot, r);
           Lt.put(slot, v);
-          gst(S + r, 1 + slot);
+          gst(S + pk_flat(r, nx), 1 + slot);
         }
       }
     }
@@ -408,7 +441,7 @@ __global__ __launch_bounds__(kThreads) void fmm_band_kernel(BandParams P) {
       }
       const int s = wave_push(&sh.hi, push, P.capL, &sh.err);
       if (s >= 0) {
-        L0.put(s, c);
+        L0.put(s, pk(c / P.nx, c % P.nx));
         Lt0.put(s, t);
         gst(B->S + c, 1 + s);
       }
@@ -421,7 +454,7 @@ __global__ __launch_bounds__(kThreads) void fmm_band_kernel(BandParams P) {
     }
     for (int k = tid; k < B->nl0; k += kThreads) {
       const int c = gld(B->L0 + k);
-      if (k < kLcap) sh.Ll[k] = c;
+      L0.put(k, pk(c / P.nx, c % P.nx));  // (in place: entry k of L0 is read before it is rewritten)
       Lt0.put(k, gld(B->T + c));
     }
   }

@@ -11,19 +11,23 @@
 #include "device_common.h"
 #include "local_ops.h"
 #include "kernels.h"
+#include "fields.h"
 
 namespace af {
 
 constexpr int kInitMaxN = 109 * 109;  // largest stage grid (stage 1 / 2)
-constexpr int kInitHeap = 8192;       // heap slots (reference sizes them 0.5 * cells)
+constexpr int kInitHeap = 2048;       // heap slots (the stage fronts stay below ~500 nodes)
+constexpr int kInitMat = 256;         // material records staged in LDS (DevModel::mtab)
 constexpr int kInitDec = 37 * 37;     // decimated stage-1/2 grid
 
 struct InitLds {
   double T[kInitMaxN];
   double decT[kInitDec];
   short S[kInitMaxN];
-  unsigned short btg[kInitHeap];  // (z << 8) | x
-  signed char decC[kInitDec];     // 0 far, 1 known inner, 2 known outer, 3 close
+  double hkey[kInitHeap];          // heap keys: ttn of the node (kept equal to it by add/upd)
+  MatRec mat[kInitMat];
+  unsigned short hcell[kInitHeap];  // heap nodes (z << 8) | x
+  signed char decC[kInitDec];       // 0 far, 1 known inner, 2 known outer, 3 close
 };
 
 struct LdsField {
@@ -34,61 +38,62 @@ struct LdsField {
   AF_DEV double tt(long z, long x) const { return z >= nz ? 0.0 : T[z * nx + x]; }
 };
 
+// addtree / updtree / downtree (:94-237).  Keys are stored in the heap next to the node (a copy
+// of its ttn, refreshed by every add/upd), so a sift level is one LDS read instead of two
+// dependent ones; comparisons are exactly the reference's.
 struct Heap {
   InitLds* L;
   int nz, nx;
   int ntr;
   int err;
-  AF_DEV int bz(int k) const { return L->btg[k] >> 8; }
-  AF_DEV int bx(int k) const { return L->btg[k] & 255; }
-  AF_DEV double tb(int k) const { return L->T[bz(k) * nx + bx(k)]; }
+  AF_DEV int bz(int k) const { return L->hcell[k] >> 8; }
+  AF_DEV int bx(int k) const { return L->hcell[k] & 255; }
+  AF_DEV double tb(int k) const { return L->hkey[k]; }
   AF_DEV static int parent(int t) { return (int)rint((double)t / 2.0); }  // half-even (:123)
   AF_DEV void swap(int a, int b) {
-    unsigned short e = L->btg[a];
-    L->btg[a] = L->btg[b];
-    L->btg[b] = e;
+    unsigned short e = L->hcell[a];
+    L->hcell[a] = L->hcell[b];
+    L->hcell[b] = e;
+    double k = L->hkey[a];
+    L->hkey[a] = L->hkey[b];
+    L->hkey[b] = k;
+  }
+  AF_DEV void sift_up(int iz, int ix, int tpc) {
+    int tpp = parent(tpc);
+    const double tv = L->hkey[tpc];
+    while (tpp > 0) {
+      if (tv < tb(tpp)) {
+        L->S[iz * nx + ix] = (short)tpp;
+        L->S[bz(tpp) * nx + bx(tpp)] = (short)tpc;
+        swap(tpc, tpp);
+        tpc = tpp;
+        tpp = parent(tpc);
+      } else {
+        tpp = 0;
+      }
+    }
   }
   // addtree :94-138
   AF_DEV void add(int iz, int ix) {
     ntr += 1;
     if (ntr >= kInitHeap) { err = 1; ntr = kInitHeap - 1; return; }
     L->S[iz * nx + ix] = (short)ntr;
-    L->btg[ntr] = (unsigned short)((iz << 8) | ix);
-    int tpc = ntr, tpp = parent(tpc);
-    double tv = L->T[iz * nx + ix];
-    while (tpp > 0) {
-      if (tv < tb(tpp)) {
-        L->S[iz * nx + ix] = (short)tpp;
-        L->S[bz(tpp) * nx + bx(tpp)] = (short)tpc;
-        swap(tpc, tpp);
-        tpc = tpp;
-        tpp = parent(tpc);
-      } else {
-        tpp = 0;
-      }
-    }
+    L->hcell[ntr] = (unsigned short)((iz << 8) | ix);
+    L->hkey[ntr] = L->T[iz * nx + ix];
+    sift_up(iz, ix, ntr);
   }
   // updtree :141-175
   AF_DEV void upd(int iz, int ix) {
-    int tpc = L->S[iz * nx + ix], tpp = parent(tpc);
-    double tv = L->T[iz * nx + ix];
-    while (tpp > 0) {
-      if (tv < tb(tpp)) {
-        L->S[iz * nx + ix] = (short)tpp;
-        L->S[bz(tpp) * nx + bx(tpp)] = (short)tpc;
-        swap(tpc, tpp);
-        tpc = tpp;
-        tpp = parent(tpc);
-      } else {
-        tpp = 0;
-      }
-    }
+    const int tpc = L->S[iz * nx + ix];
+    L->hkey[tpc] = L->T[iz * nx + ix];
+    sift_up(iz, ix, tpc);
   }
   // downtree :178-237
   AF_DEV void down() {
     if (ntr == 1) { ntr -= 1; return; }
     L->S[bz(ntr) * nx + bx(ntr)] = 1;
-    L->btg[1] = L->btg[ntr];
+    L->hcell[1] = L->hcell[ntr];
+    L->hkey[1] = L->hkey[ntr];
     ntr -= 1;
     int tpp = 1, tpc = 2;
     while (tpc < ntr) {
@@ -113,6 +118,19 @@ struct Heap {
   }
 };
 
+// material of a node: one id load + the LDS record (LDSMAT), else the model arrays
+template <bool LDSMAT>
+AF_DEV CellMat init_mat(const DevModel& M, const InitLds* L, const MatView& v, int z, int x) {
+  if (!LDSMAT) return cell_mat(M, v, z, x);
+  const MatRec m = L->mat[gld(M.mid + mv_cell(M, v, z, x))];
+  CellMat r;
+  r.velpn = m.velpn;
+  r.veln = v.quant ? (double)(int)m.veln : m.veln;
+  r.vm = v.quant ? (double)(float)m.vm : m.vm;
+  r.stif = m.sidx >= 0 ? M.stab + 5 * m.sidx : nullptr;
+  return r;
+}
+
 struct StageCfg {
   double dnx;
   int isx, isz, max_dist, quirk;
@@ -120,15 +138,21 @@ struct StageCfg {
 };
 
 // relax one neighbour: update() then fouds18_A() (:1635-1638)
-AF_DEV void relax(InitLds* L, const DevModel& M, const StageCfg& c, int nz, int nx, int iz, int ix, int quirk) {
+AF_DEV void relax(InitLds* L, const DevModel& M, const StageCfg& c, int nz, int nx, int iz, int ix, int quirk,
+                  const CellMat& cm) {
   LdsField F{L->T, L->S, nz, nx};
-  CellMat cm = cell_mat(M, c.mv, iz, ix);
-  double v = update(F, M, cm, iz, ix, c.dnx, quirk ? nx : nz, nx);
+  // register copy of the neighbourhood; rows past nz read as nsts -1 (the padded reads of the
+  // stage-1 quirk nnz = nnx1, :1645); update() bounds-checks every other position itself
+  NbFieldT nb;
+  nb.load_lds(L->T, L->S, 0, 0, nz - 1, nx - 1, nx, iz, ix);
+  double v = update(nb, M, cm, iz, ix, c.dnx, quirk ? nx : nz, nx);
   if (v == -1.0) v = fouds18(F, M, cm, iz, ix, c.dnx, c.dnx, nx, nz);
   L->T[iz * nx + ix] = v;
 }
 
-// stage FMM loop (:1620-1674)
+// stage FMM loop (:1620-1674).  The four neighbours' materials are fetched together at each
+// pop (they do not depend on the heap), then relaxed in the reference's order.
+template <bool LDSMAT>
 AF_DEV void stage_loop(Heap& h, const DevModel& M, const StageCfg& c) {
   InitLds* L = h.L;
   const int nz = h.nz, nx = h.nx;
@@ -137,15 +161,21 @@ AF_DEV void stage_loop(Heap& h, const DevModel& M, const StageCfg& c) {
     int ix = h.bx(1), iz = h.bz(1);
     L->S[iz * nx + ix] = 0;
     h.down();
+    CellMat cm[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int z = k < 2 ? iz : iz + (k == 2 ? -1 : 1), x = k < 2 ? ix + (k == 0 ? -1 : 1) : ix;
+      if (0 <= z && z <= nz - 1 && 0 <= x && x <= nx - 1) cm[k] = init_mat<LDSMAT>(M, L, c.mv, z, x);
+    }
     for (int s = 0; s < 2; s++) {
       int i = s == 0 ? ix - 1 : ix + 1;
       if (0 <= i && i <= nx - 1) {
         int st = L->S[iz * nx + i];
         if (st == -1) {
-          relax(L, M, c, nz, nx, iz, i, 0);
+          relax(L, M, c, nz, nx, iz, i, 0, cm[s]);
           h.add(iz, i);
         } else if (st > 0) {
-          relax(L, M, c, nz, nx, iz, i, c.quirk);
+          relax(L, M, c, nz, nx, iz, i, c.quirk, cm[s]);
           h.upd(iz, i);
         }
       } else if (abs(c.isx - i) == c.max_dist + 1) {
@@ -157,10 +187,10 @@ AF_DEV void stage_loop(Heap& h, const DevModel& M, const StageCfg& c) {
       if (0 <= i && i <= nz - 1) {
         int st = L->S[i * nx + ix];
         if (st == -1) {
-          relax(L, M, c, nz, nx, i, ix, 0);
+          relax(L, M, c, nz, nx, i, ix, 0, cm[2 + s]);
           h.add(i, ix);
         } else if (st > 0) {
-          relax(L, M, c, nz, nx, i, ix, 0);
+          relax(L, M, c, nz, nx, i, ix, 0, cm[2 + s]);
           h.upd(i, ix);
         }
       } else if (abs(c.isz - i) == c.max_dist + 1) {
@@ -215,15 +245,17 @@ struct WinField {
 };
 
 // main loop :2055-2102 on the LDS window (heap in window-local coordinates)
+template <bool LDSMAT>
 AF_DEV void main_prefix(Heap& h, const DevModel& M, const InitJob& J, int wz0, int wx0, int wz1, int wx1) {
   InitLds* L = h.L;
   const int ww = h.nx;
   const int nnz = M.nz0, nnx = M.nx0;
   const MatView ident{1, 0, 0, 1, 0, 0, 1, 0, 0, 0, 0};
   const WinField F{L->T, L->S, wz0, wx0, wz1, wx1, ww};
-  auto relax_main = [&](int iz, int ix) {
-    CellMat cm = cell_mat(M, ident, iz, ix);
-    double v = update(F, M, cm, iz, ix, J.dnx, nnz, nnx);
+  auto relax_main = [&](int iz, int ix, const CellMat& cm) {
+    NbFieldT nb;
+    nb.load_lds(L->T, L->S, wz0, wx0, wz1, wx1, ww, iz, ix);
+    double v = update(nb, M, cm, iz, ix, J.dnx, nnz, nnx);
     if (v == -1.0) v = fouds18(F, M, cm, iz, ix, J.dnx, J.dnz, nnx, nnz);
     L->T[(iz - wz0) * ww + (ix - wx0)] = v;
   };
@@ -236,16 +268,22 @@ AF_DEV void main_prefix(Heap& h, const DevModel& M, const InitJob& J, int wz0, i
       break;
     L->S[lz * ww + lx] = 0;
     h.down();
+    CellMat cm[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int z = k < 2 ? iz : iz + (k == 2 ? -1 : 1), x = k < 2 ? ix + (k == 0 ? -1 : 1) : ix;
+      if (0 <= z && z <= nnz - 1 && 0 <= x && x <= nnx - 1) cm[k] = init_mat<LDSMAT>(M, L, ident, z, x);
+    }
     for (int s = 0; s < 2; s++) {
       int i = s == 0 ? ix - 1 : ix + 1;
       if (0 <= i && i <= nnx - 1) {
         int li = i - wx0;
         int st = L->S[lz * ww + li];
         if (st == -1) {
-          relax_main(iz, i);
+          relax_main(iz, i, cm[s]);
           h.add(lz, li);
         } else if (st > 0) {
-          relax_main(iz, i);
+          relax_main(iz, i, cm[s]);
           h.upd(lz, li);
         }
       }
@@ -256,10 +294,10 @@ AF_DEV void main_prefix(Heap& h, const DevModel& M, const InitJob& J, int wz0, i
         int li = i - wz0;
         int st = L->S[li * ww + lx];
         if (st == -1) {
-          relax_main(i, ix);
+          relax_main(i, ix, cm[2 + s]);
           h.add(li, lx);
         } else if (st > 0) {
-          relax_main(i, ix);
+          relax_main(i, ix, cm[2 + s]);
           h.upd(li, lx);
         }
       }
@@ -267,10 +305,13 @@ AF_DEV void main_prefix(Heap& h, const DevModel& M, const InitJob& J, int wz0, i
   }
 }
 
+template <bool LDSMAT>
 __global__ __launch_bounds__(64) void fmm_init_kernel(DevModel M, InitJob* jobs, int njobs, HandoverOut* out) {
   __shared__ InitLds lds;
   InitLds* L = &lds;
   const int src = blockIdx.x;
+  if (LDSMAT)
+    for (int k = threadIdx.x; k < M.nmat; k += blockDim.x) L->mat[k] = M.mtab[k];
   if (src >= njobs) return;
   const int lane = threadIdx.x, nl = blockDim.x;
   InitJob J = jobs[src];
@@ -342,7 +383,7 @@ __global__ __launch_bounds__(64) void fmm_init_kernel(DevModel M, InitJob* jobs,
       }
     }
     if (lane == 0) {
-      stage_loop(h, M, c);
+      stage_loop<LDSMAT>(h, M, c);
       err |= h.err;
     }
     __syncthreads();
@@ -379,7 +420,7 @@ __global__ __launch_bounds__(64) void fmm_init_kernel(DevModel M, InitJob* jobs,
           if (cls == 1 || cls == 2) L->S[pz * ww + px] = 0;
           if (cls >= 2) h.add(pz, px);
         }
-        main_prefix(h, M, J, wz0, wx0, wz1, wx1);
+        main_prefix<LDSMAT>(h, M, J, wz0, wx0, wz1, wx1);
         err |= h.err;
       }
       __syncthreads();
@@ -424,6 +465,9 @@ __global__ __launch_bounds__(64) void fmm_init_kernel(DevModel M, InitJob* jobs,
 
 extern "C" hipError_t af_launch_init(const af::DevModel* M, af::InitJob* jobs, int njobs, af::HandoverOut* out,
                                      hipStream_t stream) {
-  hipLaunchKernelGGL(af::fmm_init_kernel, dim3(njobs), dim3(64), 0, stream, *M, jobs, njobs, out);
+  if (M->mid && M->nmat <= af::kInitMat)
+    hipLaunchKernelGGL(af::fmm_init_kernel<true>, dim3(njobs), dim3(64), 0, stream, *M, jobs, njobs, out);
+  else
+    hipLaunchKernelGGL(af::fmm_init_kernel<false>, dim3(njobs), dim3(64), 0, stream, *M, jobs, njobs, out);
   return hipGetLastError();
 }

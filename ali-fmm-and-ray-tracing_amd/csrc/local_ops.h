@@ -36,6 +36,7 @@ AF_DEV double fouds18(const F& f, const DevModel& M, const CellMat& cm, long iz,
         else slo3 = g;
     }
     double slown = slo0;
+    #pragma unroll 1
     for (int jj_ = 0; jj_ < 2; jj_++) {
         long j = jj_ == 0 ? ix - 1 : ix + 1;
         if (0 <= j && j <= nnx - 1) {
@@ -54,6 +55,7 @@ AF_DEV double fouds18(const F& f, const DevModel& M, const CellMat& cm, long iz,
             } else {
                 swj = -1;
             }
+            #pragma unroll 1
             for (int kk_ = 0; kk_ < 2; kk_++) {
                 long k = kk_ == 0 ? iz - 1 : iz + 1;
                 if (0 <= k && k <= nnz - 1) {
@@ -153,6 +155,7 @@ AF_DEV double fouds18(const F& f, const DevModel& M, const CellMat& cm, long iz,
     double travmd = 0;
     slown = slo1;
     double mf2 = sqrt(2.0);
+    #pragma unroll 1
     for (int jj_ = 0; jj_ < 2; jj_++) {
         long j = (jj_ == 0) ? ix - 1 : ix + 1;
         long k = (j == ix - 1) ? iz + 1 : iz - 1;
@@ -172,6 +175,7 @@ AF_DEV double fouds18(const F& f, const DevModel& M, const CellMat& cm, long iz,
             } else {
                 swdiag = -1;
             }
+            #pragma unroll 1
             for (int q_ = 0; q_ < 2; q_++) {
                 long jj = (q_ == 0) ? ix - 1 : ix + 1;
                 long kk = (jj == ix - 1) ? iz - 1 : iz + 1;
@@ -276,6 +280,7 @@ AF_DEV double fouds18(const F& f, const DevModel& M, const CellMat& cm, long iz,
 
     /* ---- atan(1/2) stencils (:698-897) ---- */
     double travmt = 0, travms = 0;
+    #pragma unroll 1
     for (int pass = 0; pass < 2; pass++) {
         slown = pass == 0 ? slo2 : slo3;
         double m5 = sqrt(5.0);
@@ -286,6 +291,7 @@ AF_DEV double fouds18(const F& f, const DevModel& M, const CellMat& cm, long iz,
                                : ((l) % 4 == 0 ? -2 : (l) == 1 ? 1 : (l) == 2 ? 2 : -1)))
         int tsw = 0;
         double tm = 0;
+        #pragma unroll 1
         for (int lp = 0; lp < 4; lp++) {
             long j = JV(lp), k = KV(lp), jj = JV(lp + 1), kk = KV(lp + 1);
             if (0 <= j && j <= nnx - 1 && 0 <= k && k <= nnz - 1 && 0 <= jj && jj <= nnx - 1 && 0 <= kk &&
