@@ -1,11 +1,13 @@
 // rays.hip — plane-search ray back-trace find_ray (Anis_TTF_rays.py:3104-3465) on gfx950.
 //
-// One 64-lane wavefront per ray.  Each step is wave-uniform except the candidate evaluation:
-// lane i evaluates candidate i of the plane (6*sg+3 candidates on axis planes, <= 5*sg+3 on
-// diagonal planes), i.e. rec_TTF at the candidate plus the straight-segment time
+// One group of G lanes per ray (G = 16, 32 or 64: the smallest power of two >= the 6*sg+3
+// candidates of an axis plane, so subgrid 1 packs 4 rays into a wavefront; G = 64 loops over the
+// candidates when there are more).  Each step is uniform within the group except the candidate
+// evaluation: lane i evaluates candidate i of the plane (6*sg+3 candidates on axis planes,
+// <= 5*sg+3 on diagonal planes), i.e. rec_TTF at the candidate plus the straight-segment time
 // time_between_points (:2835-2989, a DDA over coarse cells).  The parabolic local-minimum search
-// (:3192-3218) is a lexicographic (value, order) wave reduction, which selects exactly the
-// candidate the reference's sequential strict-'<' scan selects.  ray_time (:2992-3022) is
+// (:3192-3218) is a lexicographic (value, order) reduction over the group's lanes, which selects
+// exactly the candidate the reference's sequential strict-'<' scan selects.  ray_time (:2992-3022) is
 // accumulated segment by segment as the ray grows, i.e. in the reference's summation order, so
 // times match the CPU to the last bit
 // except where ocml's atan/tan/sin/cos differ from glibc.  All arithmetic is double precision.
@@ -25,10 +27,13 @@ struct Key {
 };
 AF_DEV bool key_less(const Key& a, const Key& b) { return a.v < b.v || (a.v == b.v && a.order < b.order); }
 
+template <int G>
 __global__ __launch_bounds__(64 * kRayWaves) void find_ray_kernel(RayParams P) {
+  constexpr int kGroups = 64 / G;             // rays per wavefront
+  constexpr int kTT = kMaxCand / kGroups;      // candidate slots per ray
   __shared__ double TTs[kRayWaves][kMaxCand];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int ray = blockIdx.x * kRayWaves + w;
+  const int lane = threadIdx.x & (G - 1), w = threadIdx.x >> 6, grp = (threadIdx.x & 63) / G;
+  const int ray = (blockIdx.x * kRayWaves + w) * kGroups + grp;
   if (ray >= P.nrays) return;
   const RayJob J = P.jobs[ray];
   const int sg = P.sg;
@@ -36,7 +41,7 @@ __global__ __launch_bounds__(64 * kRayWaves) void find_ray_kernel(RayParams P) {
   const long nnx = P.fnz, nnz = P.fnx;  // reference naming (:3151-3152)
   double* rxo = P.ray_x + (long)ray * P.max_pts;
   double* ryo = P.ray_y + (long)ray * P.max_pts;
-  double* TT = TTs[w];
+  double* TT = &TTs[w][grp * kTT];
   long cap = 5L * (P.M.nz0 + P.M.nx0);
   if (cap > P.max_pts) cap = P.max_pts;
   const double recx = J.rx, recy = J.ry;
@@ -49,7 +54,7 @@ __global__ __launch_bounds__(64 * kRayWaves) void find_ray_kernel(RayParams P) {
     rxo[0] = J.sx;
     ryo[0] = J.sy;
   }
-#define RT(r, c) J.ttf[(long)(r) * P.fnx + (long)(c)]
+#define RT(r, c) gld(J.ttf + (long)(r) * P.fnx + (long)(c))
   while ((last_x - recx) * (last_x - recx) + (last_y - recy) * (last_y - recy) > (1.6 * sg) * (1.6 * sg)) {
     if ((last_x - recx) * (last_x - recx) + (last_y - recy) * (last_y - recy) < (double)(4 * sg) * (4 * sg)) {
       lvx = recx - last_x;
@@ -108,12 +113,12 @@ __global__ __launch_bounds__(64 * kRayWaves) void find_ray_kernel(RayParams P) {
       n = mx - mn + 1;
     }
     if (stop) break;
-    if (n <= 0 || n > kMaxCand) {
+    if (n <= 0 || n > kTT) {
       flags |= 4;
       break;
     }
     // candidates across lanes
-    for (long i0 = 0; i0 < n; i0 += 64) {
+    for (long i0 = 0; i0 < n; i0 += G) {
       long i = i0 + lane;
       if (i < n) {
         double t;
@@ -139,7 +144,7 @@ __global__ __launch_bounds__(64 * kRayWaves) void find_ray_kernel(RayParams P) {
     Key best;
     if (TT[0] < TT[n - 1]) best = Key{TT[0], 0, 0.0};
     else best = Key{TT[n - 1], 0, (double)(n - 1)};
-    for (long j0 = 1; j0 < n - 1; j0 += 64) {
+    for (long j0 = 1; j0 < n - 1; j0 += G) {
       long j = j0 + lane;
       if (j < n - 1) {
         double t1 = TT[j - 1], t2 = TT[j], t3 = TT[j + 1];
@@ -161,7 +166,7 @@ __global__ __launch_bounds__(64 * kRayWaves) void find_ray_kernel(RayParams P) {
         }
       }
     }
-    for (int o = 32; o > 0; o >>= 1) {
+    for (int o = G / 2; o > 0; o >>= 1) {  // stays inside the aligned group of G lanes
       Key other{__shfl_xor(best.v, o), __shfl_xor(best.order, o), __shfl_xor(best.pos, o)};
       if (key_less(other, best)) best = other;
     }
@@ -234,7 +239,12 @@ extern "C" hipError_t af_launch_pack_rays(const double* rx, const double* ry, co
 }
 
 extern "C" hipError_t af_launch_rays(const af::RayParams* P, hipStream_t stream) {
-  int blocks = (P->nrays + af::kRayWaves - 1) / af::kRayWaves;
-  hipLaunchKernelGGL(af::find_ray_kernel, dim3(blocks), dim3(64 * af::kRayWaves), 0, stream, *P);
+  const int ncand = 6 * P->sg + 3;  // axis planes; diagonal planes have <= 5*sg+3
+  const int G = ncand <= 16 ? 16 : ncand <= 32 ? 32 : 64;
+  const int per_block = af::kRayWaves * (64 / G);
+  const dim3 grid((P->nrays + per_block - 1) / per_block), block(64 * af::kRayWaves);
+  if (G == 16) hipLaunchKernelGGL(af::find_ray_kernel<16>, grid, block, 0, stream, *P);
+  else if (G == 32) hipLaunchKernelGGL(af::find_ray_kernel<32>, grid, block, 0, stream, *P);
+  else hipLaunchKernelGGL(af::find_ray_kernel<64>, grid, block, 0, stream, *P);
   return hipGetLastError();
 }

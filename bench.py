@@ -96,6 +96,20 @@ def main():
     band_avg_s = band_ms / args.steps / 1e3
     achieved = BYTES_PER_SWEEP * sweeps / band_avg_s / 1e9 if band_avg_s > 0 else None
 
+    traffic = traffic_bytes = None  # HBM-side bytes per launch (PMC passes of tools/profile.sh, this library)
+    try:
+        import glob
+        import hashlib
+
+        lib_sha = hashlib.sha256(open(_alifmm.LIB_PATH, "rb").read()).hexdigest()
+        for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json"))):
+            t = json.load(open(f))
+            if t.get("libalifmm_sha256") == lib_sha and t.get("traffic_bytes_per_launch"):
+                traffic_bytes = t["traffic_bytes_per_launch"]
+                traffic = traffic_bytes / band_avg_s / 1e9  # GB/s over the same launch time as achieved
+    except OSError:
+        pass
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and args.cpu_sample > 0:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -130,9 +144,11 @@ def main():
             "kernel_ms_per_step": {"fmm_init_kernel": init_ms / args.steps, "fmm_band_kernel": band_ms / args.steps},
             "band_steps_main_mean": float(np.mean(steps_main)),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
+                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
                          "kernel": "fmm_band_kernel", "bytes_per_cell_sweep": BYTES_PER_SWEEP,
-                         "cell_sweeps_per_launch": int(sweeps)},
+                         "cell_sweeps_per_launch": int(sweeps),
+                         "algorithmic_bytes_per_launch": BYTES_PER_SWEEP * int(sweeps),
+                         "traffic_bytes_per_launch": traffic_bytes},
             "cpu_baseline": cpu,
         }
         if cpu:
