@@ -144,8 +144,13 @@ AF_DEV double christoffel_group(const double* s, double eff, double vm) {
 
 // Christoffel PHASE velocity (update() :1400-1406).
 AF_DEV double christoffel_phase(const double* s, double eff, double vm) {
+#if AF_SINCOS
+  double sa, ca;
+  sincos(eff * kDeg2Rad, &sa, &ca);
+#else
   double ca = cos(eff * kDeg2Rad);
   double sa = sin(eff * kDeg2Rad);
+#endif
   double A = ca * ca * s[0] + sa * sa * s[3];
   double B = ca * sa * (s[1] + s[3]);
   double C = ca * ca * s[3] + sa * sa * s[2];
@@ -159,8 +164,9 @@ AF_DEV double group_vel_cell(const DevModel& M, const CellMat& c, double eff) {
 }
 
 // wavefront_angle_dist :1413-1460
-AF_DEV void wad(long ix, long iz, long x1, long x2, long x3, long z1, long z2, long z3, double y1, double y2,
-                double y3, double& angle, double& dist) {
+template <class I>
+AF_DEV void wad(I ix, I iz, I x1, I x2, I x3, I z1, I z2, I z3, double y1, double y2, double y3, double& angle,
+                double& dist) {
   double a;
   if (y3 != y1) {
     a = (y2 - y1) / (y3 - y1);

@@ -352,9 +352,14 @@ AF_DEV double fouds18(const F& f, const DevModel& M, const CellMat& cm, long iz,
 }
 
 
+// update() index type: grid coordinates fit in int; the long of the reference's numba code
+// only widens the integer arithmetic (the doubles formed from the coordinates are the same)
+#ifndef AF_UPD_IDX
+#define AF_UPD_IDX int
+#endif
 template <class F>
-AF_DEV double update(const F& f, const DevModel& M, const CellMat& cm, long iz, long ix, double dnx, long nnz,
-                     long nnx) {
+AF_DEV double update(const F& f, const DevModel& M, const CellMat& cm, AF_UPD_IDX iz, AF_UPD_IDX ix, double dnx,
+                     AF_UPD_IDX nnz, AF_UPD_IDX nnx) {
 #define N_(z, x) f.st((z), (x))
 #define T_(z, x) f.tt((z), (x))
     int sp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -391,7 +396,7 @@ AF_DEV double update(const F& f, const DevModel& M, const CellMat& cm, long iz, 
        stencil that the reference's last wavefront_angle_dist call would use (same result, one
        inlined instance instead of 32: keeps the kernels free of register spills) */
     bool have_w = false;
-    long wx1 = 0, wx2 = 0, wx3 = 0, wz1 = 0, wz2 = 0, wz3 = 0;
+    AF_UPD_IDX wx1 = 0, wx2 = 0, wx3 = 0, wz1 = 0, wz2 = 0, wz3 = 0;
     double wy1 = 0, wy2 = 0, wy3 = 0;
 #define SETW(a1, a2, a3, b1, b2, b3, c1, c2, c3) \
     do { wx1 = (a1); wx2 = (a2); wx3 = (a3); wz1 = (b1); wz2 = (b2); wz3 = (b3); \

@@ -248,3 +248,28 @@ def test_c4_4096_fields_rays_and_batch_consistency(golden, ctx):
         assert abs(t[i] - ref_t) / ref_t <= RAY_END2END, (x, t[i], ref_t)
         rx = g["ray_x_%d" % x]
         assert abs(len(rays[i][0]) - len(rx)) <= 0.02 * len(rx), (x, len(rays[i][0]), len(rx))
+
+
+def test_weld_example_end_to_end(golden, A):
+    """Weld_rays.py (the reference's example) through the unchanged ALI_FMM surface, minus plots:
+    31 bottom receiver fields at subgrid 9 + 961 top->bottom rays (find_all_TTF_rays_parallel),
+    the trimmed ray arrays the script saves, and rays 0/15/30 -> 46 vs the reference's times."""
+    veln, velpn, vel_map, stif = W.weld_model()
+    velpn = velpn.astype(int)
+    sx, sy = W.weld_transducers()
+    n = len(sx) // 2
+    pairs = np.zeros((2 * n, 2 * n))
+    pairs[:n, n:] = 1
+    M = A.ALI_FMM(veln, velpn, vel_map, sx, sy, stif_den=stif, dnx=0.0002)
+    t = M.find_all_TTF_rays_parallel(veln, velpn, vel_map, stif_den=stif, n_threads=8, trans_pairs=pairs)
+    g = golden("weld_sg9")
+    for i in (0, 15, 30):
+        ref = float(g["time_%d" % i])
+        assert abs(t[i, 46] - ref) / ref <= RAY_END2END, (i, t[i, 46], ref)
+    assert np.all(t[:n, n:] > 0) and np.all(t[n:, :] == 0) and np.all(t[:n, :n] == 0)
+    max_len = int(np.max(M.ray_len))
+    assert 2 < max_len <= M.ray_paths_x.shape[2]
+    k = int(M.ray_len[15, 46])
+    rx, ry = M.ray_path(15, 46)
+    assert len(rx) == k and abs(rx[0] - sx[15] / 0.0002) < 1e-9
+    assert abs(ry[0] - 0) < 1e-12 and abs(ry[-1] - 423) < 1e-12 and abs(rx[-1] - 250) < 1e-12

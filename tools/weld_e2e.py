@@ -1,0 +1,47 @@
+"""The reference's weld example (Weld_rays.py) end to end through the drop-in module, minus the
+plots (GPU box): 62 transducers, 31 bottom receiver fields at subgrid 9 (travel_finer_grid, the
+example's default), 961 top->bottom rays via find_all_TTF_rays_parallel(n_threads=8).
+weld_stif_den.npy is absent from the reference: the notebook's stiffness row is
+used for every cell, as in the golden fixtures.  Prints wall time and the rays 0/15/30 -> 46 vs
+the reference's times (tests/golden/weld_sg9.npz).
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "ali-fmm-and-ray-tracing_amd"))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+import workloads as W  # noqa: E402
+from Anis_TTF_rays import ALI_FMM  # noqa: E402
+
+
+def main():
+    veln, velpn, vel_map, stif_density = W.weld_model()
+    velpn = velpn.astype(int)
+    dnx = 0.0002
+    nnz, nnx = veln.shape
+    source_x1, source_y1 = W.weld_transducers(nnz, nnx, dnx)
+    n_trans = len(source_x1) // 2
+    trans_pairs = np.zeros((2 * n_trans, 2 * n_trans))
+    for i in range(n_trans):
+        for j in range(n_trans, 2 * n_trans):
+            trans_pairs[i, j] = 1
+    t0 = time.perf_counter()
+    model = ALI_FMM(veln, velpn, vel_map, source_x1, source_y1, stif_den=stif_density, dnx=dnx)
+    trav_times = model.find_all_TTF_rays_parallel(veln, velpn, vel_map, stif_den=stif_density, n_threads=8,
+                                                  trans_pairs=trans_pairs)
+    dt = time.perf_counter() - t0
+    max_len = int(np.max(model.ray_len))
+    g = np.load(os.path.join(REPO, "tests", "golden", "weld_sg9.npz"))
+    rel = {i: abs(trav_times[i, 46] - float(g["time_%d" % i])) / float(g["time_%d" % i]) for i in (0, 15, 30)}
+    print(json.dumps({"wall_s": dt, "rays": int(np.sum(trans_pairs)), "receiver_fields": n_trans,
+                      "subgrid": 9, "max_ray_len": max_len, "ray_time_rel_err_vs_reference": rel}))
+
+
+if __name__ == "__main__":
+    main()
