@@ -38,6 +38,7 @@ def _load():
             "alifmm_last_error": (ctypes.c_char_p, [_p]),
             "alifmm_set_model": (_i, [_p, _i, _i, _p, _p, _p, _p, _p, _p, _i, _d, _d, _d, _d]),
             "alifmm_set_option": (_i, [_p, ctypes.c_char_p, _d]),
+            "alifmm_get_option": (_i, [_p, ctypes.c_char_p, _p]),
             "alifmm_field_shape": (_i, [_p, _i, _p, _p]),
             "alifmm_travel": (_i, [_p, _i, _i, _p, _p, _i, _p]),
             "alifmm_get_field": (_i, [_p, _i, _p]),
@@ -121,6 +122,11 @@ class Context:
 
     def set_option(self, name, value):
         self._chk(lib().alifmm_set_option(self._h, name.encode(), float(value)), "set_option(%s)" % name)
+
+    def get_option(self, name):
+        v = ctypes.c_double(0)
+        self._chk(lib().alifmm_get_option(self._h, name.encode(), ctypes.byref(v)), "get_option(%s)" % name)
+        return v.value
 
     def set_model(self, veln, velpn, vel_map, stif_den, group_tab, phase_tab, dnx, dnz=None, gox=0.0, goz=0.0,
                   key=None):

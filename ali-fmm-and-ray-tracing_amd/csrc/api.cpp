@@ -34,6 +34,8 @@ struct Arena {  // per-chunk scratch, reused across calls
   long cells = 0, capL = 0, capC = 0, capS = 0;
   int* S = nullptr;
   int* own = nullptr;
+  int* ax = nullptr;         // pair mode: 2 exchange lists per source
+  af::PairX* px = nullptr;   // pair mode: exchange blocks
   int* lists = nullptr;    // L0 | L1 | A | C | Cp per source
   double* dlists = nullptr;  // Lt0 | Lt1 | V per source
   double* Ts = nullptr;  // stage grids (travel_finer_grid), 2 per source
@@ -72,6 +74,9 @@ struct alifmm_ctx {
   int exact_r = 40;
   int batch = 256;
   int prof = 0;
+  int pair = 1;     // two workgroups per source when the chunk fits the device (fmm_band_pair.hip)
+  int n_cu = 0;
+  int last_pair = 0;
   long cap_scale = 1;
   // state
   std::vector<Field> fields;
@@ -104,7 +109,7 @@ static void dfree(void* p) {
 }
 
 static void free_arena(Arena& a) {
-  dfree(a.S); dfree(a.own); dfree(a.lists); dfree(a.dlists); dfree(a.Ts); dfree(a.Ss); dfree(a.srcs); dfree(a.ho); dfree(a.jobs);
+  dfree(a.S); dfree(a.own); dfree(a.ax); dfree(a.px); dfree(a.lists); dfree(a.dlists); dfree(a.Ts); dfree(a.Ss); dfree(a.srcs); dfree(a.ho); dfree(a.jobs);
   dfree(a.dscx); dfree(a.dscz);
   a = Arena();
 }
@@ -161,6 +166,8 @@ int alifmm_ctx_create(int device, alifmm_ctx** out) {
     return ALIFMM_E_HIP;
   }
   for (auto& e : ctx->ev) (void)hipEventCreate(&e);
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess) ctx->n_cu = prop.multiProcessorCount;
   *out = ctx;
   return ALIFMM_OK;
 }
@@ -205,8 +212,23 @@ int alifmm_set_option(alifmm_ctx* ctx, const char* name, double value) {
   else if (!strcmp(name, "r0") && value >= 0) ctx->r0 = value;
   else if (!strcmp(name, "batch") && value >= 1) ctx->batch = (int)value;
   else if (!strcmp(name, "prof")) ctx->prof = value != 0;
+  else if (!strcmp(name, "pair")) ctx->pair = value != 0;
   else if (!strcmp(name, "exact_r") && value >= 0 && value <= 48) ctx->exact_r = (int)value;
   else return fail(ctx, ALIFMM_E_ARG, "unknown option or bad value: %s=%g", name, value);
+  return ALIFMM_OK;
+}
+
+int alifmm_get_option(alifmm_ctx* ctx, const char* name, double* value) {
+  if (!ctx || !name || !value) return ALIFMM_E_ARG;
+  if (!strcmp(name, "cdelta")) *value = ctx->cdelta;
+  else if (!strcmp(name, "r0")) *value = ctx->r0;
+  else if (!strcmp(name, "batch")) *value = ctx->batch;
+  else if (!strcmp(name, "exact_r")) *value = ctx->exact_r;
+  else if (!strcmp(name, "prof")) *value = ctx->prof;
+  else if (!strcmp(name, "pair")) *value = ctx->pair;
+  else if (!strcmp(name, "last_pair")) *value = ctx->last_pair;
+  else if (!strcmp(name, "n_cu")) *value = ctx->n_cu;
+  else return fail(ctx, ALIFMM_E_ARG, "unknown option: %s", name);
   return ALIFMM_OK;
 }
 
@@ -378,6 +400,8 @@ static int ensure_arena(alifmm_ctx* ctx, int nsrc, long cells, long capL, long c
   a.capS = capS;
   HIPCHK(dalloc(&a.S, (size_t)nsrc * cells));
   HIPCHK(dalloc(&a.own, (size_t)nsrc * cells));
+  HIPCHK(dalloc(&a.ax, (size_t)nsrc * 2 * capL));
+  HIPCHK(dalloc(&a.px, nsrc));
   HIPCHK(dalloc(&a.lists, (size_t)nsrc * (3 * capL + 2 * capC)));
   HIPCHK(dalloc(&a.dlists, (size_t)nsrc * (2 * capL + capC)));
   if (capS > 0) {
@@ -436,6 +460,9 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
     b.T = ctx->fields[slot].d;
     b.S = a.S + (size_t)i * a.cells;
     b.own = a.own + (size_t)i * a.cells;
+    b.ax[0] = a.ax + (size_t)i * 2 * a.capL;
+    b.ax[1] = b.ax[0] + a.capL;
+    b.px = a.px + i;
     int* base = a.lists + (size_t)i * (3 * a.capL + 2 * a.capC);
     b.L0 = base;
     b.L1 = base + a.capL;
@@ -515,7 +542,14 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
     HIPCHK(af_launch_exact(&P, ctx->stream));
   }
   HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
-  HIPCHK(af_launch_band(&P, ctx->stream));
+  bool paired = false;
+  if (ctx->pair && !ctx->prof && 16 * ((n + 7) / 8) <= ctx->n_cu) {
+    HIPCHK(hipMemsetAsync(a.px, 0, sizeof(af::PairX) * n, ctx->stream));
+    paired = af_launch_band_pair(&P, ctx->stream) == hipSuccess;
+    if (!paired) (void)hipGetLastError();  // not co-resident / model too large for LDS: single kernel
+  }
+  ctx->last_pair = paired;
+  if (!paired) HIPCHK(af_launch_band(&P, ctx->stream));
   HIPCHK(hipEventRecord(ctx->ev[2], ctx->stream));
   if (sg > 1)
     for (int i = 0; i < n; i++) HIPCHK(af_launch_scale(hs[i].T, cells, (double)sg, ctx->stream));
@@ -560,8 +594,10 @@ int alifmm_travel(alifmm_ctx* ctx, int subgrid, int nsrc, const double* scx, con
   hipEvent_t t_begin;
   HIPCHK(hipEventCreate(&t_begin));
   HIPCHK(hipEventRecord(t_begin, ctx->stream));
-  for (int s0 = 0; s0 < nsrc; s0 += ctx->batch) {
-    int n = std::min(ctx->batch, nsrc - s0);
+  // chunk: two workgroups per source need 2n CUs (pair mode), one per source otherwise
+  const int chunk = (ctx->pair && !ctx->prof && ctx->n_cu >= 16) ? std::min(ctx->batch, ctx->n_cu / 16 * 8) : ctx->batch;
+  for (int s0 = 0; s0 < nsrc; s0 += chunk) {
+    int n = std::min(chunk, nsrc - s0);
     int rc;
     for (;;) {
       rc = travel_chunk(ctx, subgrid, n, scx + s0, scz + s0, first_slot + s0, fz, fx, &ms_init, &ms_band);

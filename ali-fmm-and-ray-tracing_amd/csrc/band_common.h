@@ -1,0 +1,92 @@
+// band_common.h — helpers shared by the band-synchronous FMM kernels (fmm_band.hip: one
+// workgroup per source; fmm_band_pair.hip: two workgroups per source).
+#pragma once
+#include "kernels.h"
+
+namespace af {
+
+template <class T, int CAP>
+struct HList {
+  T* l;  // LDS head
+  T* g;  // global array (same indexing)
+  AF_DEV T get(int i) const { return i < CAP ? l[i] : gld(g + i); }
+  AF_DEV void put(int i, T v) const {
+    if (i < CAP) l[i] = v;
+    else gst(g + i, v);
+  }
+};
+
+AF_DEV int lane_id() { return threadIdx.x & 63; }
+
+// append with one LDS atomic per wave; returns the slot or -1 (pred false / overflow)
+AF_DEV int wave_push(int* counter, bool pred, int cap, int* err) {
+  unsigned long long m = __ballot(pred);
+  if (m == 0) return -1;
+  int lane = lane_id();
+  int leader = __ffsll((long long)m) - 1;
+  int base = 0;
+  if (lane == leader) base = atomicAdd(counter, __popcll(m));
+  base = __shfl(base, leader);
+  int off = __popcll(m & ((1ull << lane) - 1ull));
+  if (!pred) return -1;
+  int slot = base + off;
+  if (slot >= cap) {
+    *err = 2;
+    return -1;
+  }
+  return slot;
+}
+
+AF_DEV double wave_min(double v) {
+  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
+  return v;
+}
+
+// Lists hold cells as packed (z << 16 | x) keys (grids are < 32768 per side): no integer
+// divisions on the hot path; the flat index z * nx + x is formed where memory is addressed.
+AF_DEV int pk(int z, int x) { return (z << 16) | x; }
+AF_DEV int pkz(int k) { return k >> 16; }
+AF_DEV int pkx(int k) { return k & 0xffff; }
+AF_DEV int pk_flat(int k, int nx) { return pkz(k) * nx + pkx(k); }
+
+// neighbour d (0 -x, 1 +x, 2 -z, 3 +z) of packed cell c, or -1 outside the grid
+AF_DEV int nb_cell(int c, int d, int nz, int nx) {
+  const int z = pkz(c) + (d == 2 ? -1 : d == 3 ? 1 : 0);
+  const int x = pkx(c) + (d == 0 ? -1 : d == 1 ? 1 : 0);
+  return (z < 0 || z >= nz || x < 0 || x >= nx) ? -1 : pk(z, x);
+}
+
+// exclusive prefix sum over the wave's lanes, and the wave total
+AF_DEV int wave_excl_scan(int v, int& total) {
+  const int lane = threadIdx.x & 63;
+  int inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(inc, o);
+    if (lane >= o) inc += t;
+  }
+  total = __shfl(inc, 63);
+  return inc - v;
+}
+
+struct RunCfg {
+  int nz, nx;
+  double dnx, dnz;  // update() spacing and fouds18 dnz
+  MatView mv;
+  double delta, t0;
+};
+
+// material of main-grid cell (z, x): LDSMAT = one id load + the LDS record; else four arrays
+template <bool LDSMAT>
+AF_DEV CellMat band_mat(const DevModel& M, const MatRec* mat, const double* stab, const MatView& v, int z, int x) {
+  if (!LDSMAT) return cell_mat(M, v, z, x);
+  const MatRec m = mat[gld(M.mid + mv_cell(M, v, z, x))];
+  CellMat r;
+  r.velpn = m.velpn;
+  r.veln = v.quant ? (double)(int)m.veln : m.veln;
+  r.vm = v.quant ? (double)(float)m.vm : m.vm;
+  r.stif = m.sidx >= 0 ? stab + 5 * m.sidx : nullptr;
+  return r;
+}
+
+}  // namespace af

@@ -25,6 +25,17 @@ AF_DEV void gst(T* p, T v) {
   *(AF_GLOBAL T*)p = v;
 }
 AF_DEV int gatomic_max(int* p, int v) { return __atomic_fetch_max((AF_GLOBAL int*)p, v, __ATOMIC_RELAXED); }
+// sc1 (L1-bypassing load, write-through store) accesses for data another CU writes or reads
+// within the same launch (MI355X_MICROARCH.md "inter-workgroup visibility": sc1 stores, drained
+// with vmcnt(0) before the signal, read back with sc1 loads after the signal)
+template <class T>
+AF_DEV T gld_sc1(const T* p) {
+  return __hip_atomic_load((AF_GLOBAL T*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T>
+AF_DEV void gst_sc1(T* p, T v) {
+  __hip_atomic_store((AF_GLOBAL T*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 constexpr double kDeg2Rad = M_PI / 180.0;
 constexpr double kRad2Deg = 180.0 / M_PI;

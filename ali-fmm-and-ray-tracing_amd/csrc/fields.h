@@ -17,6 +17,15 @@ struct GField {
   AF_DEV double tt(long z, long x) const { return z >= nz ? 0.0 : far0(gld(T + z * nx + x)); }
 };
 
+// GField with sc1 loads: a grid that another workgroup of the same launch also writes
+struct GFieldSC1 {
+  const double* T;
+  const int* S;
+  int nz, nx;
+  AF_DEV int st(long z, long x) const { return z >= nz ? -1 : gld_sc1(S + z * nx + x); }
+  AF_DEV double tt(long z, long x) const { return z >= nz ? 0.0 : far0(gld_sc1(T + z * nx + x)); }
+};
+
 // Register copy of the 12 cells update() reads around (iz, ix): (0,+-1) (+-1,0) (+-1,+-1) (0,+-2)
 // (+-2,0).  All 24 loads are issued together (one memory round trip instead of a chain of
 // branch-dependent gathers).  Same values as GField: rows >= nz read status -1 / time 0 (the
@@ -114,6 +123,27 @@ struct NbFieldT {
     t[7] = gld(T + cl(p + 2 * nx, 1));
     const int dz[12] = {0, 0, 0, 0, -2, -1, 1, 2, -1, -1, 1, 1};
     unsigned m = 0;
+#pragma unroll
+    for (int k = 0; k < 12; k++)
+      if (z + dz[k] < nz && t[k] == t[k]) m |= 1u << k;
+    vm = m;
+    t0 = t[0]; t1 = t[1]; t2 = t[2]; t3 = t[3]; t4 = t[4]; t5 = t[5];
+    t6 = t[6]; t7 = t[7]; t8 = t[8]; t9 = t[9]; t10 = t[10]; t11 = t[11];
+  }
+  // As load(), with 12 sc1 loads (cells another workgroup of the launch writes)
+  AF_DEV void load_sc1(const double* T, int nz, int nx, int z, int x) {
+    iz = z;
+    ix = x;
+    const int n = nz * nx;
+    const int dz[12] = {0, 0, 0, 0, -2, -1, 1, 2, -1, -1, 1, 1};
+    const int dx[12] = {-2, -1, 1, 2, 0, 0, 0, 0, -1, 1, -1, 1};
+    double t[12];
+    unsigned m = 0;
+#pragma unroll
+    for (int k = 0; k < 12; k++) {
+      const int c = (z + dz[k]) * nx + (x + dx[k]);
+      t[k] = gld_sc1(T + (c < 0 ? 0 : c >= n ? n - 1 : c));
+    }
 #pragma unroll
     for (int k = 0; k < 12; k++)
       if (z + dz[k] < nz && t[k] == t[k]) m |= 1u << k;

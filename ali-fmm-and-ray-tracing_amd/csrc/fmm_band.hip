@@ -18,6 +18,7 @@
 #include "kernels.h"
 #include "local_ops.h"
 #include "fields.h"
+#include "band_common.h"
 
 namespace af {
 
@@ -65,77 +66,6 @@ struct BandLds {
   int err;
 };
 
-template <class T, int CAP>
-struct HList {
-  T* l;  // LDS head
-  T* g;  // global array (same indexing)
-  AF_DEV T get(int i) const { return i < CAP ? l[i] : gld(g + i); }
-  AF_DEV void put(int i, T v) const {
-    if (i < CAP) l[i] = v;
-    else gst(g + i, v);
-  }
-};
-
-AF_DEV int lane_id() { return threadIdx.x & 63; }
-
-// append with one LDS atomic per wave; returns the slot or -1 (pred false / overflow)
-AF_DEV int wave_push(int* counter, bool pred, int cap, int* err) {
-  unsigned long long m = __ballot(pred);
-  if (m == 0) return -1;
-  int lane = lane_id();
-  int leader = __ffsll((long long)m) - 1;
-  int base = 0;
-  if (lane == leader) base = atomicAdd(counter, __popcll(m));
-  base = __shfl(base, leader);
-  int off = __popcll(m & ((1ull << lane) - 1ull));
-  if (!pred) return -1;
-  int slot = base + off;
-  if (slot >= cap) {
-    *err = 2;
-    return -1;
-  }
-  return slot;
-}
-
-AF_DEV double wave_min(double v) {
-  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
-  return v;
-}
-
-// Lists hold cells as packed (z << 16 | x) keys (grids are < 32768 per side): no integer
-// divisions on the hot path; the flat index z * nx + x is formed where memory is addressed.
-AF_DEV int pk(int z, int x) { return (z << 16) | x; }
-AF_DEV int pkz(int k) { return k >> 16; }
-AF_DEV int pkx(int k) { return k & 0xffff; }
-AF_DEV int pk_flat(int k, int nx) { return pkz(k) * nx + pkx(k); }
-
-// neighbour d (0 -x, 1 +x, 2 -z, 3 +z) of packed cell c, or -1 outside the grid
-AF_DEV int nb_cell(int c, int d, int nz, int nx) {
-  const int z = pkz(c) + (d == 2 ? -1 : d == 3 ? 1 : 0);
-  const int x = pkx(c) + (d == 0 ? -1 : d == 1 ? 1 : 0);
-  return (z < 0 || z >= nz || x < 0 || x >= nx) ? -1 : pk(z, x);
-}
-
-// exclusive prefix sum over the wave's lanes, and the wave total
-AF_DEV int wave_excl_scan(int v, int& total) {
-  const int lane = threadIdx.x & 63;
-  int inc = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int t = __shfl_up(inc, o);
-    if (lane >= o) inc += t;
-  }
-  total = __shfl(inc, 63);
-  return inc - v;
-}
-
-struct RunCfg {
-  int nz, nx;
-  double dnx, dnz;  // update() spacing and fouds18 dnz
-  MatView mv;
-  double delta, t0;
-};
-
 // fouds18_A() fallback out of line: rare, and inlined its live ranges (~180 VGPRs) would set
 // the whole kernel's register budget
 #if AF_FOUDS_NOINLINE
@@ -146,19 +76,6 @@ AF_DEV
 double fouds18_global(const GField& F, const DevModel& M, const CellMat& cm, int z, int x, double dnx, double dnz,
                       int nx, int nz) {
   return fouds18(F, M, cm, z, x, dnx, dnz, nx, nz);
-}
-
-// material of main-grid cell (z, x): LDSMAT = one id load + the LDS record; else four arrays
-template <bool LDSMAT>
-AF_DEV CellMat band_mat(const DevModel& M, const BandLds* sh, const MatView& v, int z, int x) {
-  if (!LDSMAT) return cell_mat(M, v, z, x);
-  const MatRec m = sh->mat[gld(M.mid + mv_cell(M, v, z, x))];
-  CellMat r;
-  r.velpn = m.velpn;
-  r.veln = v.quant ? (double)(int)m.veln : m.veln;
-  r.vm = v.quant ? (double)(float)m.vm : m.vm;
-  r.stif = m.sidx >= 0 ? sh->stab + 5 * m.sidx : nullptr;
-  return r;
 }
 
 AF_DEV unsigned hash_slot(int key) { return ((unsigned)key * 2654435761u) >> (32 - AF_HASH_LOG2); }
@@ -309,8 +226,8 @@ AF_DEV long long band_run(const BandParams& P, BandLds* sh, BandSrc* B, const Ru
       const bool has1 = e1 < nE;
       const int r0 = EL.get(e0), r1 = has1 ? EL.get(e1) : r0;
       const int z0 = pkz(r0), x0 = pkx(r0), z1 = pkz(r1), x1 = pkx(r1);
-      const CellMat m0 = band_mat<LDSMAT>(M, sh, R.mv, z0, x0);
-      const CellMat m1 = band_mat<LDSMAT>(M, sh, R.mv, z1, x1);
+      const CellMat m0 = band_mat<LDSMAT>(M, sh->mat, sh->stab, R.mv, z0, x0);
+      const CellMat m1 = band_mat<LDSMAT>(M, sh->mat, sh->stab, R.mv, z1, x1);
       NbFieldT n0, n1;
       n0.load(T, nz, nx, z0, x0);
       n1.load(T, nz, nx, z1, x1);
@@ -323,7 +240,7 @@ AF_DEV long long band_run(const BandParams& P, BandLds* sh, BandSrc* B, const Ru
       const int r = EL.get(e);
       const int z = pkz(r), x = pkx(r);
       if (prof) ts = wall_clock64();
-      const CellMat cm = band_mat<LDSMAT>(M, sh, R.mv, z, x);
+      const CellMat cm = band_mat<LDSMAT>(M, sh->mat, sh->stab, R.mv, z, x);
       NbFieldT nb;
       nb.load(T, nz, nx, z, x);
       AF_SUB(3)
@@ -338,7 +255,7 @@ AF_DEV long long band_run(const BandParams& P, BandLds* sh, BandSrc* B, const Ru
       if (VL.get(e) == -1.0) {
         const int r = EL.get(e);
         const int z = pkz(r), x = pkx(r);
-        const CellMat cm = band_mat<LDSMAT>(M, sh, R.mv, z, x);
+        const CellMat cm = band_mat<LDSMAT>(M, sh->mat, sh->stab, R.mv, z, x);
         VL.put(e, fouds18_global(F, M, cm, z, x, R.dnx, R.dnz, nx, nz));
       }
     }

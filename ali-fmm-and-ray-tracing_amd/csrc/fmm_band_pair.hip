@@ -1,0 +1,419 @@
+// fmm_band_pair.hip — the band-synchronous FMM of fmm_band.hip with TWO workgroups (two CUs)
+// per source, so that 128 sources fill the 256 CUs of an MI355X.
+//
+// Cells are owned by column stripes of 64: member m owns columns with (x >> 6) & 1 == m.  Each
+// member keeps the close set, accepted / claimed lists and claim hash of its own cells in LDS and
+// evaluates / commits only its own cells; the step is the single-workgroup step with two
+// pair barriers (one counter per source, relaxed agent-scope atomics + sc1 polling):
+//   P1  local Tmin -> exchange (Tmin, live, err) --X1--  global Tmin; apply the previous step's
+//       deferred edge commits
+//   P2  accept own cells; own accepted cells next to the partner's columns -> exchange list --X2--
+//   P3  claim own neighbours of both members' accepted cells; evaluate them (Jacobi)
+//   P4  commit: interior cells directly; EDGE cells (within 2 columns of a stripe boundary, i.e.
+//       readable by the partner's 12-cell stencil) are deferred to after the next X1, so the
+//       partner never sees a value of this step while it may still be evaluating it.
+// Data the partner reads (edge cells' T and status, exchange lists) is written with sc1 stores,
+// drained (vmcnt 0) before the barrier, and read with sc1 loads.  Results are identical to the
+// single-workgroup kernel: the same cells are accepted, claimed and evaluated against the same
+// state each step; only which CU does the work differs.
+#include "kernels.h"
+#include "local_ops.h"
+#include "fields.h"
+#include "band_common.h"
+
+namespace af {
+
+namespace pair {
+
+constexpr int kThreads = 512;
+constexpr int kWaves = kThreads / 64;
+constexpr int kStripeLog = 6;
+constexpr int kStripe = 1 << kStripeLog;
+constexpr int kLcap = 2560, kAcap = 1024, kEcap = 1536, kDcap = 1024;
+constexpr int kHashLog = 13;
+constexpr int kHash = 1 << kHashLog;
+constexpr int kHashItems = 6144;  // claim items (both members' accepted cells x 4) for the LDS hash
+constexpr int kStabLds = 64, kPtabLds = 722, kMatLds = 256;
+
+struct Lds {
+  double red[kWaves];
+  double Lt[kLcap];
+  double Vl[kEcap];
+  double Dv[kDcap];  // deferred edge commits: value
+  double stab[kStabLds * 5];
+  double ptab[kPtabLds];
+  MatRec mat[kMatLds];
+  int Ll[kLcap];
+  int Fs[kLcap];
+  int Al[kAcap];
+  int El[kEcap];
+  int Ep[kEcap];
+  int Dc[kDcap];  // deferred edge commits: packed cell
+  int Ds[kDcap];  // deferred edge commits: new status (1 + slot) or 0 for "T only"
+  alignas(16) int H[kHash];
+  double tmin_g;
+  int nA, nE, nF, hi, taken, nD, nAx, live_g, err_g, err;
+};
+
+AF_DEV bool mine(int x, int m) { return ((x >> kStripeLog) & 1) == m; }
+// within 2 columns of a stripe boundary: the partner's stencils (update() and fouds18_A()) read it
+AF_DEV bool edge(int x) {
+  const int r = x & (kStripe - 1);
+  return r < 2 || r >= kStripe - 2;
+}
+// next to a stripe boundary: its x-neighbour belongs to the partner
+AF_DEV bool rim(int x) {
+  const int r = x & (kStripe - 1);
+  return r == 0 || r == kStripe - 1;
+}
+AF_DEV unsigned hslot(int key) { return ((unsigned)key * 2654435761u) >> (32 - kHashLog); }
+
+// two-member barrier; false on timeout (the partner never arrived: both members then stop)
+AF_DEV bool pair_barrier(int* ctr, int& gen, Lds* sh) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores are complete
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add((AF_GLOBAL int*)ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    gen += 2;
+    long spins = 0;
+    while (gld_sc1(ctr) < gen) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1L << 25)) {  // ~seconds: never reached unless the partner is not resident
+        sh->err = 7;
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  return sh->err != 7;
+}
+
+template <int MODE, bool LDSMAT>
+__global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
+  __shared__ Lds sh_;
+  Lds* sh = &sh_;
+  const int b = blockIdx.x;
+  const int src = (b / 16) * 8 + (b % 8), me = (b / 8) & 1, pt = me ^ 1;
+  if (src >= P.nsrc) return;  // both members of a pair take this exit together
+  BandSrc* B = P.src + src;
+  PairX* X = B->px;
+  const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
+  const int nz = P.nz, nx = P.nx;
+  double* T = B->T;
+  int* S = B->S;
+  int* own = B->own;
+  int* AXm = B->ax[me];
+  const int* AXp = B->ax[pt];
+  DevModel M = P.M;
+  if (LDSMAT) {
+    for (int k = tid; k < 5 * M.nstab; k += kThreads) sh->stab[k] = M.stab[k];
+    for (int k = tid; k < 361 * M.ncol; k += kThreads) sh->ptab[k] = M.ptab[k];
+    for (int k = tid; k < M.nmat; k += kThreads) sh->mat[k] = M.mtab[k];
+    M.ptab = sh->ptab;
+  }
+  // per-member halves of the work arrays (global spill of the LDS lists)
+  const long hL = P.capL / 2, hC = P.capC / 2;
+  const HList<int, kLcap> L{sh->Ll, B->L0 + me * hL};
+  const HList<double, kLcap> Lt{sh->Lt, B->Lt0 + me * hL};
+  const HList<int, kLcap> FS{sh->Fs, B->L1 + me * hL};
+  const HList<int, kAcap> AL{sh->Al, B->A + me * hL};
+  const HList<int, kEcap> EL{sh->El, B->C + me * hC};
+  const HList<int, kEcap> EP{sh->Ep, B->Cp + me * hC};
+  const HList<double, kEcap> VL{sh->Vl, B->V + me * hC};
+  const int capL = (int)hL, capC = (int)hC;
+  if (tid == 0) {
+    sh->hi = 0;
+    sh->nF = 0;
+    sh->nD = 0;
+    sh->err = 0;
+  }
+  __syncthreads();
+  // ---------------- hand-over: own cells only ----------------
+  if (MODE == 0) {
+    const HandoverOut* H = P.ho + src;
+    if (tid == 0 && H->err) sh->err = 3;
+    const int n = H->n;
+    for (int k0 = wv * 64; k0 < n; k0 += kThreads) {
+      const int k = k0 + lane;
+      bool push = false;
+      int c = 0, z = 0, x = 0;
+      double t = 0.0;
+      if (k < n) {
+        c = H->cell[k];
+        z = c / nx;
+        x = c - z * nx;
+        if (mine(x, me)) {
+          t = H->ttn[k];
+          gst_sc1(T + c, t);
+          if (H->cls[k] == 1) gst_sc1(S + c, (int)kKnown);
+          else push = true;
+        }
+      }
+      const int s = wave_push(&sh->hi, push, capL, &sh->err);
+      if (s >= 0) {
+        L.put(s, pk(z, x));
+        Lt.put(s, t);
+        gst_sc1(S + c, 1 + s);
+      }
+    }
+  } else {
+    if (tid == 0 && B->err) sh->err = B->err;
+    const int n = B->nl0;
+    for (int k0 = wv * 64; k0 < n; k0 += kThreads) {
+      const int k = k0 + lane;
+      bool push = false;
+      int c = 0, z = 0, x = 0;
+      if (k < n) {
+        c = gld(B->L0 + k);
+        z = c / nx;
+        x = c - z * nx;
+        push = mine(x, me);
+      }
+      // both members read all of L0 before either rewrites its half (member 0's half starts at
+      // L0[0]): stage the own cells first, then rewrite after the barrier below
+      const int s = wave_push(&sh->hi, push, capL, &sh->err);
+      if (s >= 0) {  // cells staged in the (still unused) free-stack arrays, copied after the barrier
+        Lt.put(s, gld(T + c));
+        FS.put(s, pk(z, x));
+        gst_sc1(S + c, 1 + s);
+      }
+    }
+  }
+  int gen = 0;
+  // both members have read the hand-over input and written their statuses
+  pair_barrier(&X->bar, gen, sh);
+  if (MODE == 1) {
+    for (int k = tid; k < sh->hi; k += kThreads) L.put(k, FS.get(k));
+    __syncthreads();
+  }
+  RunCfg R;
+  R.nz = nz;
+  R.nx = nx;
+  R.dnx = P.dnx;
+  R.dnz = P.dnz;
+  if (MODE == 0)
+    R.mv = MatView{1, 0, 0, 1, 0, 0, 1, 0, 0, 0, 0};
+  else
+    R.mv = MatView{P.sg, (P.sg - 1) / 2, 0, P.sg, (P.sg - 1) / 2, 0, 1, 0, 0, 0, 1};
+  R.delta = P.cdelta * P.dnx / P.vmax;
+  R.t0 = P.r0 * P.dnx / P.vmax;
+  const GFieldSC1 F{T, S, nz, nx};
+  long long steps = 0, myupd = 0;
+  while (true) {
+    const int par = (int)(steps & 1);
+    const int hi = sh->hi;
+    // ---- P1: local Tmin, exchange ----
+    double tmin = INFINITY;
+    for (int e = tid; e < hi; e += kThreads) tmin = fmin(tmin, Lt.get(e));
+    for (int k = tid * 4; k < kHash; k += kThreads * 4) *(int4*)&sh->H[k] = make_int4(0, 0, 0, 0);
+    tmin = wave_min(tmin);
+    if (lane == 0) sh->red[wv] = tmin;
+    __syncthreads();
+    if (tid == 0) {
+      double t = sh->red[0];
+      for (int w = 1; w < kWaves; w++) t = fmin(t, sh->red[w]);
+      gst_sc1(&X->tmin[me][par], t);
+      gst_sc1(&X->live[me][par], hi - sh->nF);
+      gst_sc1(&X->err[me][par], sh->err);
+      sh->tmin_g = t;
+      sh->nA = 0;
+      sh->nE = 0;
+      sh->taken = 0;
+    }
+    if (!pair_barrier(&X->bar, gen, sh)) break;  // X1
+    if (tid == 0) {
+      sh->tmin_g = fmin(sh->tmin_g, gld_sc1(&X->tmin[pt][par]));
+      sh->live_g = (hi - sh->nF) + gld_sc1(&X->live[pt][par]);
+      sh->err_g = sh->err | gld_sc1(&X->err[pt][par]);
+    }
+    // apply the previous step's deferred edge commits (the partner finished evaluating it)
+    for (int d = tid; d < sh->nD; d += kThreads) {
+      const int c = sh->Dc[d];
+      const long f = (long)pkz(c) * nx + pkx(c);
+      gst_sc1(T + f, sh->Dv[d]);
+      if (sh->Ds[d] > 0) gst_sc1(S + f, sh->Ds[d]);
+    }
+    __syncthreads();
+    if (sh->live_g <= 0 || sh->err_g) break;
+    if (tid == 0) sh->nD = 0;
+    tmin = sh->tmin_g;
+    double dl = R.delta;
+    if (R.t0 > 0 && tmin < R.t0) dl = R.delta * (tmin / R.t0);
+    const double thr = tmin + dl;
+    // ---- P2: accept own cells; rim cells go to the exchange list ----
+    int* nax = &sh->nAx;
+    if (tid == 0) *nax = 0;
+    __syncthreads();
+    for (int e0 = wv * 64; e0 < hi; e0 += kThreads) {
+      const int e = e0 + lane;
+      const double t = e < hi ? Lt.get(e) : INFINITY;
+      const bool acc = t <= thr;
+      const int c = acc ? L.get(e) : 0;
+      const int sa = wave_push(&sh->nA, acc, capL, &sh->err);
+      if (sa >= 0) {
+        AL.put(sa, c);
+        const long f = (long)pkz(c) * nx + pkx(c);
+        if (edge(pkx(c))) gst_sc1(S + f, (int)kKnown);
+        else gst(S + f, (int)kKnown);
+        Lt.put(e, INFINITY);
+      }
+      const int sf = wave_push(&sh->nF, acc, capL, &sh->err);
+      if (sf >= 0) FS.put(sf, e);
+      const int sx = wave_push(nax, acc && rim(pkx(c)), capL, &sh->err);
+      if (sx >= 0) gst_sc1(AXm + sx, c);
+    }
+    __syncthreads();
+    if (tid == 0) gst_sc1(&X->nax[me][par], *nax);
+    if (!pair_barrier(&X->bar, gen, sh)) break;  // X2
+    const int nA = min(sh->nA, capL);
+    const int nAp = gld_sc1(&X->nax[pt][par]);  // (uniform; every thread reads it)
+    // ---- P3a: claim own neighbours of own accepted cells and of the partner's rim cells ----
+    const int nItems = 4 * (nA + nAp);
+    const bool use_hash = nItems <= kHashItems;
+    const int stamp = (int)steps;
+    for (int q0 = wv * 64 * 8; q0 < nItems; q0 += kThreads * 8) {
+      int r[8], s[8], o[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int q = q0 + u * 64 + lane;
+        int c = -1;
+        if (q < nItems) {
+          const int a = q >> 2;
+          const int ac = a < nA ? AL.get(a) : gld_sc1(AXp + (a - nA));
+          c = nb_cell(ac, q & 3, nz, nx);
+          if (c >= 0 && !mine(pkx(c), me)) c = -1;
+        }
+        if (use_hash && c >= 0) {
+          unsigned h = hslot(c);
+          for (int probe = 0;; probe++) {
+            const int prev = atomicCAS(&sh->H[h], 0, c + 1);
+            if (prev == 0) break;
+            if (prev == c + 1 || probe >= kHash) {
+              if (probe >= kHash) sh->err = 5;
+              c = -1;
+              break;
+            }
+            h = (h + 1) & (kHash - 1);
+          }
+        }
+        r[u] = c;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const long f = r[u] >= 0 ? (long)pkz(r[u]) * nx + pkx(r[u]) : 0;
+        s[u] = r[u] >= 0 ? (edge(pkx(r[u])) ? gld_sc1(S + f) : gld(S + f)) : (int)kKnown;
+        o[u] = (!use_hash && r[u] >= 0) ? gatomic_max(own + f, stamp) : -1;
+      }
+      int nw = 0;
+#pragma unroll
+      for (int u = 0; u < 8; u++) nw += (s[u] != kKnown && o[u] < stamp) ? 1 : 0;
+      int tot;
+      const int off = wave_excl_scan(nw, tot);
+      int base = 0;
+      if (lane == 0 && tot) base = atomicAdd(&sh->nE, tot);
+      base = __shfl(base, 0) + off;
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        if (s[u] != kKnown && o[u] < stamp) {
+          if (base < capC) {
+            EL.put(base, r[u]);
+            EP.put(base, s[u] > 0 ? s[u] - 1 : -1);
+          } else {
+            sh->err = 2;
+          }
+          base++;
+        }
+      }
+    }
+    __syncthreads();
+    const int nE = min(sh->nE, capC);
+    // ---- P3b: evaluate (cells whose stencil reaches the partner's columns: sc1 loads) ----
+    for (int e = tid; e < nE; e += kThreads) {
+      const int r = EL.get(e);
+      const int z = pkz(r), x = pkx(r);
+      const CellMat cm = band_mat<LDSMAT>(M, sh->mat, sh->stab, R.mv, z, x);
+      NbFieldT nb;
+      if (edge(x)) nb.load_sc1(T, nz, nx, z, x);
+      else nb.load(T, nz, nx, z, x);
+      VL.put(e, update(nb, M, cm, z, x, R.dnx, nz, nx));
+      myupd++;
+    }
+    for (int e = tid; e < nE; e += kThreads) {
+      if (VL.get(e) == -1.0) {
+        const int r = EL.get(e);
+        const int z = pkz(r), x = pkx(r);
+        const CellMat cm = band_mat<LDSMAT>(M, sh->mat, sh->stab, R.mv, z, x);
+        VL.put(e, fouds18(F, M, cm, z, x, R.dnx, R.dnz, nx, nz));
+      }
+    }
+    __syncthreads();
+    // ---- P4: commit own cells; edge cells deferred to after the next X1 ----
+    const int nF = sh->nF;
+    for (int e0 = wv * 64; e0 < nE; e0 += kThreads) {
+      const int e = e0 + lane;
+      bool fresh = false, defer = false;
+      int r = 0;
+      double v = 0.0;
+      if (e < nE) {
+        r = EL.get(e);
+        v = VL.get(e);
+        const int p = EP.get(e);
+        defer = edge(pkx(r));
+        if (!defer) gst(T + (long)pkz(r) * nx + pkx(r), v);
+        if (p >= 0) Lt.put(p, v);
+        else fresh = true;
+      }
+      const int k = wave_push(&sh->taken, fresh, 1 << 30, &sh->err);
+      int slot = -1;
+      if (k >= 0) {
+        slot = k < nF ? FS.get(nF - 1 - k) : hi + (k - nF);
+        if (slot >= capL) {
+          sh->err = 2;
+          slot = -1;
+        } else {
+          L.put(slot, r);
+          Lt.put(slot, v);
+          if (!defer) gst(S + (long)pkz(r) * nx + pkx(r), 1 + slot);
+        }
+      }
+      const int dslot = wave_push(&sh->nD, defer, kDcap, &sh->err);
+      if (dslot >= 0) {
+        sh->Dc[dslot] = r;
+        sh->Dv[dslot] = v;
+        sh->Ds[dslot] = slot >= 0 ? 1 + slot : 0;
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      const int tk_ = sh->taken;
+      sh->nF = max(0, nF - tk_);
+      sh->hi = hi + max(0, tk_ - nF);
+    }
+    steps++;
+    __syncthreads();
+  }
+  for (int o = 32; o > 0; o >>= 1) myupd += __shfl_xor(myupd, o);
+  if (lane == 0 && myupd) atomicAdd((unsigned long long*)&B->nupd, (unsigned long long)myupd);
+  if (tid == 0) {
+    if (me == 0) B->steps[3] = steps;
+    const int e = sh->err ? sh->err : sh->err_g;
+    if (e) B->err = e;
+  }
+}
+
+}  // namespace pair
+}  // namespace af
+
+// cooperative launch (all 2*nsrc workgroups resident, one per CU); hipErrorCooperativeLaunchTooLarge
+// (or any launch error) tells the caller to use the single-workgroup kernel instead
+extern "C" hipError_t af_launch_band_pair(const af::BandParams* P, hipStream_t stream) {
+  const bool lds = P->M.mid && P->M.nmat <= af::pair::kMatLds && P->M.nstab <= af::pair::kStabLds &&
+                   361 * P->M.ncol <= af::pair::kPtabLds;
+  if (!lds) return hipErrorNotSupported;
+  const dim3 g(16 * ((P->nsrc + 7) / 8)), b(af::pair::kThreads);
+  af::BandParams Pc = *P;
+  void* args[] = {&Pc};
+  const void* fn = P->mode == 0 ? (const void*)af::pair::fmm_band_pair_kernel<0, true>
+                                : (const void*)af::pair::fmm_band_pair_kernel<1, true>;
+  return hipLaunchCooperativeKernel(fn, g, b, args, 0, stream);
+}

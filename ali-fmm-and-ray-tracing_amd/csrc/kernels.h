@@ -5,6 +5,17 @@
 
 namespace af {
 
+// per-source exchange block of the two-workgroup band kernel (fmm_band_pair.hip); zeroed by the
+// host before each launch.  Every field is written by one member with sc1 stores.
+struct PairX {
+  int bar;          // pair barrier counter
+  int pad[31];
+  double tmin[2][2];  // [member][step parity]
+  int live[2][2];
+  int err[2][2];
+  int nax[2][2];    // accepted cells next to the other member's columns, per step
+};
+
 struct BandSrc {
   double* T;      // field (main grid)
   int* S;         // status: far -1, known 0, close 1 + close-list slot
@@ -18,6 +29,8 @@ struct BandSrc {
   int* Cp;        // their close-list slot (-1: far)
   double* V;      // claimed cells' new values
   double* Ts[2];  // stage grids (mode 1)
+  int* ax[2];     // pair mode: each member's accepted cells next to the partner's columns
+  PairX* px;      // pair mode: exchange block
   int* Ss[2];
   long long steps[4];
   long long nupd;  // relax evaluations (cell-sweeps) in the main run
@@ -97,6 +110,7 @@ extern "C" {
 hipError_t af_launch_init(const af::DevModel* M, af::InitJob* jobs, int njobs, af::HandoverOut* out, hipStream_t stream);
 hipError_t af_launch_exact(const af::BandParams* P, hipStream_t stream);
 hipError_t af_launch_band(const af::BandParams* P, hipStream_t stream);
+hipError_t af_launch_band_pair(const af::BandParams* P, hipStream_t stream);
 hipError_t af_launch_scale(double* T, long n, double sg, hipStream_t stream);
 hipError_t af_launch_rays(const af::RayParams* P, hipStream_t stream);
 hipError_t af_launch_pack_rays(const double* rx, const double* ry, const int* len, const long long* off, int nrays,

@@ -46,10 +46,15 @@ int alifmm_set_model(alifmm_ctx* ctx, int nnz, int nnx, const double* veln, cons
                      const double* vel_map, const int64_t* stif_den, const double* group_tab,
                      const double* phase_tab, int ncol, double dnx, double dnz, double gox, double goz);
 
-/* Tuning: "prof" (1: record the band profile, alifmm_band_profile), "cdelta" (band width in units of dnx/vmax, default 0.5), "r0" (near-source band
+/* Tuning: "pair" (1, default: two workgroups per source when the chunk fits the device, results
+ * identical to the one-workgroup kernel), "prof" (1: record the band profile, alifmm_band_profile;
+ * uses the one-workgroup kernel), "cdelta" (band width in units of dnx/vmax, default 0.5), "r0" (near-source band
  * schedule radius in cells, default 40), "exact_r" (radius in cells of the exact heap-ordered
  * main-loop prefix for subgrid 1, 0..48, default 40), "batch" (sources per launch, default 256). */
 int alifmm_set_option(alifmm_ctx* ctx, const char* name, double value);
+/* Read an option, or "last_pair" (1 if the last alifmm_travel ran the two-workgroup kernel) and
+ * "n_cu" (compute units of the device). */
+int alifmm_get_option(alifmm_ctx* ctx, const char* name, double* value);
 
 /* Shape of a travel-time field for subgrid size sg: (sg*(nnz-1)+1, sg*(nnx-1)+1). */
 int alifmm_field_shape(alifmm_ctx* ctx, int subgrid, int* fnz, int* fnx);

@@ -273,3 +273,31 @@ def test_weld_example_end_to_end(golden, A):
     rx, ry = M.ray_path(15, 46)
     assert len(rx) == k and abs(rx[0] - sx[15] / 0.0002) < 1e-9
     assert abs(ry[0] - 0) < 1e-12 and abs(ry[-1] - 423) < 1e-12 and abs(rx[-1] - 250) < 1e-12
+
+
+def test_pair_kernel_identical_to_single_workgroup(ctx):
+    """Two workgroups per source (fmm_band_pair.hip) vs one (fmm_band.hip): bit-identical fields,
+    subgrid 1 on the C4 grid (sources across stripe boundaries and the grid corner) and subgrid 3
+    on the weld model."""
+    vt = W.default_table()
+    dnx = W.weldlike_dnx()
+    ctx.set_model(*W.weldlike_model(), vt, vt, dnx)
+    xs = dnx * np.array([0.0, 63.0, 64.0, 2047.0, 4095.0, 1000.0])
+    zs = dnx * np.array([0.0, 0.0, 100.0, 4095.0, 4095.0, 2000.0])
+    ctx.set_option("pair", 1)
+    A = ctx.travel(xs, zs)
+    assert ctx.get_option("last_pair") == 1.0
+    ctx.set_option("pair", 0)
+    Bf = ctx.travel(xs, zs)
+    assert ctx.get_option("last_pair") == 0.0
+    ctx.set_option("pair", 1)
+    assert np.array_equal(A, Bf), [float(np.max(np.abs(A[i] - Bf[i]))) for i in range(len(xs))]
+    del A, Bf
+    veln, velpn, vm, sd = W.weld_model()
+    ctx.set_model(veln, velpn, vm, sd, vt, vt, 2e-4)
+    scx, scz = W.weld_transducers()
+    A = ctx.travel(scx[[0, 46]], scz[[0, 46]], subgrid=3)
+    ctx.set_option("pair", 0)
+    Bf = ctx.travel(scx[[0, 46]], scz[[0, 46]], subgrid=3)
+    ctx.set_option("pair", 1)
+    assert np.array_equal(A, Bf)
