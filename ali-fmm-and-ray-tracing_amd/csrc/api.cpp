@@ -543,7 +543,7 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
   }
   HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
   bool paired = false;
-  if (ctx->pair && !ctx->prof && 16 * ((n + 7) / 8) <= ctx->n_cu) {
+  if (ctx->pair && 16 * ((n + 7) / 8) <= ctx->n_cu) {
     HIPCHK(hipMemsetAsync(a.px, 0, sizeof(af::PairX) * n, ctx->stream));
     paired = af_launch_band_pair(&P, ctx->stream) == hipSuccess;
     if (!paired) (void)hipGetLastError();  // not co-resident / model too large for LDS: single kernel
@@ -595,7 +595,7 @@ int alifmm_travel(alifmm_ctx* ctx, int subgrid, int nsrc, const double* scx, con
   HIPCHK(hipEventCreate(&t_begin));
   HIPCHK(hipEventRecord(t_begin, ctx->stream));
   // chunk: two workgroups per source need 2n CUs (pair mode), one per source otherwise
-  const int chunk = (ctx->pair && !ctx->prof && ctx->n_cu >= 16) ? std::min(ctx->batch, ctx->n_cu / 16 * 8) : ctx->batch;
+  const int chunk = (ctx->pair && ctx->n_cu >= 16) ? std::min(ctx->batch, ctx->n_cu / 16 * 8) : ctx->batch;
   for (int s0 = 0; s0 < nsrc; s0 += chunk) {
     int n = std::min(chunk, nsrc - s0);
     int rc;

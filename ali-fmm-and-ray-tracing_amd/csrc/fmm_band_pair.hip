@@ -51,6 +51,7 @@ struct Lds {
   int Dc[kDcap];  // deferred edge commits: packed cell
   int Ds[kDcap];  // deferred edge commits: new status (1 + slot) or 0 for "T only"
   alignas(16) int H[kHash];
+  int Px[kThreads];  // the partner's rim list, first kThreads entries (prefetched after X2)
   double tmin_g;
   int nA, nE, nF, hi, taken, nD, nAx, live_g, err_g, err;
 };
@@ -199,6 +200,19 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
   R.t0 = P.r0 * P.dnx / P.vmax;
   const GFieldSC1 F{T, S, nz, nx};
   long long steps = 0, myupd = 0;
+  // profile (P.prof): thread 0 of member 0; phases [P1+X1, P2+X2, claim, evaluate, fallback, commit],
+  // sub [X1 wait, X2 wait, deferred apply, -] — BandSrc::ph / sub, same layout as fmm_band.hip
+  const bool prof = P.prof && tid == 0 && me == 0;
+  long long ph[6] = {0, 0, 0, 0, 0, 0}, sub[4] = {0, 0, 0, 0}, ls[3] = {0, 0, 0}, lmax = 0;
+  long long tk = prof ? wall_clock64() : 0;
+#define AF_TICK(k)                 \
+  if (prof) {                      \
+    long long t_ = wall_clock64(); \
+    ph[k] += t_ - tk;              \
+    tk = t_;                       \
+  }
+#define AF_SUBT(k, t0)                   \
+  if (prof) sub[k] += wall_clock64() - (t0);
   while (true) {
     const int par = (int)(steps & 1);
     const int hi = sh->hi;
@@ -220,7 +234,10 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
       sh->nE = 0;
       sh->taken = 0;
     }
+    const long long tx1 = prof ? wall_clock64() : 0;
     if (!pair_barrier(&X->bar, gen, sh)) break;  // X1
+    AF_SUBT(0, tx1)
+    const long long tap = prof ? wall_clock64() : 0;
     if (tid == 0) {
       sh->tmin_g = fmin(sh->tmin_g, gld_sc1(&X->tmin[pt][par]));
       sh->live_g = (hi - sh->nF) + gld_sc1(&X->live[pt][par]);
@@ -234,6 +251,8 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
       if (sh->Ds[d] > 0) gst_sc1(S + f, sh->Ds[d]);
     }
     __syncthreads();
+    AF_SUBT(2, tap)
+    AF_TICK(0)
     if (sh->live_g <= 0 || sh->err_g) break;
     if (tid == 0) sh->nD = 0;
     tmin = sh->tmin_g;
@@ -264,9 +283,16 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
     }
     __syncthreads();
     if (tid == 0) gst_sc1(&X->nax[me][par], *nax);
+    const long long tx2 = prof ? wall_clock64() : 0;
     if (!pair_barrier(&X->bar, gen, sh)) break;  // X2
+    AF_SUBT(1, tx2)
+    AF_TICK(1)
     const int nA = min(sh->nA, capL);
-    const int nAp = gld_sc1(&X->nax[pt][par]);  // (uniform; every thread reads it)
+    // the partner's rim count and the head of its list in ONE round trip (entries past the count
+    // are stale and never read), staged in LDS
+    const int nAp = gld_sc1(&X->nax[pt][par]);
+    sh->Px[tid] = gld_sc1(AXp + tid);
+    __syncthreads();
     // ---- P3a: claim own neighbours of own accepted cells and of the partner's rim cells ----
     const int nItems = 4 * (nA + nAp);
     const bool use_hash = nItems <= kHashItems;
@@ -279,7 +305,8 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
         int c = -1;
         if (q < nItems) {
           const int a = q >> 2;
-          const int ac = a < nA ? AL.get(a) : gld_sc1(AXp + (a - nA));
+          const int ap = a - nA;
+          const int ac = a < nA ? AL.get(a) : ap < kThreads ? sh->Px[ap] : gld_sc1(AXp + ap);
           c = nb_cell(ac, q & 3, nz, nx);
           if (c >= 0 && !mine(pkx(c), me)) c = -1;
         }
@@ -326,6 +353,7 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
       }
     }
     __syncthreads();
+    AF_TICK(2)
     const int nE = min(sh->nE, capC);
     // ---- P3b: evaluate (cells whose stencil reaches the partner's columns: sc1 loads) ----
     for (int e = tid; e < nE; e += kThreads) {
@@ -338,6 +366,7 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
       VL.put(e, update(nb, M, cm, z, x, R.dnx, nz, nx));
       myupd++;
     }
+    AF_TICK(3)
     for (int e = tid; e < nE; e += kThreads) {
       if (VL.get(e) == -1.0) {
         const int r = EL.get(e);
@@ -347,6 +376,7 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
       }
     }
     __syncthreads();
+    AF_TICK(4)
     // ---- P4: commit own cells; edge cells deferred to after the next X1 ----
     const int nF = sh->nF;
     for (int e0 = wv * 64; e0 < nE; e0 += kThreads) {
@@ -389,8 +419,23 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
       sh->nF = max(0, nF - tk_);
       sh->hi = hi + max(0, tk_ - nF);
     }
+    if (prof) {
+      ls[0] += hi - sh->nF;
+      ls[1] += nA;
+      ls[2] += nE;
+      lmax = max(lmax, (long long)hi);
+    }
     steps++;
     __syncthreads();
+    AF_TICK(5)
+  }
+#undef AF_TICK
+#undef AF_SUBT
+  if (prof) {
+    for (int k = 0; k < 6; k++) B->ph[k] += ph[k];
+    for (int k = 0; k < 4; k++) B->sub[k] += sub[k];
+    for (int k = 0; k < 3; k++) B->lsum[k] += ls[k];
+    B->lmax = max(B->lmax, lmax);
   }
   for (int o = 32; o > 0; o >>= 1) myupd += __shfl_xor(myupd, o);
   if (lane == 0 && myupd) atomicAdd((unsigned long long*)&B->nupd, (unsigned long long)myupd);
