@@ -37,6 +37,30 @@ AF_DEV int wave_push(int* counter, bool pred, int cap, int* err) {
   return slot;
 }
 
+// wave_push onto two counters with the same predicate (both LDS atomics in flight together)
+AF_DEV void wave_push2(int* c1, int* c2, bool pred, int cap, int* err, int& s1, int& s2) {
+  s1 = s2 = -1;
+  unsigned long long m = __ballot(pred);
+  if (m == 0) return;
+  int lane = lane_id();
+  int leader = __ffsll((long long)m) - 1;
+  int b1 = 0, b2 = 0;
+  if (lane == leader) {
+    b1 = atomicAdd(c1, __popcll(m));
+    b2 = atomicAdd(c2, __popcll(m));
+  }
+  b1 = __shfl(b1, leader);
+  b2 = __shfl(b2, leader);
+  if (!pred) return;
+  int off = __popcll(m & ((1ull << lane) - 1ull));
+  s1 = b1 + off;
+  s2 = b2 + off;
+  if (s1 >= cap || s2 >= cap) {
+    *err = 2;
+    s1 = s2 = -1;
+  }
+}
+
 AF_DEV double wave_min(double v) {
   for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
   return v;

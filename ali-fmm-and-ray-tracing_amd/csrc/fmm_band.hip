@@ -22,6 +22,13 @@
 
 namespace af {
 
+#ifndef AF_CAS8
+#define AF_CAS8 1
+#endif
+#ifndef AF_UMAJOR
+#define AF_UMAJOR 1
+#endif
+
 #ifndef AF_THREADS
 #define AF_THREADS 512
 #endif
@@ -79,6 +86,20 @@ double fouds18_global(const GField& F, const DevModel& M, const CellMat& cm, int
 }
 
 AF_DEV unsigned hash_slot(int key) { return ((unsigned)key * 2654435761u) >> (32 - AF_HASH_LOG2); }
+// linear probing after a failed first CAS (prev = the occupant of slot h): returns c if this item
+// inserted c + 1 (it owns the cell), -1 if c was already present
+AF_DEV int claim_probe(int* H, unsigned h, int c, int prev, int* err) {
+  for (int probe = 0;; probe++) {
+    if (prev == c + 1) return -1;
+    if (probe >= kHash) {
+      *err = 5;
+      return -1;
+    }
+    h = (h + 1) & (kHash - 1);
+    prev = atomicCAS(&H[h], 0, c + 1);
+    if (prev == 0) return c;
+  }
+}
 
 // one band run over the main grid; returns steps.  T/S in global memory, sets and lists in LDS.
 // On entry the close set holds slots [0, sh->hi) with sh->nF free slots in sh->Fs.
@@ -143,15 +164,15 @@ AF_DEV long long band_run(const BandParams& P, BandLds* sh, BandSrc* B, const Ru
       const int e = e0 + lane;
       const double t = e < hi ? Lt.get(e) : INFINITY;
       const bool acc = t <= thr;
-      const int sa = wave_push(&sh->nA, acc, P.capL, &sh->err);
+      int sa, sf;
+      wave_push2(&sh->nA, &sh->nF, acc, P.capL, &sh->err, sa, sf);
       if (sa >= 0) {
         const int c = L.get(e);
         AL.put(sa, c);
         gst(S + pk_flat(c, nx), (int)kKnown);
         Lt.put(e, INFINITY);
+        FS.put(sf, e);
       }
-      const int sf = wave_push(&sh->nF, acc, P.capL, &sh->err);
-      if (sf >= 0) FS.put(sf, e);
     }
     __syncthreads();
     AF_TICK(1)
@@ -165,6 +186,25 @@ AF_DEV long long band_run(const BandParams& P, BandLds* sh, BandSrc* B, const Ru
     for (int q0 = wv * 64 * 8; q0 < nItems; q0 += kThreads * 8) {
       int r[8], s[8], o[8];
       if (prof) ts = wall_clock64();
+#if AF_CAS8
+      // first probe of all 8 items issued back to back (one LDS round trip), collisions after
+      unsigned hh[8];
+      int pv[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int q = q0 + u * 64 + lane;
+        r[u] = q < nItems ? nb_cell(AL.get(q >> 2), q & 3, nz, nx) : -1;
+        hh[u] = hash_slot(r[u]);
+      }
+      if (use_hash) {
+#pragma unroll
+        for (int u = 0; u < 8; u++) pv[u] = r[u] >= 0 ? atomicCAS(&sh->H[hh[u]], 0, r[u] + 1) : 0;
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          if (pv[u] != 0) r[u] = claim_probe(sh->H, hh[u], r[u], pv[u], &sh->err);
+        }
+      }
+#else
 #pragma unroll
       for (int u = 0; u < 8; u++) {
         const int q = q0 + u * 64 + lane;
@@ -184,6 +224,7 @@ AF_DEV long long band_run(const BandParams& P, BandLds* sh, BandSrc* B, const Ru
         }
         r[u] = c;
       }
+#endif
       AF_SUB(0)
 #pragma unroll
       for (int u = 0; u < 8; u++) {
@@ -193,6 +234,34 @@ AF_DEV long long band_run(const BandParams& P, BandLds* sh, BandSrc* B, const Ru
       }
       AF_SUB(1)
       // one list allocation per wave for all 8 items
+#if AF_UMAJOR
+      // u-major list order: consecutive entries are neighbours of consecutive accepted cells, so
+      // the lanes of an evaluating wave read overlapping stencils (fewer distinct cache lines)
+      unsigned long long bm[8];
+      int cnt = 0;
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        bm[u] = __ballot(s[u] != kKnown && o[u] < stamp);
+        cnt += __popcll(bm[u]);
+      }
+      int base = 0;
+      if (lane == 0 && cnt) base = atomicAdd(&sh->nE, cnt);
+      base = __shfl(base, 0);
+      const unsigned long long lt = (1ull << lane) - 1ull;
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        if ((bm[u] >> lane) & 1ull) {
+          const int pos = base + __popcll(bm[u] & lt);
+          if (pos < P.capC) {
+            EL.put(pos, r[u]);
+            EP.put(pos, s[u] > 0 ? s[u] - 1 : -1);
+          } else {
+            sh->err = 2;
+          }
+        }
+        base += __popcll(bm[u]);
+      }
+#else
       int nw = 0;
 #pragma unroll
       for (int u = 0; u < 8; u++) nw += (s[u] != kKnown && o[u] < stamp) ? 1 : 0;
@@ -213,6 +282,7 @@ AF_DEV long long band_run(const BandParams& P, BandLds* sh, BandSrc* B, const Ru
           base++;
         }
       }
+#endif
       AF_SUB(2)
     }
     __syncthreads();

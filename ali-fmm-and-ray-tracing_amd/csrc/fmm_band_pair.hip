@@ -23,9 +23,23 @@
 
 namespace af {
 
+#ifndef AF_UMAJOR
+#define AF_UMAJOR 1
+#endif
+
 namespace pair {
 
-constexpr int kThreads = 512;
+#ifndef AF_CAS8
+#define AF_CAS8 1
+#endif
+#ifndef AF_PAIR_PX
+#define AF_PAIR_PX 1
+#endif
+
+#ifndef AF_PAIR_THREADS
+#define AF_PAIR_THREADS 512
+#endif
+constexpr int kThreads = AF_PAIR_THREADS;
 constexpr int kWaves = kThreads / 64;
 constexpr int kStripeLog = 6;
 constexpr int kStripe = 1 << kStripeLog;
@@ -68,6 +82,20 @@ AF_DEV bool rim(int x) {
   return r == 0 || r == kStripe - 1;
 }
 AF_DEV unsigned hslot(int key) { return ((unsigned)key * 2654435761u) >> (32 - kHashLog); }
+// linear probing after a failed first CAS (prev = the occupant of slot h): returns c if this item
+// inserted c + 1 (it owns the cell), -1 if c was already present
+AF_DEV int claim_probe(int* H, unsigned h, int c, int prev, int* err) {
+  for (int probe = 0;; probe++) {
+    if (prev == c + 1) return -1;
+    if (probe >= kHash) {
+      *err = 5;
+      return -1;
+    }
+    h = (h + 1) & (kHash - 1);
+    prev = atomicCAS(&H[h], 0, c + 1);
+    if (prev == 0) return c;
+  }
+}
 
 // two-member barrier; false on timeout (the partner never arrived: both members then stop)
 AF_DEV bool pair_barrier(int* ctr, int& gen, Lds* sh) {
@@ -89,7 +117,7 @@ AF_DEV bool pair_barrier(int* ctr, int& gen, Lds* sh) {
   return sh->err != 7;
 }
 
-template <int MODE, bool LDSMAT>
+template <int MODE, bool LDSMAT, bool PROF>
 __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
   __shared__ Lds sh_;
   Lds* sh = &sh_;
@@ -202,7 +230,7 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
   long long steps = 0, myupd = 0;
   // profile (P.prof): thread 0 of member 0; phases [P1+X1, P2+X2, claim, evaluate, fallback, commit],
   // sub [X1 wait, X2 wait, deferred apply, -] — BandSrc::ph / sub, same layout as fmm_band.hip
-  const bool prof = P.prof && tid == 0 && me == 0;
+  const bool prof = PROF && tid == 0 && me == 0;
   long long ph[6] = {0, 0, 0, 0, 0, 0}, sub[4] = {0, 0, 0, 0}, ls[3] = {0, 0, 0}, lmax = 0;
   long long tk = prof ? wall_clock64() : 0;
 #define AF_TICK(k)                 \
@@ -231,6 +259,7 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
       gst_sc1(&X->err[me][par], sh->err);
       sh->tmin_g = t;
       sh->nA = 0;
+      sh->nAx = 0;
       sh->nE = 0;
       sh->taken = 0;
     }
@@ -260,24 +289,22 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
     if (R.t0 > 0 && tmin < R.t0) dl = R.delta * (tmin / R.t0);
     const double thr = tmin + dl;
     // ---- P2: accept own cells; rim cells go to the exchange list ----
-    int* nax = &sh->nAx;
-    if (tid == 0) *nax = 0;
-    __syncthreads();
+    int* nax = &sh->nAx;  // reset with nA in P1
     for (int e0 = wv * 64; e0 < hi; e0 += kThreads) {
       const int e = e0 + lane;
       const double t = e < hi ? Lt.get(e) : INFINITY;
       const bool acc = t <= thr;
       const int c = acc ? L.get(e) : 0;
-      const int sa = wave_push(&sh->nA, acc, capL, &sh->err);
+      int sa, sf;
+      wave_push2(&sh->nA, &sh->nF, acc, capL, &sh->err, sa, sf);
       if (sa >= 0) {
         AL.put(sa, c);
         const long f = (long)pkz(c) * nx + pkx(c);
         if (edge(pkx(c))) gst_sc1(S + f, (int)kKnown);
         else gst(S + f, (int)kKnown);
         Lt.put(e, INFINITY);
+        FS.put(sf, e);
       }
-      const int sf = wave_push(&sh->nF, acc, capL, &sh->err);
-      if (sf >= 0) FS.put(sf, e);
       const int sx = wave_push(nax, acc && rim(pkx(c)), capL, &sh->err);
       if (sx >= 0) gst_sc1(AXm + sx, c);
     }
@@ -291,14 +318,20 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
     // the partner's rim count and the head of its list in ONE round trip (entries past the count
     // are stale and never read), staged in LDS
     const int nAp = gld_sc1(&X->nax[pt][par]);
+#if AF_PAIR_PX
     sh->Px[tid] = gld_sc1(AXp + tid);
     __syncthreads();
+#endif
     // ---- P3a: claim own neighbours of own accepted cells and of the partner's rim cells ----
     const int nItems = 4 * (nA + nAp);
     const bool use_hash = nItems <= kHashItems;
     const int stamp = (int)steps;
     for (int q0 = wv * 64 * 8; q0 < nItems; q0 += kThreads * 8) {
       int r[8], s[8], o[8];
+#if AF_CAS8
+      // first probe of all 8 items issued back to back (one LDS round trip), collisions after
+      unsigned hh[8];
+      int pv[8];
 #pragma unroll
       for (int u = 0; u < 8; u++) {
         const int q = q0 + u * 64 + lane;
@@ -306,7 +339,30 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
         if (q < nItems) {
           const int a = q >> 2;
           const int ap = a - nA;
-          const int ac = a < nA ? AL.get(a) : ap < kThreads ? sh->Px[ap] : gld_sc1(AXp + ap);
+          const int ac = a < nA ? AL.get(a) : (AF_PAIR_PX && ap < kThreads) ? sh->Px[ap] : gld_sc1(AXp + ap);
+          c = nb_cell(ac, q & 3, nz, nx);
+          if (c >= 0 && !mine(pkx(c), me)) c = -1;
+        }
+        r[u] = c;
+        hh[u] = hslot(c);
+      }
+      if (use_hash) {
+#pragma unroll
+        for (int u = 0; u < 8; u++) pv[u] = r[u] >= 0 ? atomicCAS(&sh->H[hh[u]], 0, r[u] + 1) : 0;
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          if (pv[u] != 0) r[u] = claim_probe(sh->H, hh[u], r[u], pv[u], &sh->err);
+        }
+      }
+#else
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int q = q0 + u * 64 + lane;
+        int c = -1;
+        if (q < nItems) {
+          const int a = q >> 2;
+          const int ap = a - nA;
+          const int ac = a < nA ? AL.get(a) : (AF_PAIR_PX && ap < kThreads) ? sh->Px[ap] : gld_sc1(AXp + ap);
           c = nb_cell(ac, q & 3, nz, nx);
           if (c >= 0 && !mine(pkx(c), me)) c = -1;
         }
@@ -325,12 +381,41 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
         }
         r[u] = c;
       }
+#endif
 #pragma unroll
       for (int u = 0; u < 8; u++) {
         const long f = r[u] >= 0 ? (long)pkz(r[u]) * nx + pkx(r[u]) : 0;
         s[u] = r[u] >= 0 ? (edge(pkx(r[u])) ? gld_sc1(S + f) : gld(S + f)) : (int)kKnown;
         o[u] = (!use_hash && r[u] >= 0) ? gatomic_max(own + f, stamp) : -1;
       }
+#if AF_UMAJOR
+      // u-major list order: consecutive entries are neighbours of consecutive accepted cells, so
+      // the lanes of an evaluating wave read overlapping stencils (fewer distinct cache lines)
+      unsigned long long bm[8];
+      int cnt = 0;
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        bm[u] = __ballot(s[u] != kKnown && o[u] < stamp);
+        cnt += __popcll(bm[u]);
+      }
+      int base = 0;
+      if (lane == 0 && cnt) base = atomicAdd(&sh->nE, cnt);
+      base = __shfl(base, 0);
+      const unsigned long long lt = (1ull << lane) - 1ull;
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        if ((bm[u] >> lane) & 1ull) {
+          const int pos = base + __popcll(bm[u] & lt);
+          if (pos < capC) {
+            EL.put(pos, r[u]);
+            EP.put(pos, s[u] > 0 ? s[u] - 1 : -1);
+          } else {
+            sh->err = 2;
+          }
+        }
+        base += __popcll(bm[u]);
+      }
+#else
       int nw = 0;
 #pragma unroll
       for (int u = 0; u < 8; u++) nw += (s[u] != kKnown && o[u] < stamp) ? 1 : 0;
@@ -351,6 +436,7 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
           base++;
         }
       }
+#endif
     }
     __syncthreads();
     AF_TICK(2)
@@ -458,7 +544,9 @@ extern "C" hipError_t af_launch_band_pair(const af::BandParams* P, hipStream_t s
   const dim3 g(16 * ((P->nsrc + 7) / 8)), b(af::pair::kThreads);
   af::BandParams Pc = *P;
   void* args[] = {&Pc};
-  const void* fn = P->mode == 0 ? (const void*)af::pair::fmm_band_pair_kernel<0, true>
-                                : (const void*)af::pair::fmm_band_pair_kernel<1, true>;
+  const void* fn = P->mode == 0 ? (P->prof ? (const void*)af::pair::fmm_band_pair_kernel<0, true, true>
+                                            : (const void*)af::pair::fmm_band_pair_kernel<0, true, false>)
+                                : (P->prof ? (const void*)af::pair::fmm_band_pair_kernel<1, true, true>
+                                           : (const void*)af::pair::fmm_band_pair_kernel<1, true, false>);
   return hipLaunchCooperativeKernel(fn, g, b, args, 0, stream);
 }

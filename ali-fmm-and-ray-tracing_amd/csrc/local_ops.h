@@ -12,8 +12,11 @@
 
 namespace af {
 
+#ifndef AF_FOUDS_DEV
+#define AF_FOUDS_DEV AF_DEV
+#endif
 template <class F>
-AF_DEV double fouds18(const F& f, const DevModel& M, const CellMat& cm, long iz, long ix, double dnx, double dnz,
+AF_FOUDS_DEV double fouds18(const F& f, const DevModel& M, const CellMat& cm, long iz, long ix, double dnx, double dnz,
                       long nnx, long nnz) {
 #define N_(z, x) f.st((z), (x))
 #define T_(z, x) f.tt((z), (x))
