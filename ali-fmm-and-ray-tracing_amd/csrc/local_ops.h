@@ -8,6 +8,7 @@
 // is st >= 0 (alive or close), "known" in fouds18() is st == 0, exactly as in the reference.
 // Material is read only at the target cell (CellMat), as in the reference.
 #pragma once
+#include <type_traits>
 #include "device_common.h"
 
 namespace af {
@@ -360,129 +361,24 @@ AF_FOUDS_DEV double fouds18(const F& f, const DevModel& M, const CellMat& cm, lo
 #ifndef AF_UPD_IDX
 #define AF_UPD_IDX int
 #endif
-template <class F>
-AF_DEV double update(const F& f, const DevModel& M, const CellMat& cm, AF_UPD_IDX iz, AF_UPD_IDX ix, double dnx,
-                     AF_UPD_IDX nnz, AF_UPD_IDX nnx) {
+// update()'s triangular-stencil stage (:1146-1366) and its inputs/outputs, shared by the
+// reference-form square stage (update_ref) and the branch-free one for register neighbourhoods
+// (update_nb).  W holds the parameters of the one wavefront_angle_dist() call.
+template <class I>
+struct UpdW {
+    I x1, x2, x3, z1, z2, z3;
+    double y1, y2, y3;
+    bool have;
+};
+template <class F, class I>
+AF_DEV void upd_tri(const F& f, I iz, I ix, I nnz, I nnx, int& sno, double& min_diff, double& diff, UpdW<I>& w,
+                    double& wt, double& angle, double& dist) {
 #define N_(z, x) f.st((z), (x))
 #define T_(z, x) f.tt((z), (x))
-    int sp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (ix > 1) { if (N_(iz, ix - 2) >= 0) sp[3]++; }
-    if (ix > 0) {
-        if (N_(iz, ix - 1) >= 0) { sp[4]++; sp[7]++; }
-        if (iz > 0) { if (N_(iz - 1, ix - 1) >= 0) { sp[0]++; sp[3]++; sp[4]++; } }
-        if (iz < nnz - 1) { if (N_(iz + 1, ix - 1) >= 0) { sp[2]++; sp[3]++; sp[7]++; } }
-    }
-    if (ix < nnx - 2) { if (N_(iz, ix + 2) >= 0) sp[1]++; }
-    if (ix < nnx - 1) {
-        if (N_(iz, ix + 1) >= 0) { sp[5]++; sp[6]++; }
-        if (iz > 0) { if (N_(iz - 1, ix + 1) >= 0) { sp[0]++; sp[1]++; sp[5]++; } }
-        if (iz < nnz - 1) { if (N_(iz + 1, ix + 1) >= 0) { sp[1]++; sp[2]++; sp[6]++; } }
-    }
-    if (iz > 1) { if (N_(iz - 2, ix) >= 0) sp[0]++; }
-    if (iz > 0) { if (N_(iz - 1, ix) >= 0) { sp[4]++; sp[5]++; } }
-    if (iz < nnz - 2) { if (N_(iz + 2, ix) >= 0) sp[2]++; }
-    if (iz < nnz - 1) { if (N_(iz + 1, ix) >= 0) { sp[6]++; sp[7]++; } }
-
-    int sno = -1;
-    double min_diff = 1000000.0, diff;
-    if (sp[0] == 3) { diff = fabs(T_(iz - 1, ix - 1) - T_(iz - 1, ix + 1)); if (diff < min_diff) { sno = 0; min_diff = diff; } }
-    if (sp[1] == 3) { diff = fabs(T_(iz - 1, ix + 1) - T_(iz + 1, ix + 1)); if (diff < min_diff) { sno = 1; min_diff = diff; } }
-    if (sp[2] == 3) { diff = fabs(T_(iz + 1, ix - 1) - T_(iz + 1, ix + 1)); if (diff < min_diff) { sno = 2; min_diff = diff; } }
-    if (sp[3] == 3) { diff = fabs(T_(iz - 1, ix - 1) - T_(iz + 1, ix - 1)); if (diff < min_diff) { sno = 3; min_diff = diff; } }
-    if (sp[4] == 3) { diff = fabs(T_(iz, ix - 1) - T_(iz - 1, ix)); if (diff < min_diff) { sno = 4; min_diff = diff; } }
-    if (sp[5] == 3) { diff = fabs(T_(iz - 1, ix) - T_(iz, ix + 1)); if (diff < min_diff) { sno = 5; min_diff = diff; } }
-    if (sp[6] == 3) { diff = fabs(T_(iz + 1, ix) - T_(iz, ix + 1)); if (diff < min_diff) { sno = 6; min_diff = diff; } }
-    if (sp[7] == 3) { diff = fabs(T_(iz, ix - 1) - T_(iz + 1, ix)); if (diff < min_diff) { sno = 7; min_diff = diff; } }
-
-    double angle = 0.0, dist = -1.0, wt = 0.0;
-    /* wavefront_angle_dist is evaluated once, after stencil selection, on the parameters of the
-       stencil that the reference's last wavefront_angle_dist call would use (same result, one
-       inlined instance instead of 32: keeps the kernels free of register spills) */
-    bool have_w = false;
-    AF_UPD_IDX wx1 = 0, wx2 = 0, wx3 = 0, wz1 = 0, wz2 = 0, wz3 = 0;
-    double wy1 = 0, wy2 = 0, wy3 = 0;
 #define SETW(a1, a2, a3, b1, b2, b3, c1, c2, c3) \
-    do { wx1 = (a1); wx2 = (a2); wx3 = (a3); wz1 = (b1); wz2 = (b2); wz3 = (b3); \
-         wy1 = (c1); wy2 = (c2); wy3 = (c3); have_w = true; } while (0)
-    if (sno != -1) {
-        /* square stencils :1039-1143 (both nsts sub-branches of stencils 0-3 are identical) */
-        switch (sno) {
-        case 0:
-            if (T_(iz - 1, ix - 1) < T_(iz - 1, ix + 1)) {
-                SETW(ix, ix - 1, ix + 1, iz - 2, iz - 1, iz - 1, T_(iz - 2, ix), T_(iz - 1, ix - 1), T_(iz - 1, ix + 1));
-                wt = T_(iz - 1, ix - 1);
-            } else {
-                SETW(ix, ix + 1, ix - 1, iz - 2, iz - 1, iz - 1, T_(iz - 2, ix), T_(iz - 1, ix + 1), T_(iz - 1, ix - 1));
-                wt = T_(iz - 1, ix + 1);
-            }
-            break;
-        case 1:
-            if (T_(iz - 1, ix + 1) < T_(iz + 1, ix + 1)) {
-                SETW(ix + 2, ix + 1, ix + 1, iz, iz - 1, iz + 1, T_(iz, ix + 2), T_(iz - 1, ix + 1), T_(iz + 1, ix + 1));
-                wt = T_(iz - 1, ix + 1);
-            } else {
-                SETW(ix + 2, ix + 1, ix + 1, iz, iz + 1, iz - 1, T_(iz, ix + 2), T_(iz + 1, ix + 1), T_(iz - 1, ix + 1));
-                wt = T_(iz + 1, ix + 1);
-            }
-            break;
-        case 2:
-            if (T_(iz + 1, ix - 1) < T_(iz + 1, ix + 1)) {
-                SETW(ix, ix - 1, ix + 1, iz + 2, iz + 1, iz + 1, T_(iz + 2, ix), T_(iz + 1, ix - 1), T_(iz + 1, ix + 1));
-                wt = T_(iz + 1, ix - 1);
-            } else {
-                SETW(ix, ix + 1, ix - 1, iz + 2, iz + 1, iz + 1, T_(iz + 2, ix), T_(iz + 1, ix + 1), T_(iz + 1, ix - 1));
-                wt = T_(iz + 1, ix + 1);
-            }
-            break;
-        case 3:
-            if (T_(iz - 1, ix - 1) < T_(iz + 1, ix - 1)) {
-                SETW(ix - 2, ix - 1, ix - 1, iz, iz - 1, iz + 1, T_(iz, ix - 2), T_(iz - 1, ix - 1), T_(iz + 1, ix - 1));
-                wt = T_(iz - 1, ix - 1);
-            } else {
-                SETW(ix - 2, ix - 1, ix - 1, iz, iz + 1, iz - 1, T_(iz, ix - 2), T_(iz + 1, ix - 1), T_(iz - 1, ix - 1));
-                wt = T_(iz + 1, ix - 1);
-            }
-            break;
-        case 4:
-            if (T_(iz, ix - 1) < T_(iz - 1, ix)) {
-                SETW(ix - 1, ix - 1, ix, iz - 1, iz, iz - 1, T_(iz - 1, ix - 1), T_(iz, ix - 1), T_(iz - 1, ix));
-                wt = T_(iz, ix - 1);
-            } else {
-                SETW(ix - 1, ix, ix - 1, iz - 1, iz - 1, iz, T_(iz - 1, ix - 1), T_(iz - 1, ix), T_(iz, ix - 1));
-                wt = T_(iz - 1, ix);
-            }
-            break;
-        case 5:
-            if (T_(iz - 1, ix) < T_(iz, ix + 1)) {
-                SETW(ix + 1, ix, ix + 1, iz - 1, iz - 1, iz, T_(iz - 1, ix + 1), T_(iz - 1, ix), T_(iz, ix + 1));
-                wt = T_(iz - 1, ix);
-            } else {
-                SETW(ix + 1, ix + 1, ix, iz - 1, iz, iz - 1, T_(iz - 1, ix + 1), T_(iz, ix + 1), T_(iz - 1, ix));
-                wt = T_(iz, ix + 1);
-            }
-            break;
-        case 6:
-            if (T_(iz + 1, ix) < T_(iz, ix + 1)) {
-                SETW(ix + 1, ix, ix + 1, iz + 1, iz + 1, iz, T_(iz + 1, ix + 1), T_(iz + 1, ix), T_(iz, ix + 1));
-                wt = T_(iz + 1, ix);
-            } else {
-                SETW(ix + 1, ix + 1, ix, iz + 1, iz, iz + 1, T_(iz + 1, ix + 1), T_(iz, ix + 1), T_(iz + 1, ix));
-                wt = T_(iz, ix + 1);
-            }
-            break;
-        case 7:
-            if (T_(iz, ix - 1) < T_(iz + 1, ix)) {
-                SETW(ix - 1, ix - 1, ix, iz + 1, iz, iz + 1, T_(iz + 1, ix - 1), T_(iz, ix - 1), T_(iz + 1, ix));
-                wt = T_(iz, ix - 1);
-            } else {
-                SETW(ix - 1, ix, ix - 1, iz + 1, iz + 1, iz, T_(iz + 1, ix - 1), T_(iz + 1, ix), T_(iz, ix - 1));
-                wt = T_(iz + 1, ix);
-            }
-            break;
-        }
-    }
-
-    if (sno == -1 || ix == 0 || ix == nnx - 1 || iz == 0 || iz == nnz - 1) {
+    do { w.x1 = (a1); w.x2 = (a2); w.x3 = (a3); w.z1 = (b1); w.z2 = (b2); w.z3 = (b3); \
+         w.y1 = (c1); w.y2 = (c2); w.y3 = (c3); w.have = true; } while (0)
+    bool& have_w = w.have;
         /* triangular stencils :1146-1366 */
         int tp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         if (ix > 1) { if (N_(iz, ix - 2) >= 0) { tp[4]++; tp[7]++; } }
@@ -607,9 +503,16 @@ AF_DEV double update(const F& f, const DevModel& M, const CellMat& cm, AF_UPD_ID
             }
             sno += 8;
         }
-    }
-    if (have_w) wad(ix, iz, wx1, wx2, wx3, wz1, wz2, wz3, wy1, wy2, wy3, angle, dist);
 #undef SETW
+#undef N_
+#undef T_
+}
+
+// the phase velocity of the chosen stencil's wavefront direction and the result (:1368-1410)
+template <class I>
+AF_DEV double upd_finish(const DevModel& M, const CellMat& cm, I ix, I iz, const UpdW<I>& w, double wt,
+                         double angle, double dist, double dnx) {
+    if (w.have) wad(ix, iz, w.x1, w.x2, w.x3, w.z1, w.z2, w.z3, w.y1, w.y2, w.y3, angle, dist);
     if (dist != -1.0) {
         double effa = pymod(cm.veln - angle, 180);
         double velocity;
@@ -618,9 +521,222 @@ AF_DEV double update(const F& f, const DevModel& M, const CellMat& cm, AF_UPD_ID
         return wt + (dist * dnx / velocity);
     }
     return -1.0;
+}
+
+template <class F>
+AF_DEV double update_ref(const F& f, const DevModel& M, const CellMat& cm, AF_UPD_IDX iz, AF_UPD_IDX ix, double dnx,
+                     AF_UPD_IDX nnz, AF_UPD_IDX nnx) {
+#define N_(z, x) f.st((z), (x))
+#define T_(z, x) f.tt((z), (x))
+    int sp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (ix > 1) { if (N_(iz, ix - 2) >= 0) sp[3]++; }
+    if (ix > 0) {
+        if (N_(iz, ix - 1) >= 0) { sp[4]++; sp[7]++; }
+        if (iz > 0) { if (N_(iz - 1, ix - 1) >= 0) { sp[0]++; sp[3]++; sp[4]++; } }
+        if (iz < nnz - 1) { if (N_(iz + 1, ix - 1) >= 0) { sp[2]++; sp[3]++; sp[7]++; } }
+    }
+    if (ix < nnx - 2) { if (N_(iz, ix + 2) >= 0) sp[1]++; }
+    if (ix < nnx - 1) {
+        if (N_(iz, ix + 1) >= 0) { sp[5]++; sp[6]++; }
+        if (iz > 0) { if (N_(iz - 1, ix + 1) >= 0) { sp[0]++; sp[1]++; sp[5]++; } }
+        if (iz < nnz - 1) { if (N_(iz + 1, ix + 1) >= 0) { sp[1]++; sp[2]++; sp[6]++; } }
+    }
+    if (iz > 1) { if (N_(iz - 2, ix) >= 0) sp[0]++; }
+    if (iz > 0) { if (N_(iz - 1, ix) >= 0) { sp[4]++; sp[5]++; } }
+    if (iz < nnz - 2) { if (N_(iz + 2, ix) >= 0) sp[2]++; }
+    if (iz < nnz - 1) { if (N_(iz + 1, ix) >= 0) { sp[6]++; sp[7]++; } }
+
+    int sno = -1;
+    double min_diff = 1000000.0, diff;
+    if (sp[0] == 3) { diff = fabs(T_(iz - 1, ix - 1) - T_(iz - 1, ix + 1)); if (diff < min_diff) { sno = 0; min_diff = diff; } }
+    if (sp[1] == 3) { diff = fabs(T_(iz - 1, ix + 1) - T_(iz + 1, ix + 1)); if (diff < min_diff) { sno = 1; min_diff = diff; } }
+    if (sp[2] == 3) { diff = fabs(T_(iz + 1, ix - 1) - T_(iz + 1, ix + 1)); if (diff < min_diff) { sno = 2; min_diff = diff; } }
+    if (sp[3] == 3) { diff = fabs(T_(iz - 1, ix - 1) - T_(iz + 1, ix - 1)); if (diff < min_diff) { sno = 3; min_diff = diff; } }
+    if (sp[4] == 3) { diff = fabs(T_(iz, ix - 1) - T_(iz - 1, ix)); if (diff < min_diff) { sno = 4; min_diff = diff; } }
+    if (sp[5] == 3) { diff = fabs(T_(iz - 1, ix) - T_(iz, ix + 1)); if (diff < min_diff) { sno = 5; min_diff = diff; } }
+    if (sp[6] == 3) { diff = fabs(T_(iz + 1, ix) - T_(iz, ix + 1)); if (diff < min_diff) { sno = 6; min_diff = diff; } }
+    if (sp[7] == 3) { diff = fabs(T_(iz, ix - 1) - T_(iz + 1, ix)); if (diff < min_diff) { sno = 7; min_diff = diff; } }
+
+    double angle = 0.0, dist = -1.0, wt = 0.0;
+    /* wavefront_angle_dist is evaluated once, after stencil selection, on the parameters of the
+       stencil that the reference's last wavefront_angle_dist call would use (same result, one
+       inlined instance instead of 32: keeps the kernels free of register spills) */
+    bool have_w = false;
+    AF_UPD_IDX wx1 = 0, wx2 = 0, wx3 = 0, wz1 = 0, wz2 = 0, wz3 = 0;
+    double wy1 = 0, wy2 = 0, wy3 = 0;
+#define SETW(a1, a2, a3, b1, b2, b3, c1, c2, c3) \
+    do { wx1 = (a1); wx2 = (a2); wx3 = (a3); wz1 = (b1); wz2 = (b2); wz3 = (b3); \
+         wy1 = (c1); wy2 = (c2); wy3 = (c3); have_w = true; } while (0)
+    if (sno != -1) {
+        /* square stencils :1039-1143 (both nsts sub-branches of stencils 0-3 are identical) */
+        switch (sno) {
+        case 0:
+            if (T_(iz - 1, ix - 1) < T_(iz - 1, ix + 1)) {
+                SETW(ix, ix - 1, ix + 1, iz - 2, iz - 1, iz - 1, T_(iz - 2, ix), T_(iz - 1, ix - 1), T_(iz - 1, ix + 1));
+                wt = T_(iz - 1, ix - 1);
+            } else {
+                SETW(ix, ix + 1, ix - 1, iz - 2, iz - 1, iz - 1, T_(iz - 2, ix), T_(iz - 1, ix + 1), T_(iz - 1, ix - 1));
+                wt = T_(iz - 1, ix + 1);
+            }
+            break;
+        case 1:
+            if (T_(iz - 1, ix + 1) < T_(iz + 1, ix + 1)) {
+                SETW(ix + 2, ix + 1, ix + 1, iz, iz - 1, iz + 1, T_(iz, ix + 2), T_(iz - 1, ix + 1), T_(iz + 1, ix + 1));
+                wt = T_(iz - 1, ix + 1);
+            } else {
+                SETW(ix + 2, ix + 1, ix + 1, iz, iz + 1, iz - 1, T_(iz, ix + 2), T_(iz + 1, ix + 1), T_(iz - 1, ix + 1));
+                wt = T_(iz + 1, ix + 1);
+            }
+            break;
+        case 2:
+            if (T_(iz + 1, ix - 1) < T_(iz + 1, ix + 1)) {
+                SETW(ix, ix - 1, ix + 1, iz + 2, iz + 1, iz + 1, T_(iz + 2, ix), T_(iz + 1, ix - 1), T_(iz + 1, ix + 1));
+                wt = T_(iz + 1, ix - 1);
+            } else {
+                SETW(ix, ix + 1, ix - 1, iz + 2, iz + 1, iz + 1, T_(iz + 2, ix), T_(iz + 1, ix + 1), T_(iz + 1, ix - 1));
+                wt = T_(iz + 1, ix + 1);
+            }
+            break;
+        case 3:
+            if (T_(iz - 1, ix - 1) < T_(iz + 1, ix - 1)) {
+                SETW(ix - 2, ix - 1, ix - 1, iz, iz - 1, iz + 1, T_(iz, ix - 2), T_(iz - 1, ix - 1), T_(iz + 1, ix - 1));
+                wt = T_(iz - 1, ix - 1);
+            } else {
+                SETW(ix - 2, ix - 1, ix - 1, iz, iz + 1, iz - 1, T_(iz, ix - 2), T_(iz + 1, ix - 1), T_(iz - 1, ix - 1));
+                wt = T_(iz + 1, ix - 1);
+            }
+            break;
+        case 4:
+            if (T_(iz, ix - 1) < T_(iz - 1, ix)) {
+                SETW(ix - 1, ix - 1, ix, iz - 1, iz, iz - 1, T_(iz - 1, ix - 1), T_(iz, ix - 1), T_(iz - 1, ix));
+                wt = T_(iz, ix - 1);
+            } else {
+                SETW(ix - 1, ix, ix - 1, iz - 1, iz - 1, iz, T_(iz - 1, ix - 1), T_(iz - 1, ix), T_(iz, ix - 1));
+                wt = T_(iz - 1, ix);
+            }
+            break;
+        case 5:
+            if (T_(iz - 1, ix) < T_(iz, ix + 1)) {
+                SETW(ix + 1, ix, ix + 1, iz - 1, iz - 1, iz, T_(iz - 1, ix + 1), T_(iz - 1, ix), T_(iz, ix + 1));
+                wt = T_(iz - 1, ix);
+            } else {
+                SETW(ix + 1, ix + 1, ix, iz - 1, iz, iz - 1, T_(iz - 1, ix + 1), T_(iz, ix + 1), T_(iz - 1, ix));
+                wt = T_(iz, ix + 1);
+            }
+            break;
+        case 6:
+            if (T_(iz + 1, ix) < T_(iz, ix + 1)) {
+                SETW(ix + 1, ix, ix + 1, iz + 1, iz + 1, iz, T_(iz + 1, ix + 1), T_(iz + 1, ix), T_(iz, ix + 1));
+                wt = T_(iz + 1, ix);
+            } else {
+                SETW(ix + 1, ix + 1, ix, iz + 1, iz, iz + 1, T_(iz + 1, ix + 1), T_(iz, ix + 1), T_(iz + 1, ix));
+                wt = T_(iz, ix + 1);
+            }
+            break;
+        case 7:
+            if (T_(iz, ix - 1) < T_(iz + 1, ix)) {
+                SETW(ix - 1, ix - 1, ix, iz + 1, iz, iz + 1, T_(iz + 1, ix - 1), T_(iz, ix - 1), T_(iz + 1, ix));
+                wt = T_(iz, ix - 1);
+            } else {
+                SETW(ix - 1, ix, ix - 1, iz + 1, iz + 1, iz, T_(iz + 1, ix - 1), T_(iz + 1, ix), T_(iz, ix - 1));
+                wt = T_(iz + 1, ix);
+            }
+            break;
+        }
+    }
+
+    if (sno == -1 || ix == 0 || ix == nnx - 1 || iz == 0 || iz == nnz - 1) {
+        UpdW<AF_UPD_IDX> w{wx1, wx2, wx3, wz1, wz2, wz3, wy1, wy2, wy3, have_w};
+        upd_tri(f, iz, ix, nnz, nnx, sno, min_diff, diff, w, wt, angle, dist);
+#undef SETW
+        return upd_finish(M, cm, ix, iz, w, wt, angle, dist, dnx);
+    }
+    UpdW<AF_UPD_IDX> w{wx1, wx2, wx3, wz1, wz2, wz3, wy1, wy2, wy3, have_w};
+    return upd_finish(M, cm, ix, iz, w, wt, angle, dist, dnx);
 #undef N_
 #undef T_
 }
 
+
+
+// update() on a register neighbourhood (NbField / NbFieldT: t0..t11 and the validity mask vm,
+// slots as NbField::slot): the same square-stencil stage as update_ref without branches — the
+// sp[k] == 3 tests become mask tests (the bounds checks folded into the mask), the first-minimum
+// selection keeps the reference's order and strict '<', and the chosen stencil's wavefront
+// parameters are carried through the selection instead of a 16-way switch, so a wavefront does
+// not serialise over its lanes' stencil cases.  The triangular stage and the velocity are shared
+// with update_ref.  Bit-identical to update_ref (tools/micro/update_bench checksums, GPU tests).
+template <class F>
+AF_DEV double update_nb(const F& f, const DevModel& M, const CellMat& cm, AF_UPD_IDX iz, AF_UPD_IDX ix, double dnx,
+                        AF_UPD_IDX nnz, AF_UPD_IDX nnx) {
+    using I = AF_UPD_IDX;
+    const bool l1 = ix > 0, l2 = ix > 1, r1 = ix < nnx - 1, r2 = ix < nnx - 2;
+    const bool u1 = iz > 0, u2 = iz > 1, d1 = iz < nnz - 1, d2 = iz < nnz - 2;
+    const unsigned inb = (l2 ? 1u : 0u) | (l1 ? 2u : 0u) | (r1 ? 4u : 0u) | (r2 ? 8u : 0u) | (u2 ? 16u : 0u) |
+                         (u1 ? 32u : 0u) | (d1 ? 64u : 0u) | (d2 ? 128u : 0u) | (l1 && u1 ? 256u : 0u) |
+                         (r1 && u1 ? 512u : 0u) | (l1 && d1 ? 1024u : 0u) | (r1 && d1 ? 2048u : 0u);
+    const unsigned em = f.vm & inb;
+    const double t[12] = {f.t0, f.t1, f.t2, f.t3, f.t4, f.t5, f.t6, f.t7, f.t8, f.t9, f.t10, f.t11};
+    // square stencil k: apex, a, b slots; diff = |T_a - T_b|; the wavefront points are (apex, a, b)
+    // when T_a < T_b, else (apex, b, a) (:1039-1143)
+    constexpr int AP[8] = {4, 3, 7, 0, 8, 9, 11, 10};
+    constexpr int SA[8] = {8, 9, 10, 8, 1, 5, 6, 1};
+    constexpr int SB[8] = {9, 11, 11, 10, 5, 2, 2, 6};
+    // slot -> (dz + 2) * 8 + (dx + 2)
+    constexpr int OFF[12] = {16, 17, 19, 20, 2, 10, 26, 34, 9, 11, 25, 27};
+    int sno = -1, code = 0;
+    double min_diff = 1000000.0, diff = 0.0, yap = 0.0, ya = 0.0, yb = 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const unsigned msk = (1u << AP[k]) | (1u << SA[k]) | (1u << SB[k]);
+        const double d = fabs(t[SA[k]] - t[SB[k]]);
+        if ((em & msk) == msk && d < min_diff) {
+            sno = k;
+            min_diff = d;
+            yap = t[AP[k]];
+            ya = t[SA[k]];
+            yb = t[SB[k]];
+            code = OFF[AP[k]] | (OFF[SA[k]] << 6) | (OFF[SB[k]] << 12);
+        }
+    }
+    UpdW<I> w{0, 0, 0, 0, 0, 0, 0.0, 0.0, 0.0, false};
+    double wt = 0.0, angle = 0.0, dist = -1.0;
+    if (sno >= 0) {
+        const bool lo = ya < yb;
+        const int pa = (code >> 6) & 63, pb = (code >> 12) & 63;
+        const int p1 = code & 63, p2 = lo ? pa : pb, p3 = lo ? pb : pa;
+        w.x1 = ix + (p1 & 7) - 2;
+        w.z1 = iz + (p1 >> 3) - 2;
+        w.x2 = ix + (p2 & 7) - 2;
+        w.z2 = iz + (p2 >> 3) - 2;
+        w.x3 = ix + (p3 & 7) - 2;
+        w.z3 = iz + (p3 >> 3) - 2;
+        w.y1 = yap;
+        w.y2 = lo ? ya : yb;
+        w.y3 = lo ? yb : ya;
+        w.have = true;
+        wt = w.y2;
+    }
+    if (sno == -1 || ix == 0 || ix == nnx - 1 || iz == 0 || iz == nnz - 1)
+        upd_tri(f, iz, ix, nnz, nnx, sno, min_diff, diff, w, wt, angle, dist);
+    return upd_finish(M, cm, ix, iz, w, wt, angle, dist, dnx);
+}
+
+#ifndef AF_UPD_LEAN
+#define AF_UPD_LEAN 1
+#endif
+template <class F, class = void>
+struct upd_regs : std::false_type {};
+template <class F>
+struct upd_regs<F, std::void_t<decltype(&F::t11)>> : std::true_type {};
+
+// update() (Anis_TTF_rays.py:904-1410): the branch-free form on register neighbourhoods, the
+// reference form on every other field accessor
+template <class F>
+AF_DEV double update(const F& f, const DevModel& M, const CellMat& cm, AF_UPD_IDX iz, AF_UPD_IDX ix, double dnx,
+                     AF_UPD_IDX nnz, AF_UPD_IDX nnx) {
+    if constexpr (AF_UPD_LEAN && upd_regs<F>::value) return update_nb(f, M, cm, iz, ix, dnx, nnz, nnx);
+    else return update_ref(f, M, cm, iz, ix, dnx, nnz, nnx);
+}
 
 }  // namespace af
