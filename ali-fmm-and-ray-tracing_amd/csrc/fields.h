@@ -90,60 +90,25 @@ struct NbFieldT {
     return k == 0 ? t0 : k == 1 ? t1 : k == 2 ? t2 : k == 3 ? t3 : k == 4 ? t4 : k == 5 ? t5 : k == 6 ? t6
          : k == 7 ? t7 : k == 8 ? t8 : k == 9 ? t9 : k == 10 ? t10 : t11;
   }
-  // 8 loads: rows z-2 and z+2 one double each; rows z-1, z+1 (x-1, x) as one 16-byte load plus
-  // (x+1); row z (x-2, x-1) and (x+1, x+2) as 16-byte loads.  Addresses are clamped into the
-  // grid; values at out-of-grid columns are never read by update() (it bounds-checks first).
-  AF_DEV void load(const double* T, int nz, int nx, int z, int x) {
-    iz = z;
-    ix = x;
-    const int n = nz * nx;
-    const int p = z * nx + x;
-    auto cl = [n](int c, int w) { return c < 0 ? 0 : c > n - w ? n - w : c; };
-    auto ld2 = [&](int c, double& a, double& b) {
-      if (c >= 0 && c <= n - 2) {
-        double v[2];
-        __builtin_memcpy(v, (const AF_GLOBAL char*)(T + c), 16);
-        a = v[0];
-        b = v[1];
-      } else {  // grid corners: element-wise, so clamping never shifts a value into a valid slot
-        a = gld(T + cl(c, 1));
-        b = gld(T + cl(c + 1, 1));
-      }
-    };
-    // slots: 0 (0,-2) 1 (0,-1) 2 (0,+1) 3 (0,+2) 4 (-2,0) 5 (-1,0) 6 (+1,0) 7 (+2,0)
-    //        8 (-1,-1) 9 (-1,+1) 10 (+1,-1) 11 (+1,+1)
-    double t[12];
-    ld2(p - 2, t[0], t[1]);
-    ld2(p + 1, t[2], t[3]);
-    ld2(p - nx - 1, t[8], t[5]);
-    t[9] = gld(T + cl(p - nx + 1, 1));
-    ld2(p + nx - 1, t[10], t[6]);
-    t[11] = gld(T + cl(p + nx + 1, 1));
-    t[4] = gld(T + cl(p - 2 * nx, 1));
-    t[7] = gld(T + cl(p + 2 * nx, 1));
-    const int dz[12] = {0, 0, 0, 0, -2, -1, 1, 2, -1, -1, 1, 1};
-    unsigned m = 0;
-#pragma unroll
-    for (int k = 0; k < 12; k++)
-      if (z + dz[k] < nz && t[k] == t[k]) m |= 1u << k;
-    vm = m;
-    t0 = t[0]; t1 = t[1]; t2 = t[2]; t3 = t[3]; t4 = t[4]; t5 = t[5];
-    t6 = t[6]; t7 = t[7]; t8 = t[8]; t9 = t[9]; t10 = t[10]; t11 = t[11];
-  }
-  // As load(), with 12 sc1 loads (cells another workgroup of the launch writes)
-  AF_DEV void load_sc1(const double* T, int nz, int nx, int z, int x) {
+  // 12 independent 8-byte loads at addresses clamped into the grid (no branches: a wavefront
+  // issues them back to back); values at out-of-grid positions are never read by update() (it
+  // bounds-checks first).  SC1: L1-bypassing loads, for cells another workgroup writes.
+  template <bool SC1>
+  AF_DEV void load_t(const double* T, int nz, int nx, int z, int x) {
     iz = z;
     ix = x;
     const int n = nz * nx;
     const int dz[12] = {0, 0, 0, 0, -2, -1, 1, 2, -1, -1, 1, 1};
     const int dx[12] = {-2, -1, 1, 2, 0, 0, 0, 0, -1, 1, -1, 1};
+    const int p = z * nx + x;
     double t[12];
-    unsigned m = 0;
 #pragma unroll
     for (int k = 0; k < 12; k++) {
-      const int c = (z + dz[k]) * nx + (x + dx[k]);
-      t[k] = gld_sc1(T + (c < 0 ? 0 : c >= n ? n - 1 : c));
+      const int c = p + dz[k] * nx + dx[k];
+      const double* a = T + (c < 0 ? 0 : c >= n ? n - 1 : c);
+      t[k] = SC1 ? gld_sc1(a) : gld(a);
     }
+    unsigned m = 0;
 #pragma unroll
     for (int k = 0; k < 12; k++)
       if (z + dz[k] < nz && t[k] == t[k]) m |= 1u << k;
@@ -151,6 +116,9 @@ struct NbFieldT {
     t0 = t[0]; t1 = t[1]; t2 = t[2]; t3 = t[3]; t4 = t[4]; t5 = t[5];
     t6 = t[6]; t7 = t[7]; t8 = t[8]; t9 = t[9]; t10 = t[10]; t11 = t[11];
   }
+  AF_DEV void load(const double* T, int nz, int nx, int z, int x) { load_t<false>(T, nz, nx, z, x); }
+  // As load(), with sc1 loads (cells another workgroup of the launch writes)
+  AF_DEV void load_sc1(const double* T, int nz, int nx, int z, int x) { load_t<true>(T, nz, nx, z, x); }
   // From a status-coded grid in LDS (the init kernel's stage grids / prefix window): validity =
   // inside rows [z0, z1] and columns [x0, x1] (else never-relaxed: nsts -1) and status >= 0;
   // the 24 LDS reads are issued together instead of as update()'s chain of dependent reads.

@@ -310,9 +310,9 @@ AF_DEV long long band_run(const BandParams& P, BandLds* sh, BandSrc* B, const Ru
       const int r = EL.get(e);
       const int z = pkz(r), x = pkx(r);
       if (prof) ts = wall_clock64();
-      const CellMat cm = band_mat<LDSMAT>(M, sh->mat, sh->stab, R.mv, z, x);
-      NbFieldT nb;
+      NbFieldT nb;  // stencil loads first, then the material id: one memory round trip
       nb.load(T, nz, nx, z, x);
+      const CellMat cm = band_mat<LDSMAT>(M, sh->mat, sh->stab, R.mv, z, x);
       AF_SUB(3)
       VL.put(e, update(nb, M, cm, z, x, R.dnx, nz, nx));
       myupd++;

@@ -29,6 +29,9 @@ namespace af {
 
 namespace pair {
 
+#ifndef AF_PAIR_ALLSC1
+#define AF_PAIR_ALLSC1 0
+#endif
 #ifndef AF_CAS8
 #define AF_CAS8 1
 #endif
@@ -445,10 +448,14 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
     for (int e = tid; e < nE; e += kThreads) {
       const int r = EL.get(e);
       const int z = pkz(r), x = pkx(r);
-      const CellMat cm = band_mat<LDSMAT>(M, sh->mat, sh->stab, R.mv, z, x);
-      NbFieldT nb;
+      NbFieldT nb;  // stencil loads first, then the material id: one memory round trip
+#if AF_PAIR_ALLSC1
+      nb.load_sc1(T, nz, nx, z, x);
+#else
       if (edge(x)) nb.load_sc1(T, nz, nx, z, x);
       else nb.load(T, nz, nx, z, x);
+#endif
+      const CellMat cm = band_mat<LDSMAT>(M, sh->mat, sh->stab, R.mv, z, x);
       VL.put(e, update(nb, M, cm, z, x, R.dnx, nz, nx));
       myupd++;
     }
