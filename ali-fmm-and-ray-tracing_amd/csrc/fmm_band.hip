@@ -32,9 +32,6 @@ namespace af {
 #ifndef AF_THREADS
 #define AF_THREADS 512
 #endif
-#ifndef AF_EVAL2
-#define AF_EVAL2 0
-#endif
 #ifndef AF_FOUDS_NOINLINE
 #define AF_FOUDS_NOINLINE 0
 #endif
@@ -289,23 +286,6 @@ AF_DEV long long band_run(const BandParams& P, BandLds* sh, BandSrc* B, const Ru
     AF_TICK(2)
     const int nE = min(sh->nE, P.capC);
     // ---- phase 3b: evaluate ----
-#if AF_EVAL2
-    // two cells per lane per round trip
-    for (int e0 = tid; e0 < nE; e0 += 2 * kThreads) {
-      const int e1 = e0 + kThreads;
-      const bool has1 = e1 < nE;
-      const int r0 = EL.get(e0), r1 = has1 ? EL.get(e1) : r0;
-      const int z0 = pkz(r0), x0 = pkx(r0), z1 = pkz(r1), x1 = pkx(r1);
-      const CellMat m0 = band_mat<LDSMAT>(M, sh->mat, sh->stab, R.mv, z0, x0);
-      const CellMat m1 = band_mat<LDSMAT>(M, sh->mat, sh->stab, R.mv, z1, x1);
-      NbFieldT n0, n1;
-      n0.load(T, nz, nx, z0, x0);
-      n1.load(T, nz, nx, z1, x1);
-      VL.put(e0, update(n0, M, m0, z0, x0, R.dnx, nz, nx));
-      if (has1) VL.put(e1, update(n1, M, m1, z1, x1, R.dnx, nz, nx));
-      myupd += has1 ? 2 : 1;
-    }
-#else
     for (int e = tid; e < nE; e += kThreads) {
       const int r = EL.get(e);
       const int z = pkz(r), x = pkx(r);
@@ -317,7 +297,6 @@ AF_DEV long long band_run(const BandParams& P, BandLds* sh, BandSrc* B, const Ru
       VL.put(e, update(nb, M, cm, z, x, R.dnx, nz, nx));
       myupd++;
     }
-#endif
     AF_TICK(3)
     // fouds18_A() fallback (update() found no usable stencil): a loop of its own, so its live
     // ranges never overlap update()'s
