@@ -22,12 +22,6 @@
 
 namespace af {
 
-#ifndef AF_CAS8
-#define AF_CAS8 1
-#endif
-#ifndef AF_UMAJOR
-#define AF_UMAJOR 1
-#endif
 
 #ifndef AF_THREADS
 #define AF_THREADS 512
@@ -183,7 +177,6 @@ AF_DEV long long band_run(const BandParams& P, BandLds* sh, BandSrc* B, const Ru
     for (int q0 = wv * 64 * 8; q0 < nItems; q0 += kThreads * 8) {
       int r[8], s[8], o[8];
       if (prof) ts = wall_clock64();
-#if AF_CAS8
       // first probe of all 8 items issued back to back (one LDS round trip), collisions after
       unsigned hh[8];
       int pv[8];
@@ -201,27 +194,6 @@ AF_DEV long long band_run(const BandParams& P, BandLds* sh, BandSrc* B, const Ru
           if (pv[u] != 0) r[u] = claim_probe(sh->H, hh[u], r[u], pv[u], &sh->err);
         }
       }
-#else
-#pragma unroll
-      for (int u = 0; u < 8; u++) {
-        const int q = q0 + u * 64 + lane;
-        int c = q < nItems ? nb_cell(AL.get(q >> 2), q & 3, nz, nx) : -1;
-        if (use_hash && c >= 0) {  // insert c + 1; the inserting item owns the cell
-          unsigned h = hash_slot(c);
-          for (int probe = 0;; probe++) {
-            const int prev = atomicCAS(&sh->H[h], 0, c + 1);
-            if (prev == 0) break;
-            if (prev == c + 1 || probe >= kHash) {
-              if (probe >= kHash) sh->err = 5;
-              c = -1;
-              break;
-            }
-            h = (h + 1) & (kHash - 1);
-          }
-        }
-        r[u] = c;
-      }
-#endif
       AF_SUB(0)
 #pragma unroll
       for (int u = 0; u < 8; u++) {
@@ -231,7 +203,6 @@ AF_DEV long long band_run(const BandParams& P, BandLds* sh, BandSrc* B, const Ru
       }
       AF_SUB(1)
       // one list allocation per wave for all 8 items
-#if AF_UMAJOR
       // u-major list order: consecutive entries are neighbours of consecutive accepted cells, so
       // the lanes of an evaluating wave read overlapping stencils (fewer distinct cache lines)
       unsigned long long bm[8];
@@ -258,28 +229,6 @@ AF_DEV long long band_run(const BandParams& P, BandLds* sh, BandSrc* B, const Ru
         }
         base += __popcll(bm[u]);
       }
-#else
-      int nw = 0;
-#pragma unroll
-      for (int u = 0; u < 8; u++) nw += (s[u] != kKnown && o[u] < stamp) ? 1 : 0;
-      int tot;
-      const int off = wave_excl_scan(nw, tot);
-      int base = 0;
-      if (lane == 0 && tot) base = atomicAdd(&sh->nE, tot);
-      base = __shfl(base, 0) + off;
-#pragma unroll
-      for (int u = 0; u < 8; u++) {
-        if (s[u] != kKnown && o[u] < stamp) {
-          if (base < P.capC) {
-            EL.put(base, r[u]);
-            EP.put(base, s[u] > 0 ? s[u] - 1 : -1);
-          } else {
-            sh->err = 2;
-          }
-          base++;
-        }
-      }
-#endif
       AF_SUB(2)
     }
     __syncthreads();

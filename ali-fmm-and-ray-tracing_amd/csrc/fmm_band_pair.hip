@@ -23,17 +23,11 @@
 
 namespace af {
 
-#ifndef AF_UMAJOR
-#define AF_UMAJOR 1
-#endif
 
 namespace pair {
 
 #ifndef AF_PAIR_ALLSC1
 #define AF_PAIR_ALLSC1 0
-#endif
-#ifndef AF_CAS8
-#define AF_CAS8 1
 #endif
 #ifndef AF_PAIR_PX
 #define AF_PAIR_PX 1
@@ -232,7 +226,7 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
   const GFieldSC1 F{T, S, nz, nx};
   long long steps = 0, myupd = 0;
   // profile (P.prof): thread 0 of member 0; phases [P1+X1, P2+X2, claim, evaluate, fallback, commit],
-  // sub [X1 wait, X2 wait, deferred apply, -] — BandSrc::ph / sub, same layout as fmm_band.hip
+  // sub [X1 wait, X2 wait, claim dedupe (waited), claim status loads] — BandSrc::ph / sub, same layout as fmm_band.hip
   const bool prof = PROF && tid == 0 && me == 0;
   long long ph[6] = {0, 0, 0, 0, 0, 0}, sub[4] = {0, 0, 0, 0}, ls[3] = {0, 0, 0}, lmax = 0;
   long long tk = prof ? wall_clock64() : 0;
@@ -283,7 +277,6 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
       if (sh->Ds[d] > 0) gst_sc1(S + f, sh->Ds[d]);
     }
     __syncthreads();
-    AF_SUBT(2, tap)
     AF_TICK(0)
     if (sh->live_g <= 0 || sh->err_g) break;
     if (tid == 0) sh->nD = 0;
@@ -331,7 +324,7 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
     const int stamp = (int)steps;
     for (int q0 = wv * 64 * 8; q0 < nItems; q0 += kThreads * 8) {
       int r[8], s[8], o[8];
-#if AF_CAS8
+      const long long tdd = prof ? wall_clock64() : 0;
       // first probe of all 8 items issued back to back (one LDS round trip), collisions after
       unsigned hh[8];
       int pv[8];
@@ -357,41 +350,15 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
           if (pv[u] != 0) r[u] = claim_probe(sh->H, hh[u], r[u], pv[u], &sh->err);
         }
       }
-#else
-#pragma unroll
-      for (int u = 0; u < 8; u++) {
-        const int q = q0 + u * 64 + lane;
-        int c = -1;
-        if (q < nItems) {
-          const int a = q >> 2;
-          const int ap = a - nA;
-          const int ac = a < nA ? AL.get(a) : (AF_PAIR_PX && ap < kThreads) ? sh->Px[ap] : gld_sc1(AXp + ap);
-          c = nb_cell(ac, q & 3, nz, nx);
-          if (c >= 0 && !mine(pkx(c), me)) c = -1;
-        }
-        if (use_hash && c >= 0) {
-          unsigned h = hslot(c);
-          for (int probe = 0;; probe++) {
-            const int prev = atomicCAS(&sh->H[h], 0, c + 1);
-            if (prev == 0) break;
-            if (prev == c + 1 || probe >= kHash) {
-              if (probe >= kHash) sh->err = 5;
-              c = -1;
-              break;
-            }
-            h = (h + 1) & (kHash - 1);
-          }
-        }
-        r[u] = c;
-      }
-#endif
+      if (prof) __builtin_amdgcn_s_waitcnt(0);
+      AF_SUBT(2, tdd)
+      const long long tcl = prof ? wall_clock64() : 0;
 #pragma unroll
       for (int u = 0; u < 8; u++) {
         const long f = r[u] >= 0 ? (long)pkz(r[u]) * nx + pkx(r[u]) : 0;
-        s[u] = r[u] >= 0 ? (edge(pkx(r[u])) ? gld_sc1(S + f) : gld(S + f)) : (int)kKnown;
+        s[u] = r[u] >= 0 ? gld_sc1(S + f) : (int)kKnown;  // one load form for every lane
         o[u] = (!use_hash && r[u] >= 0) ? gatomic_max(own + f, stamp) : -1;
       }
-#if AF_UMAJOR
       // u-major list order: consecutive entries are neighbours of consecutive accepted cells, so
       // the lanes of an evaluating wave read overlapping stencils (fewer distinct cache lines)
       unsigned long long bm[8];
@@ -401,6 +368,7 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
         bm[u] = __ballot(s[u] != kKnown && o[u] < stamp);
         cnt += __popcll(bm[u]);
       }
+      AF_SUBT(3, tcl)
       int base = 0;
       if (lane == 0 && cnt) base = atomicAdd(&sh->nE, cnt);
       base = __shfl(base, 0);
@@ -418,28 +386,6 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
         }
         base += __popcll(bm[u]);
       }
-#else
-      int nw = 0;
-#pragma unroll
-      for (int u = 0; u < 8; u++) nw += (s[u] != kKnown && o[u] < stamp) ? 1 : 0;
-      int tot;
-      const int off = wave_excl_scan(nw, tot);
-      int base = 0;
-      if (lane == 0 && tot) base = atomicAdd(&sh->nE, tot);
-      base = __shfl(base, 0) + off;
-#pragma unroll
-      for (int u = 0; u < 8; u++) {
-        if (s[u] != kKnown && o[u] < stamp) {
-          if (base < capC) {
-            EL.put(base, r[u]);
-            EP.put(base, s[u] > 0 ? s[u] - 1 : -1);
-          } else {
-            sh->err = 2;
-          }
-          base++;
-        }
-      }
-#endif
     }
     __syncthreads();
     AF_TICK(2)

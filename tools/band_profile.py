@@ -55,7 +55,7 @@ out = {
     "mean_evaluated": float((P[:, 8] / steps).mean()),
     "max_close": float(P[:, 9].max()),
     "sweeps_per_source": float(sweeps.mean()),
-    "sub_ms_mean": dict(zip(["claim_nb_dedupe", "claim_loads", "claim_push", "eval_loads"],
+    "sub_ms_mean": dict(zip(["sub0", "sub1", "sub2", "sub3"],
                             (P[:, 10:14].mean(0) / 1e5).round(2).tolist())),
 }
 print(json.dumps(out, indent=1))
