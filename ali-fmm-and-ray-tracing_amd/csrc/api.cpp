@@ -66,6 +66,7 @@ struct alifmm_ctx {
   int nstab = 0;
   int* d_mid = nullptr;
   af::MatRec* d_mtab = nullptr;
+  double* d_mslo = nullptr;  // fouds18_A() slownesses per material (DevModel::mslo)
   int nmat = 0;
   double* d_gtab = nullptr;
   double* d_ptab = nullptr;
@@ -174,9 +175,10 @@ int alifmm_ctx_create(int device, alifmm_ctx** out) {
 
 static void free_model(alifmm_ctx* c) {
   dfree(c->d_veln); dfree(c->d_vm); dfree(c->d_velpn); dfree(c->d_sidx); dfree(c->d_stab); dfree(c->d_gtab);
-  dfree(c->d_ptab); dfree(c->d_mid); dfree(c->d_mtab);
+  dfree(c->d_ptab); dfree(c->d_mid); dfree(c->d_mtab); dfree(c->d_mslo);
   c->d_mid = nullptr;
   c->d_mtab = nullptr;
+  c->d_mslo = nullptr;
   c->nmat = 0;
   c->d_veln = c->d_vm = c->d_stab = c->d_gtab = c->d_ptab = nullptr;
   c->d_velpn = c->d_sidx = nullptr;
@@ -231,6 +233,8 @@ int alifmm_get_option(alifmm_ctx* ctx, const char* name, double* value) {
   else return fail(ctx, ALIFMM_E_ARG, "unknown option: %s", name);
   return ALIFMM_OK;
 }
+
+static af::DevModel dev_model(const alifmm_ctx* c);
 
 int alifmm_set_model(alifmm_ctx* ctx, int nnz, int nnx, const double* veln, const int64_t* velpn,
                      const double* vel_map, const int64_t* stif_den, const double* group_tab,
@@ -358,6 +362,12 @@ int alifmm_set_model(alifmm_ctx* ctx, int nnz, int nnx, const double* veln, cons
   ctx->gox = gox;
   ctx->goz = goz;
   ctx->vmax = vmax;
+  if (ctx->nmat > 0) {  // fouds18_A() slownesses per material (band kernels' fallback)
+    HIPCHK(dalloc(&ctx->d_mslo, 8 * (size_t)ctx->nmat));
+    const af::DevModel M = dev_model(ctx);
+    HIPCHK(af_launch_mat_slowness(&M, ctx->d_mslo, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+  }
   ctx->have_model = true;
   return ALIFMM_OK;
 }
@@ -383,6 +393,7 @@ static af::DevModel dev_model(const alifmm_ctx* c) {
   M.mid = c->d_mid;
   M.mtab = c->d_mtab;
   M.nmat = c->nmat;
+  M.mslo = c->d_mslo;
   M.gtab = c->d_gtab;
   M.ptab = c->d_ptab;
   M.ncol = c->ncol;

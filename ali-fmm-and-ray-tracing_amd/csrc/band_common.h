@@ -10,6 +10,10 @@ struct HList {
   T* l;  // LDS head
   T* g;  // global array (same indexing)
   AF_DEV T get(int i) const { return i < CAP ? l[i] : gld(g + i); }
+  // callers that checked (uniformly) that every index is below CAP: plain LDS accesses that the
+  // compiler can batch (get/put branch per access to the global spill)
+  AF_DEV T lds(int i) const { return l[i]; }
+  AF_DEV void put_lds(int i, T v) const { l[i] = v; }
   AF_DEV void put(int i, T v) const {
     if (i < CAP) l[i] = v;
     else gst(g + i, v);
@@ -17,6 +21,17 @@ struct HList {
 };
 
 AF_DEV int lane_id() { return threadIdx.x & 63; }
+
+// Uniform double kept in (and re-read from) scalar registers: the compiler cannot hoist
+// expressions derived from it above this point.  The persistent band kernels launder their
+// step-invariant doubles per phase so that derived constants are not kept live (and spilled to
+// scratch: a memory round trip per reload) across the step loop.
+AF_DEV double launder_u(double v) {
+  const long long b = __double_as_longlong(v);
+  int lo = __builtin_amdgcn_readfirstlane((int)b), hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+  asm volatile("" : "+s"(lo), "+s"(hi));
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
 
 // append with one LDS atomic per wave; returns the slot or -1 (pred false / overflow)
 AF_DEV int wave_push(int* counter, bool pred, int cap, int* err) {
@@ -111,6 +126,12 @@ AF_DEV CellMat band_mat(const DevModel& M, const MatRec* mat, const double* stab
   r.vm = v.quant ? (double)(float)m.vm : m.vm;
   r.stif = m.sidx >= 0 ? stab + 5 * m.sidx : nullptr;
   return r;
+}
+
+// fouds18_A() slownesses of main-grid cell (z, x)'s material (DevModel::mslo), or nullptr
+AF_DEV const double* band_slo(const DevModel& M, const MatView& v, int z, int x) {
+  if (!M.mid || !M.mslo) return nullptr;
+  return M.mslo + 8 * gld(M.mid + mv_cell(M, v, z, x)) + 4 * (v.quant ? 1 : 0);
 }
 
 }  // namespace af

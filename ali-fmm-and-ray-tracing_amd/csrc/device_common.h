@@ -85,6 +85,7 @@ struct DevModel {
   const int* mid;        // material id per cell (into mtab), or nullptr when there are too many
   const MatRec* mtab;
   int nmat;
+  const double* mslo;     // per material and MatView::quant: fouds18_A()'s 4 slownesses [nmat][2][4], or nullptr
 };
 
 // Logical grid -> coarse cell: f = lo1 + (a + side1)/s1 ; c = lo2 + (f + side2)/s2

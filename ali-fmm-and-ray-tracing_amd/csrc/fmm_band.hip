@@ -72,25 +72,13 @@ __device__ __noinline__
 AF_DEV
 #endif
 double fouds18_global(const GField& F, const DevModel& M, const CellMat& cm, int z, int x, double dnx, double dnz,
-                      int nx, int nz) {
-  return fouds18(F, M, cm, z, x, dnx, dnz, nx, nz);
+                      int nx, int nz, const double* pre) {
+  return fouds18(F, M, cm, z, x, dnx, dnz, nx, nz, pre);
 }
 
 AF_DEV unsigned hash_slot(int key) { return ((unsigned)key * 2654435761u) >> (32 - AF_HASH_LOG2); }
-// linear probing after a failed first CAS (prev = the occupant of slot h): returns c if this item
-// inserted c + 1 (it owns the cell), -1 if c was already present
-AF_DEV int claim_probe(int* H, unsigned h, int c, int prev, int* err) {
-  for (int probe = 0;; probe++) {
-    if (prev == c + 1) return -1;
-    if (probe >= kHash) {
-      *err = 5;
-      return -1;
-    }
-    h = (h + 1) & (kHash - 1);
-    prev = atomicCAS(&H[h], 0, c + 1);
-    if (prev == 0) return c;
-  }
-}
+// probe stride of key (double hashing): odd, so the sequence visits every slot
+AF_DEV unsigned hstep(int key) { return (((unsigned)key * 0x85ebca6bu) >> (32 - AF_HASH_LOG2)) | 1u; }
 
 // one band run over the main grid; returns steps.  T/S in global memory, sets and lists in LDS.
 // On entry the close set holds slots [0, sh->hi) with sh->nF free slots in sh->Fs.
@@ -180,18 +168,54 @@ AF_DEV long long band_run(const BandParams& P, BandLds* sh, BandSrc* B, const Ru
       // first probe of all 8 items issued back to back (one LDS round trip), collisions after
       unsigned hh[8];
       int pv[8];
+      if (nA <= kAcap) {  // (uniform) accepted list in LDS: branch-free item generation
 #pragma unroll
-      for (int u = 0; u < 8; u++) {
-        const int q = q0 + u * 64 + lane;
-        r[u] = q < nItems ? nb_cell(AL.get(q >> 2), q & 3, nz, nx) : -1;
-        hh[u] = hash_slot(r[u]);
+        for (int u = 0; u < 8; u++) {
+          const int q = q0 + u * 64 + lane;
+          const int c = nb_cell(AL.lds(q < nItems ? q >> 2 : 0), q & 3, nz, nx);
+          r[u] = q < nItems ? c : -1;
+          hh[u] = hash_slot(r[u]);
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          const int q = q0 + u * 64 + lane;
+          r[u] = q < nItems ? nb_cell(AL.get(q >> 2), q & 3, nz, nx) : -1;
+          hh[u] = hash_slot(r[u]);
+        }
       }
       if (use_hash) {
 #pragma unroll
         for (int u = 0; u < 8; u++) pv[u] = r[u] >= 0 ? atomicCAS(&sh->H[hh[u]], 0, r[u] + 1) : 0;
+        // collisions: double hashing (odd key-dependent stride: no primary clusters), all 8
+        // items in ONE loop whose trip count is the longest probe sequence among them
+        unsigned pend = 0;
 #pragma unroll
         for (int u = 0; u < 8; u++) {
-          if (pv[u] != 0) r[u] = claim_probe(sh->H, hh[u], r[u], pv[u], &sh->err);
+          if (pv[u] != 0) {
+            if (pv[u] == r[u] + 1) r[u] = -1;  // already claimed
+            else pend |= 1u << u;
+          }
+        }
+        for (int probe = 1; pend; probe++) {
+          if (probe >= kHash) {
+            sh->err = 5;
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+              if ((pend >> u) & 1u) r[u] = -1;
+            break;
+          }
+#pragma unroll
+          for (int u = 0; u < 8; u++) {
+            if ((pend >> u) & 1u) {
+              hh[u] = (hh[u] + hstep(r[u])) & (kHash - 1);
+              pv[u] = atomicCAS(&sh->H[hh[u]], 0, r[u] + 1);
+              if (pv[u] == 0 || pv[u] == r[u] + 1) {
+                if (pv[u] != 0) r[u] = -1;
+                pend &= ~(1u << u);
+              }
+            }
+          }
         }
       }
       AF_SUB(0)
@@ -235,15 +259,18 @@ AF_DEV long long band_run(const BandParams& P, BandLds* sh, BandSrc* B, const Ru
     AF_TICK(2)
     const int nE = min(sh->nE, P.capC);
     // ---- phase 3b: evaluate ----
+    const bool lds_e = nE <= kEcap;  // (uniform) the claimed list is in LDS
     for (int e = tid; e < nE; e += kThreads) {
-      const int r = EL.get(e);
+      const int r = lds_e ? EL.lds(e) : EL.get(e);
       const int z = pkz(r), x = pkx(r);
       if (prof) ts = wall_clock64();
       NbFieldT nb;  // stencil loads first, then the material id: one memory round trip
       nb.load(T, nz, nx, z, x);
       const CellMat cm = band_mat<LDSMAT>(M, sh->mat, sh->stab, R.mv, z, x);
       AF_SUB(3)
-      VL.put(e, update(nb, M, cm, z, x, R.dnx, nz, nx));
+      const double v = update(nb, M, cm, z, x, R.dnx, nz, nx);
+      if (lds_e) VL.put_lds(e, v);
+      else VL.put(e, v);
       myupd++;
     }
     AF_TICK(3)
@@ -254,7 +281,7 @@ AF_DEV long long band_run(const BandParams& P, BandLds* sh, BandSrc* B, const Ru
         const int r = EL.get(e);
         const int z = pkz(r), x = pkx(r);
         const CellMat cm = band_mat<LDSMAT>(M, sh->mat, sh->stab, R.mv, z, x);
-        VL.put(e, fouds18_global(F, M, cm, z, x, R.dnx, R.dnz, nx, nz));
+        VL.put(e, fouds18_global(F, M, cm, z, x, R.dnx, R.dnz, nx, nz, band_slo(M, R.mv, z, x)));
       }
     }
     __syncthreads();

@@ -78,21 +78,19 @@ AF_DEV bool rim(int x) {
   const int r = x & (kStripe - 1);
   return r == 0 || r == kStripe - 1;
 }
-AF_DEV unsigned hslot(int key) { return ((unsigned)key * 2654435761u) >> (32 - kHashLog); }
-// linear probing after a failed first CAS (prev = the occupant of slot h): returns c if this item
-// inserted c + 1 (it owns the cell), -1 if c was already present
-AF_DEV int claim_probe(int* H, unsigned h, int c, int prev, int* err) {
-  for (int probe = 0;; probe++) {
-    if (prev == c + 1) return -1;
-    if (probe >= kHash) {
-      *err = 5;
-      return -1;
-    }
-    h = (h + 1) & (kHash - 1);
-    prev = atomicCAS(&H[h], 0, c + 1);
-    if (prev == 0) return c;
-  }
+#if AF_PAIR_FOUDS_CALL
+// fouds18_A() fallback out of line (rare): its registers stay out of the step loop's budget
+__device__ __noinline__ double fouds18_call(const GFieldSC1& F, const DevModel& M, const CellMat& cm, int z, int x,
+                                            double dnx, double dnz, int nx, int nz, const double* pre) {
+  return fouds18(F, M, cm, z, x, dnx, dnz, nx, nz, pre);
 }
+#define AF_FOUDS18_BAND fouds18_call
+#else
+#define AF_FOUDS18_BAND fouds18
+#endif
+AF_DEV unsigned hslot(int key) { return ((unsigned)key * 2654435761u) >> (32 - kHashLog); }
+// probe stride of key (double hashing): odd, so the sequence visits every slot
+AF_DEV unsigned hstep(int key) { return (((unsigned)key * 0x85ebca6bu) >> (32 - kHashLog)) | 1u; }
 
 // two-member barrier; false on timeout (the partner never arrived: both members then stop)
 AF_DEV bool pair_barrier(int* ctr, int& gen, Lds* sh) {
@@ -123,7 +121,12 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
   if (src >= P.nsrc) return;  // both members of a pair take this exit together
   BandSrc* B = P.src + src;
   PairX* X = B->px;
+#if AF_LAUNDER
+  const int tid0 = threadIdx.x;
+  const int tid = tid0, lane = tid & 63, wv = tid >> 6;
+#else
   const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
+#endif
   const int nz = P.nz, nx = P.nx;
   double* T = B->T;
   int* S = B->S;
@@ -221,8 +224,8 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
     R.mv = MatView{1, 0, 0, 1, 0, 0, 1, 0, 0, 0, 0};
   else
     R.mv = MatView{P.sg, (P.sg - 1) / 2, 0, P.sg, (P.sg - 1) / 2, 0, 1, 0, 0, 0, 1};
-  R.delta = P.cdelta * P.dnx / P.vmax;
-  R.t0 = P.r0 * P.dnx / P.vmax;
+  R.delta = launder_u(P.cdelta * P.dnx / P.vmax);
+  R.t0 = launder_u(P.r0 * P.dnx / P.vmax);
   const GFieldSC1 F{T, S, nz, nx};
   long long steps = 0, myupd = 0;
   // profile (P.prof): thread 0 of member 0; phases [P1+X1, P2+X2, claim, evaluate, fallback, commit],
@@ -239,6 +242,14 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
 #define AF_SUBT(k, t0)                   \
   if (prof) sub[k] += wall_clock64() - (t0);
   while (true) {
+#if AF_LAUNDER
+    // the thread index is re-read each step (opaque to the compiler), so values derived from it
+    // (per-lane list addresses) are recomputed in the step instead of being kept live across the
+    // whole loop and spilled to scratch (a memory round trip per reload)
+    int tid = tid0;
+    asm volatile("" : "+v"(tid));
+    const int lane = tid & 63, wv = tid >> 6;
+#endif
     const int par = (int)(steps & 1);
     const int hi = sh->hi;
     // ---- P1: local Tmin, exchange ----
@@ -281,8 +292,9 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
     if (sh->live_g <= 0 || sh->err_g) break;
     if (tid == 0) sh->nD = 0;
     tmin = sh->tmin_g;
-    double dl = R.delta;
-    if (R.t0 > 0 && tmin < R.t0) dl = R.delta * (tmin / R.t0);
+    const double delta = launder_u(R.delta), t0 = launder_u(R.t0);
+    double dl = delta;
+    if (t0 > 0 && tmin < t0) dl = delta * (tmin / t0);
     const double thr = tmin + dl;
     // ---- P2: accept own cells; rim cells go to the exchange list ----
     int* nax = &sh->nAx;  // reset with nA in P1
@@ -321,6 +333,7 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
     // ---- P3a: claim own neighbours of own accepted cells and of the partner's rim cells ----
     const int nItems = 4 * (nA + nAp);
     const bool use_hash = nItems <= kHashItems;
+    const bool lds_items = AF_PAIR_PX && nA <= kAcap && nAp <= kThreads;
     const int stamp = (int)steps;
     for (int q0 = wv * 64 * 8; q0 < nItems; q0 += kThreads * 8) {
       int r[8], s[8], o[8];
@@ -328,26 +341,65 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
       // first probe of all 8 items issued back to back (one LDS round trip), collisions after
       unsigned hh[8];
       int pv[8];
+      if (lds_items) {  // (uniform) both lists in LDS: branch-free item generation
 #pragma unroll
-      for (int u = 0; u < 8; u++) {
-        const int q = q0 + u * 64 + lane;
-        int c = -1;
-        if (q < nItems) {
+        for (int u = 0; u < 8; u++) {
+          const int q = q0 + u * 64 + lane;
           const int a = q >> 2;
-          const int ap = a - nA;
-          const int ac = a < nA ? AL.get(a) : (AF_PAIR_PX && ap < kThreads) ? sh->Px[ap] : gld_sc1(AXp + ap);
-          c = nb_cell(ac, q & 3, nz, nx);
-          if (c >= 0 && !mine(pkx(c), me)) c = -1;
+          const int ac = a < nA ? AL.lds(a) : sh->Px[a - nA < kThreads ? a - nA : 0];
+          int c = nb_cell(ac, q & 3, nz, nx);
+          if (q >= nItems || (c >= 0 && !mine(pkx(c), me))) c = -1;
+          r[u] = c;
+          hh[u] = hslot(c);
         }
-        r[u] = c;
-        hh[u] = hslot(c);
+      } else {
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          const int q = q0 + u * 64 + lane;
+          int c = -1;
+          if (q < nItems) {
+            const int a = q >> 2;
+            const int ap = a - nA;
+            const int ac = a < nA ? AL.get(a) : (AF_PAIR_PX && ap < kThreads) ? sh->Px[ap] : gld_sc1(AXp + ap);
+            c = nb_cell(ac, q & 3, nz, nx);
+            if (c >= 0 && !mine(pkx(c), me)) c = -1;
+          }
+          r[u] = c;
+          hh[u] = hslot(c);
+        }
       }
       if (use_hash) {
 #pragma unroll
         for (int u = 0; u < 8; u++) pv[u] = r[u] >= 0 ? atomicCAS(&sh->H[hh[u]], 0, r[u] + 1) : 0;
+        // collisions: double hashing (odd key-dependent stride: no primary clusters), all 8
+        // items in ONE loop whose trip count is the longest probe sequence among them
+        unsigned pend = 0;
 #pragma unroll
         for (int u = 0; u < 8; u++) {
-          if (pv[u] != 0) r[u] = claim_probe(sh->H, hh[u], r[u], pv[u], &sh->err);
+          if (pv[u] != 0) {
+            if (pv[u] == r[u] + 1) r[u] = -1;  // already claimed
+            else pend |= 1u << u;
+          }
+        }
+        for (int probe = 1; pend; probe++) {
+          if (probe >= kHash) {
+            sh->err = 5;
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+              if ((pend >> u) & 1u) r[u] = -1;
+            break;
+          }
+#pragma unroll
+          for (int u = 0; u < 8; u++) {
+            if ((pend >> u) & 1u) {
+              hh[u] = (hh[u] + hstep(r[u])) & (kHash - 1);
+              pv[u] = atomicCAS(&sh->H[hh[u]], 0, r[u] + 1);
+              if (pv[u] == 0 || pv[u] == r[u] + 1) {
+                if (pv[u] != 0) r[u] = -1;
+                pend &= ~(1u << u);
+              }
+            }
+          }
         }
       }
       if (prof) __builtin_amdgcn_s_waitcnt(0);
@@ -391,8 +443,10 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
     AF_TICK(2)
     const int nE = min(sh->nE, capC);
     // ---- P3b: evaluate (cells whose stencil reaches the partner's columns: sc1 loads) ----
+    const bool lds_e = nE <= kEcap;  // (uniform) the claimed list is in LDS
+    const double dnx_e = launder_u(R.dnx);
     for (int e = tid; e < nE; e += kThreads) {
-      const int r = EL.get(e);
+      const int r = lds_e ? EL.lds(e) : EL.get(e);
       const int z = pkz(r), x = pkx(r);
       NbFieldT nb;  // stencil loads first, then the material id: one memory round trip
 #if AF_PAIR_ALLSC1
@@ -402,16 +456,23 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
       else nb.load(T, nz, nx, z, x);
 #endif
       const CellMat cm = band_mat<LDSMAT>(M, sh->mat, sh->stab, R.mv, z, x);
-      VL.put(e, update(nb, M, cm, z, x, R.dnx, nz, nx));
+      const double v = update(nb, M, cm, z, x, dnx_e, nz, nx);
+      if (lds_e) VL.put_lds(e, v);
+      else VL.put(e, v);
       myupd++;
     }
     AF_TICK(3)
+    const double dnx_f = launder_u(R.dnx), dnz_f = launder_u(R.dnz);
     for (int e = tid; e < nE; e += kThreads) {
       if (VL.get(e) == -1.0) {
         const int r = EL.get(e);
         const int z = pkz(r), x = pkx(r);
         const CellMat cm = band_mat<LDSMAT>(M, sh->mat, sh->stab, R.mv, z, x);
-        VL.put(e, fouds18(F, M, cm, z, x, R.dnx, R.dnz, nx, nz));
+#if AF_FOUDS_STUB  // timing experiment only: register pressure without fouds18_A()
+        VL.put(e, gld_sc1(T + (long)z * nx + x) == gld_sc1(T + (long)z * nx + x) ? gld_sc1(T + (long)z * nx + x) : R.t0 + R.delta);
+#else
+        VL.put(e, AF_FOUDS18_BAND(F, M, cm, z, x, dnx_f, dnz_f, nx, nz, band_slo(M, R.mv, z, x)));
+#endif
       }
     }
     __syncthreads();

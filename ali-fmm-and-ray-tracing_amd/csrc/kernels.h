@@ -116,6 +116,7 @@ hipError_t af_launch_rays(const af::RayParams* P, hipStream_t stream);
 hipError_t af_launch_pack_rays(const double* rx, const double* ry, const int* len, const long long* off, int nrays,
                                int max_pts, double* packed, hipStream_t stream);
 hipError_t af_launch_local_ops(const af::LocalOpsParams* P, hipStream_t stream);
+hipError_t af_launch_mat_slowness(const af::DevModel* M, double* out, hipStream_t stream);
 hipError_t af_launch_tbp(const af::DevModel* M, int n, const double* x1, const double* x2, const double* y1,
                          const double* y2, double dnx, int sg, double* out, hipStream_t stream);
 }

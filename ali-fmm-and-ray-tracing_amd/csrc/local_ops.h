@@ -16,28 +16,43 @@ namespace af {
 #ifndef AF_FOUDS_DEV
 #define AF_FOUDS_DEV AF_DEV
 #endif
+// fouds18_A()'s stencil-family slowness q (group velocity at 0, 45, -27, +27 deg off the cell's
+// orientation, :281-300 and the three later families); a function of the cell's material only
+AF_DEV double fouds18_slowness(const DevModel& M, const CellMat& cm, int q) {
+    const double veln = cm.veln;
+    double e = q == 0 ? pymod(0 - veln, 180)
+             : q == 1 ? (double)pyround(pymod(45 - veln, 180))
+             : q == 2 ? pymod(-27.0 - veln, 180) : pymod(27.0 - veln, 180);
+    return 1.0 / group_vel_cell(M, cm, e);
+}
+
+// pre: the four slownesses of the cell's material precomputed by fouds18_slowness() (the band
+// kernels read them from DevModel::mslo: the group-velocity code is the register-heaviest part of
+// fouds18_A(), and the persistent kernels cannot afford its registers in the step loop), or null
 template <class F>
 AF_FOUDS_DEV double fouds18(const F& f, const DevModel& M, const CellMat& cm, long iz, long ix, double dnx, double dnz,
-                      long nnx, long nnz) {
+                      long nnx, long nnz, const double* pre = nullptr) {
 #define N_(z, x) f.st((z), (x))
 #define T_(z, x) f.tt((z), (x))
-    double veln = cm.veln;
     /* ---- 0 deg stencil (:281-459) ---- */
     int tsw1 = 0;
     double travm = 0;
-    /* the four stencil families' slownesses (group velocity at 0, 45, -27, +27 deg), computed
-       unconditionally in the reference; evaluated here in one loop (one inlined instance) */
+    /* the four stencil families' slownesses, computed unconditionally in the reference */
     double slo0 = 0, slo1 = 0, slo2 = 0, slo3 = 0;
+    if (pre) {
+        slo0 = gld(pre);
+        slo1 = gld(pre + 1);
+        slo2 = gld(pre + 2);
+        slo3 = gld(pre + 3);
+    } else {
 #pragma unroll 1
-    for (int q = 0; q < 4; q++) {
-        double e = q == 0 ? pymod(0 - veln, 180)
-                 : q == 1 ? (double)pyround(pymod(45 - veln, 180))
-                 : q == 2 ? pymod(-27.0 - veln, 180) : pymod(27.0 - veln, 180);
-        double g = 1.0 / group_vel_cell(M, cm, e);
-        if (q == 0) slo0 = g;
-        else if (q == 1) slo1 = g;
-        else if (q == 2) slo2 = g;
-        else slo3 = g;
+        for (int q = 0; q < 4; q++) {
+            double g = fouds18_slowness(M, cm, q);
+            if (q == 0) slo0 = g;
+            else if (q == 1) slo1 = g;
+            else if (q == 2) slo2 = g;
+            else slo3 = g;
+        }
     }
     double slown = slo0;
     #pragma unroll 1

@@ -21,6 +21,7 @@ __global__ void local_ops_kernel(LocalOpsParams P) {
   const long pn = (long)P.pz * P.px;
   PatchField F{P.ttn + k * pn, P.nsts + k * pn, P.pz, P.px};
   DevModel M;
+  M.mslo = nullptr;
   M.nz0 = 1;
   M.nx0 = 1;
   M.veln = P.cveln + k;
@@ -51,6 +52,22 @@ __global__ void tbp_kernel(DevModel M, int n, const double* x1, const double* x2
   out[k] = tbp(M, x1[k], x2[k], y1[k], y2[k], dnx, sg);
 }
 
+// fouds18_A()'s four stencil-family slownesses of every distinct material, for both MatView
+// quantisations (sg = 1: as is; sg > 1: finer_grid_n's int32 orientation / float32 vel_map), with
+// the CellMat band_mat() builds -> DevModel::mslo [nmat][2][4]
+__global__ void mat_slowness_kernel(DevModel M, double* out) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= 2 * M.nmat) return;
+  const MatRec m = M.mtab[k >> 1];
+  const bool quant = k & 1;
+  CellMat c;
+  c.velpn = m.velpn;
+  c.veln = quant ? (double)(int)m.veln : m.veln;
+  c.vm = quant ? (double)(float)m.vm : m.vm;
+  c.stif = m.sidx >= 0 ? M.stab + 5 * m.sidx : nullptr;
+  for (int q = 0; q < 4; q++) out[4 * k + q] = fouds18_slowness(M, c, q);
+}
+
 }  // namespace af
 
 extern "C" hipError_t af_launch_local_ops(const af::LocalOpsParams* P, hipStream_t stream) {
@@ -61,5 +78,11 @@ extern "C" hipError_t af_launch_local_ops(const af::LocalOpsParams* P, hipStream
 extern "C" hipError_t af_launch_tbp(const af::DevModel* M, int n, const double* x1, const double* x2, const double* y1,
                                     const double* y2, double dnx, int sg, double* out, hipStream_t stream) {
   hipLaunchKernelGGL(af::tbp_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, *M, n, x1, x2, y1, y2, dnx, sg, out);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t af_launch_mat_slowness(const af::DevModel* M, double* out, hipStream_t stream) {
+  if (M->nmat <= 0) return hipSuccess;
+  hipLaunchKernelGGL(af::mat_slowness_kernel, dim3((2 * M->nmat + 63) / 64), dim3(64), 0, stream, *M, out);
   return hipGetLastError();
 }
