@@ -8,7 +8,8 @@ computes its own shard (weak scaling), no data-path collective; torch.distribute
 provides the barrier and the max-over-ranks of the step time.
 
 Reported: value = all ranks' (cells x sources) / max-over-ranks wall time of the timed steps;
-roofline of the dominant kernel (fmm_band_kernel) from in-library HIP events; cpu_baseline = the
+roofline of the dominant kernel (the band kernel: fmm_band_pair_kernel, two workgroups per source,
+when the batch fits the device, else fmm_band_kernel) from in-library HIP events on its stream; cpu_baseline = the
 CPU restatement of the reference (oracle/, one source per thread) on a bounded sample, rank 0, N=1.
 """
 import argparse
@@ -88,6 +89,7 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     sweeps = sum(ctx.source_stats(i)[1] for i in range(args.sources))
+    band_kernel = "fmm_band_pair_kernel" if int(ctx.get_option("last_pair")) else "fmm_band_kernel"
     steps_main = [int(ctx.source_stats(i)[0][3]) for i in range(args.sources)]
     dt = sharding.max_over_ranks(dt, dist)
     cells = float(n) * n
@@ -120,7 +122,13 @@ def main():
         t1 = time.perf_counter()
         O.travel_batch(scx[:ns], scz[:ns], veln, velpn, vel_map, stif, vt, vt, dnx=dnx, n_threads=th)
         tc = time.perf_counter() - t1
+        model = ""
+        try:
+            model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
+        except (OSError, StopIteration):
+            pass
         cpu = {"value": cells * ns / tc, "unit": "grid-cell updates/s", "cores": th, "kind": "port",
+               "host_cpu": model, "host_cpus_visible": os.cpu_count(), "seconds_per_source_per_core": tc * th / ns,
                "sample": "%d C4 sources (4096^2, z=0) on %d threads, one source per thread, oracle/alifmm_oracle.c "
                          "(bit-exact restatement of the reference's heap FMM); %.1f s wall" % (ns, th, tc)}
     if rank == 0:
@@ -141,11 +149,11 @@ def main():
             "config": {"workload": "C4: %dx%d weld-like, %d top-surface Tx sources per GPU, subgrid 1" % (n, n, args.sources),
                        "sources_per_gpu": args.sources, "total_sources": total_src, "grid": [n, n], "subgrid": 1},
             "sources_per_s": total_src * args.steps / dt,
-            "kernel_ms_per_step": {"fmm_init_kernel": init_ms / args.steps, "fmm_band_kernel": band_ms / args.steps},
+            "kernel_ms_per_step": {"fmm_init_kernel": init_ms / args.steps, band_kernel: band_ms / args.steps},
             "band_steps_main_mean": float(np.mean(steps_main)),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
-                         "kernel": "fmm_band_kernel", "bytes_per_cell_sweep": BYTES_PER_SWEEP,
+                         "kernel": band_kernel, "bytes_per_cell_sweep": BYTES_PER_SWEEP,
                          "cell_sweeps_per_launch": int(sweeps),
                          "algorithmic_bytes_per_launch": BYTES_PER_SWEEP * int(sweeps),
                          "traffic_bytes_per_launch": traffic_bytes},

@@ -1,5 +1,5 @@
 """Summarise a tools/profile.sh run: kernel-trace stats -> profiles/TAG_kernel_stats.csv, and the
-per-launch HBM-side traffic of fmm_band_kernel from the FETCH_SIZE / WRITE_SIZE passes ->
+per-launch HBM-side traffic of the band kernel (fmm_band_pair_kernel, or fmm_band_kernel) from the FETCH_SIZE / WRITE_SIZE passes ->
 profiles/TAG_traffic.json (bench.py reports it as roofline.traffic when the library matches).
 
 Correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE counts 128-B requests at 64 B on gfx950,
@@ -26,7 +26,7 @@ def per_launch(d, counter):
     vals = {}
     for f in glob.glob(os.path.join(out, d, "*counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            if "fmm_band_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            if "fmm_band" in r["Kernel_Name"] and r["Counter_Name"] == counter:
                 vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
     return sum(vals.values()) / len(vals) if vals else None
 
@@ -35,7 +35,7 @@ fetch_kb = per_launch("pmc_fetch", "FETCH_SIZE")
 write_kb = per_launch("pmc_write", "WRITE_SIZE")
 lib = os.path.join(repo, "ali-fmm-and-ray-tracing_amd", "lib", "libalifmm.so")
 res = {
-    "kernel": "fmm_band_kernel",
+    "kernel": "fmm_band_pair_kernel / fmm_band_kernel (the band kernel of the run)",
     "fetch_size_kb_per_launch": fetch_kb,
     "write_size_kb_per_launch": write_kb,
     "traffic_bytes_per_launch": (2 * fetch_kb + write_kb) * 1024 if fetch_kb and write_kb else None,
