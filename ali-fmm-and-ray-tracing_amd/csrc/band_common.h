@@ -128,10 +128,5 @@ AF_DEV CellMat band_mat(const DevModel& M, const MatRec* mat, const double* stab
   return r;
 }
 
-// fouds18_A() slownesses of main-grid cell (z, x)'s material (DevModel::mslo), or nullptr
-AF_DEV const double* band_slo(const DevModel& M, const MatView& v, int z, int x) {
-  if (!M.mid || !M.mslo) return nullptr;
-  return M.mslo + 8 * gld(M.mid + mv_cell(M, v, z, x)) + 4 * (v.quant ? 1 : 0);
-}
 
 }  // namespace af

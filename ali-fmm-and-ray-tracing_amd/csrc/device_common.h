@@ -104,6 +104,13 @@ AF_DEV long mv_cell(const DevModel& M, const MatView& v, int iz, int ix) {
   return (long)cz * M.nx0 + cx;
 }
 
+// fouds18_A()'s four slownesses of cell (iz, ix)'s material under view v (DevModel::mslo,
+// precomputed per material on the device), or nullptr when the model has no material table
+AF_DEV const double* mat_slo(const DevModel& M, const MatView& v, int iz, int ix) {
+  if (!M.mid || !M.mslo) return nullptr;
+  return M.mslo + 8 * (long)gld(M.mid + mv_cell(M, v, iz, ix)) + 4 * (v.quant ? 1 : 0);
+}
+
 struct CellMat {
   double veln, vm;
   int velpn;

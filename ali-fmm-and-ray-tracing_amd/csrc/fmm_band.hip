@@ -281,7 +281,7 @@ AF_DEV long long band_run(const BandParams& P, BandLds* sh, BandSrc* B, const Ru
         const int r = EL.get(e);
         const int z = pkz(r), x = pkx(r);
         const CellMat cm = band_mat<LDSMAT>(M, sh->mat, sh->stab, R.mv, z, x);
-        VL.put(e, fouds18_global(F, M, cm, z, x, R.dnx, R.dnz, nx, nz, band_slo(M, R.mv, z, x)));
+        VL.put(e, fouds18_global(F, M, cm, z, x, R.dnx, R.dnz, nx, nz, mat_slo(M, R.mv, z, x)));
       }
     }
     __syncthreads();

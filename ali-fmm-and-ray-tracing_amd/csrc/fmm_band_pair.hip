@@ -471,7 +471,7 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
 #if AF_FOUDS_STUB  // timing experiment only: register pressure without fouds18_A()
         VL.put(e, gld_sc1(T + (long)z * nx + x) == gld_sc1(T + (long)z * nx + x) ? gld_sc1(T + (long)z * nx + x) : R.t0 + R.delta);
 #else
-        VL.put(e, AF_FOUDS18_BAND(F, M, cm, z, x, dnx_f, dnz_f, nx, nz, band_slo(M, R.mv, z, x)));
+        VL.put(e, AF_FOUDS18_BAND(F, M, cm, z, x, dnx_f, dnz_f, nx, nz, mat_slo(M, R.mv, z, x)));
 #endif
       }
     }

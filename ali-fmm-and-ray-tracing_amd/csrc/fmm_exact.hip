@@ -122,7 +122,7 @@ AF_DEV double xrelax(const DevModel& M, const XGrid& g, int iz, int ix) {
   double v = update(nb, M, cm, iz, ix, g.dnx, g.nz, g.nx);
   if (v == -1.0) {
     GField F{g.T, g.S, g.nz, g.nx};
-    v = fouds18(F, M, cm, iz, ix, g.dnx, g.dnz, g.nx, g.nz);
+    v = fouds18(F, M, cm, iz, ix, g.dnx, g.dnz, g.nx, g.nz, mat_slo(M, g.mv, iz, ix));
   }
   return v;
 }
