@@ -16,6 +16,7 @@
 // drained (vmcnt 0) before the barrier, and read with sc1 loads.  Results are identical to the
 // single-workgroup kernel: the same cells are accepted, claimed and evaluated against the same
 // state each step; only which CU does the work differs.
+#include <type_traits>
 #include "kernels.h"
 #include "local_ops.h"
 #include "fields.h"
@@ -254,7 +255,11 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
     const int hi = sh->hi;
     // ---- P1: local Tmin, exchange ----
     double tmin = INFINITY;
-    for (int e = tid; e < hi; e += kThreads) tmin = fmin(tmin, Lt.get(e));
+    if (hi <= kLcap) {  // (uniform) close set in LDS: plain LDS reads the compiler can batch
+      for (int e = tid; e < hi; e += kThreads) tmin = fmin(tmin, Lt.lds(e));
+    } else {
+      for (int e = tid; e < hi; e += kThreads) tmin = fmin(tmin, Lt.get(e));
+    }
     for (int k = tid * 4; k < kHash; k += kThreads * 4) *(int4*)&sh->H[k] = make_int4(0, 0, 0, 0);
     tmin = wave_min(tmin);
     if (lane == 0) sh->red[wv] = tmin;
@@ -298,24 +303,35 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
     const double thr = tmin + dl;
     // ---- P2: accept own cells; rim cells go to the exchange list ----
     int* nax = &sh->nAx;  // reset with nA in P1
-    for (int e0 = wv * 64; e0 < hi; e0 += kThreads) {
-      const int e = e0 + lane;
-      const double t = e < hi ? Lt.get(e) : INFINITY;
-      const bool acc = t <= thr;
-      const int c = acc ? L.get(e) : 0;
-      int sa, sf;
-      wave_push2(&sh->nA, &sh->nF, acc, capL, &sh->err, sa, sf);
-      if (sa >= 0) {
-        AL.put(sa, c);
-        const long f = (long)pkz(c) * nx + pkx(c);
-        if (edge(pkx(c))) gst_sc1(S + f, (int)kKnown);
-        else gst(S + f, (int)kKnown);
-        Lt.put(e, INFINITY);
-        FS.put(sf, e);
+    auto accept = [&](auto lds_only) {
+      constexpr bool LO = decltype(lds_only)::value;
+      for (int e0 = wv * 64; e0 < hi; e0 += kThreads) {
+        const int e = e0 + lane;
+        const double t = e < hi ? (LO ? Lt.lds(e) : Lt.get(e)) : INFINITY;
+        const bool acc = t <= thr;
+        const int c = acc ? (LO ? L.lds(e) : L.get(e)) : 0;
+        int sa, sf;
+        wave_push2(&sh->nA, &sh->nF, acc, capL, &sh->err, sa, sf);
+        if (sa >= 0) {
+          AL.put(sa, c);
+          const long f = (long)pkz(c) * nx + pkx(c);
+          if (edge(pkx(c))) gst_sc1(S + f, (int)kKnown);
+          else gst(S + f, (int)kKnown);
+          if (LO) {
+            Lt.put_lds(e, INFINITY);
+            FS.put_lds(sf, e);
+          } else {
+            Lt.put(e, INFINITY);
+            FS.put(sf, e);
+          }
+        }
+        const int sx = wave_push(nax, acc && rim(pkx(c)), capL, &sh->err);
+        if (sx >= 0) gst_sc1(AXm + sx, c);
       }
-      const int sx = wave_push(nax, acc && rim(pkx(c)), capL, &sh->err);
-      if (sx >= 0) gst_sc1(AXm + sx, c);
-    }
+    };
+    // (uniform) close set and free stack in LDS (slots and free-stack entries are < hi)
+    if (hi <= kLcap) accept(std::true_type{});
+    else accept(std::false_type{});
     __syncthreads();
     if (tid == 0) gst_sc1(&X->nax[me][par], *nax);
     const long long tx2 = prof ? wall_clock64() : 0;
@@ -479,40 +495,55 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
     AF_TICK(4)
     // ---- P4: commit own cells; edge cells deferred to after the next X1 ----
     const int nF = sh->nF;
-    for (int e0 = wv * 64; e0 < nE; e0 += kThreads) {
-      const int e = e0 + lane;
-      bool fresh = false, defer = false;
-      int r = 0;
-      double v = 0.0;
-      if (e < nE) {
-        r = EL.get(e);
-        v = VL.get(e);
-        const int p = EP.get(e);
-        defer = edge(pkx(r));
-        if (!defer) gst(T + (long)pkz(r) * nx + pkx(r), v);
-        if (p >= 0) Lt.put(p, v);
-        else fresh = true;
-      }
-      const int k = wave_push(&sh->taken, fresh, 1 << 30, &sh->err);
-      int slot = -1;
-      if (k >= 0) {
-        slot = k < nF ? FS.get(nF - 1 - k) : hi + (k - nF);
-        if (slot >= capL) {
-          sh->err = 2;
-          slot = -1;
-        } else {
-          L.put(slot, r);
-          Lt.put(slot, v);
-          if (!defer) gst(S + (long)pkz(r) * nx + pkx(r), 1 + slot);
+    auto commit = [&](auto lds_only) {
+      constexpr bool LO = decltype(lds_only)::value;
+      for (int e0 = wv * 64; e0 < nE; e0 += kThreads) {
+        const int e = e0 + lane;
+        bool fresh = false, defer = false;
+        int r = 0;
+        double v = 0.0;
+        if (e < nE) {
+          r = LO ? EL.lds(e) : EL.get(e);
+          v = LO ? VL.lds(e) : VL.get(e);
+          const int p = LO ? EP.lds(e) : EP.get(e);
+          defer = edge(pkx(r));
+          if (!defer) gst(T + (long)pkz(r) * nx + pkx(r), v);
+          if (p >= 0) {
+            if (LO) Lt.put_lds(p, v);
+            else Lt.put(p, v);
+          } else {
+            fresh = true;
+          }
+        }
+        const int k = wave_push(&sh->taken, fresh, 1 << 30, &sh->err);
+        int slot = -1;
+        if (k >= 0) {
+          slot = k < nF ? (LO ? FS.lds(nF - 1 - k) : FS.get(nF - 1 - k)) : hi + (k - nF);
+          if (slot >= capL) {
+            sh->err = 2;
+            slot = -1;
+          } else {
+            if (LO) {
+              L.put_lds(slot, r);
+              Lt.put_lds(slot, v);
+            } else {
+              L.put(slot, r);
+              Lt.put(slot, v);
+            }
+            if (!defer) gst(S + (long)pkz(r) * nx + pkx(r), 1 + slot);
+          }
+        }
+        const int dslot = wave_push(&sh->nD, defer, kDcap, &sh->err);
+        if (dslot >= 0) {
+          sh->Dc[dslot] = r;
+          sh->Dv[dslot] = v;
+          sh->Ds[dslot] = slot >= 0 ? 1 + slot : 0;
         }
       }
-      const int dslot = wave_push(&sh->nD, defer, kDcap, &sh->err);
-      if (dslot >= 0) {
-        sh->Dc[dslot] = r;
-        sh->Dv[dslot] = v;
-        sh->Ds[dslot] = slot >= 0 ? 1 + slot : 0;
-      }
-    }
+    };
+    // (uniform) claimed lists in LDS and every slot a fresh cell can take below kLcap
+    if (nE <= kEcap && hi + nE <= kLcap) commit(std::true_type{});
+    else commit(std::false_type{});
     __syncthreads();
     if (tid == 0) {
       const int tk_ = sh->taken;
