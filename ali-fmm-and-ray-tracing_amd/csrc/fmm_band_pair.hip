@@ -27,8 +27,8 @@ namespace af {
 
 namespace pair {
 
-#ifndef AF_PAIR_ALLSC1
-#define AF_PAIR_ALLSC1 0
+#ifndef AF_PAIR_INV
+#define AF_PAIR_INV 1
 #endif
 #ifndef AF_PAIR_PX
 #define AF_PAIR_PX 1
@@ -93,8 +93,11 @@ AF_DEV unsigned hslot(int key) { return ((unsigned)key * 2654435761u) >> (32 - k
 // probe stride of key (double hashing): odd, so the sequence visits every slot
 AF_DEV unsigned hstep(int key) { return (((unsigned)key * 0x85ebca6bu) >> (32 - kHashLog)) | 1u; }
 
-// two-member barrier; false on timeout (the partner never arrived: both members then stop)
-AF_DEV bool pair_barrier(int* ctr, int& gen, Lds* sh) {
+// two-member barrier; false on timeout (the partner never arrived: both members then stop).
+// acquire = true: wave 0 invalidates the CU's vector L1 (agent-scope acquire, buffer_inv sc1)
+// after the partner's arrival, so that every later plain load of the step sees the partner's
+// (and this workgroup's own sc1-stored) edge data from L2
+AF_DEV bool pair_barrier(int* ctr, int& gen, Lds* sh, bool acquire = false) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores are complete
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -109,6 +112,7 @@ AF_DEV bool pair_barrier(int* ctr, int& gen, Lds* sh) {
       }
     }
   }
+  if (acquire && threadIdx.x < 64) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   __syncthreads();
   return sh->err != 7;
 }
@@ -335,7 +339,7 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
     __syncthreads();
     if (tid == 0) gst_sc1(&X->nax[me][par], *nax);
     const long long tx2 = prof ? wall_clock64() : 0;
-    if (!pair_barrier(&X->bar, gen, sh)) break;  // X2
+    if (!pair_barrier(&X->bar, gen, sh, AF_PAIR_INV)) break;  // X2 (+ L1 invalidate)
     AF_SUBT(1, tx2)
     AF_TICK(1)
     const int nA = min(sh->nA, capL);
@@ -424,7 +428,11 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
 #pragma unroll
       for (int u = 0; u < 8; u++) {
         const long f = r[u] >= 0 ? (long)pkz(r[u]) * nx + pkx(r[u]) : 0;
+#if AF_PAIR_INV
+        s[u] = r[u] >= 0 ? gld(S + f) : (int)kKnown;  // L1 invalidated at X2
+#else
         s[u] = r[u] >= 0 ? gld_sc1(S + f) : (int)kKnown;  // one load form for every lane
+#endif
         o[u] = (!use_hash && r[u] >= 0) ? gatomic_max(own + f, stamp) : -1;
       }
       // u-major list order: consecutive entries are neighbours of consecutive accepted cells, so
@@ -465,8 +473,8 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
       const int r = lds_e ? EL.lds(e) : EL.get(e);
       const int z = pkz(r), x = pkx(r);
       NbFieldT nb;  // stencil loads first, then the material id: one memory round trip
-#if AF_PAIR_ALLSC1
-      nb.load_sc1(T, nz, nx, z, x);
+#if AF_PAIR_INV
+      nb.load(T, nz, nx, z, x);  // L1 invalidated at X2: plain loads see the partner's edge cells
 #else
       if (edge(x)) nb.load_sc1(T, nz, nx, z, x);
       else nb.load(T, nz, nx, z, x);
