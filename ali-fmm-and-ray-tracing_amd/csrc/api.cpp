@@ -72,7 +72,7 @@ struct alifmm_ctx {
   double* d_ptab = nullptr;
   // options
   double cdelta = 0.5, r0 = 40.0;
-  int exact_r = 40;
+  int exact_r = 20;
   int batch = 256;
   int prof = 0;
   int pair = 1;     // two workgroups per source when the chunk fits the device (fmm_band_pair.hip)

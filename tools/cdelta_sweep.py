@@ -1,6 +1,6 @@
 """Band width sweep (GPU box): field parity vs the reference goldens and band time per cdelta.
 
-usage: python tools/cdelta_sweep.py 0.5 0.6 0.75 ...
+usage: python tools/cdelta_sweep.py 0.5 0.6 0.75 ...     (env EXACT_R: the exact-prefix radius option)
 """
 import json
 import os
@@ -38,6 +38,8 @@ def main():
     for cd in cds:
         ctx = _alifmm.Context(0)
         ctx.set_option("cdelta", cd)
+        if os.environ.get("EXACT_R"):
+            ctx.set_option("exact_r", float(os.environ["EXACT_R"]))
         res = {"cdelta": cd}
         ctx.set_model(*c3, vt, vt, 1e-3)
         x, z = W.c3_source()
