@@ -44,6 +44,10 @@ constexpr int kStripe = 1 << kStripeLog;
 constexpr int kLcap = 2560, kAcap = 1024, kEcap = 1536, kDcap = 1024;
 constexpr int kHashLog = 13;
 constexpr int kHash = 1 << kHashLog;
+#ifndef AF_CLAIM_U
+#define AF_CLAIM_U 4
+#endif
+constexpr int kClaimU = AF_CLAIM_U;  // claim items per lane per pass
 constexpr int kHashItems = 6144;  // claim items (both members' accepted cells x 4) for the LDS hash
 constexpr int kStabLds = 64, kPtabLds = 722, kMatLds = 256;
 
@@ -355,15 +359,15 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
     const bool use_hash = nItems <= kHashItems;
     const bool lds_items = AF_PAIR_PX && nA <= kAcap && nAp <= kThreads;
     const int stamp = (int)steps;
-    for (int q0 = wv * 64 * 8; q0 < nItems; q0 += kThreads * 8) {
-      int r[8], s[8], o[8];
+    for (int q0 = wv * 64 * kClaimU; q0 < nItems; q0 += kThreads * kClaimU) {
+      int r[kClaimU], s[kClaimU], o[kClaimU];
       const long long tdd = prof ? wall_clock64() : 0;
       // first probe of all 8 items issued back to back (one LDS round trip), collisions after
-      unsigned hh[8];
-      int pv[8];
+      unsigned hh[kClaimU];
+      int pv[kClaimU];
       if (lds_items) {  // (uniform) both lists in LDS: branch-free item generation
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
+        for (int u = 0; u < kClaimU; u++) {
           const int q = q0 + u * 64 + lane;
           const int a = q >> 2;
           const int ac = a < nA ? AL.lds(a) : sh->Px[a - nA < kThreads ? a - nA : 0];
@@ -374,7 +378,7 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
         }
       } else {
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
+        for (int u = 0; u < kClaimU; u++) {
           const int q = q0 + u * 64 + lane;
           int c = -1;
           if (q < nItems) {
@@ -390,12 +394,12 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
       }
       if (use_hash) {
 #pragma unroll
-        for (int u = 0; u < 8; u++) pv[u] = r[u] >= 0 ? atomicCAS(&sh->H[hh[u]], 0, r[u] + 1) : 0;
+        for (int u = 0; u < kClaimU; u++) pv[u] = r[u] >= 0 ? atomicCAS(&sh->H[hh[u]], 0, r[u] + 1) : 0;
         // collisions: double hashing (odd key-dependent stride: no primary clusters), all 8
         // items in ONE loop whose trip count is the longest probe sequence among them
         unsigned pend = 0;
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
+        for (int u = 0; u < kClaimU; u++) {
           if (pv[u] != 0) {
             if (pv[u] == r[u] + 1) r[u] = -1;  // already claimed
             else pend |= 1u << u;
@@ -405,12 +409,12 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
           if (probe >= kHash) {
             sh->err = 5;
 #pragma unroll
-            for (int u = 0; u < 8; u++)
+            for (int u = 0; u < kClaimU; u++)
               if ((pend >> u) & 1u) r[u] = -1;
             break;
           }
 #pragma unroll
-          for (int u = 0; u < 8; u++) {
+          for (int u = 0; u < kClaimU; u++) {
             if ((pend >> u) & 1u) {
               hh[u] = (hh[u] + hstep(r[u])) & (kHash - 1);
               pv[u] = atomicCAS(&sh->H[hh[u]], 0, r[u] + 1);
@@ -426,7 +430,7 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
       AF_SUBT(2, tdd)
       const long long tcl = prof ? wall_clock64() : 0;
 #pragma unroll
-      for (int u = 0; u < 8; u++) {
+      for (int u = 0; u < kClaimU; u++) {
         const long f = r[u] >= 0 ? (long)pkz(r[u]) * nx + pkx(r[u]) : 0;
 #if AF_PAIR_INV
         s[u] = r[u] >= 0 ? gld(S + f) : (int)kKnown;  // L1 invalidated at X2
@@ -437,10 +441,10 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
       }
       // u-major list order: consecutive entries are neighbours of consecutive accepted cells, so
       // the lanes of an evaluating wave read overlapping stencils (fewer distinct cache lines)
-      unsigned long long bm[8];
+      unsigned long long bm[kClaimU];
       int cnt = 0;
 #pragma unroll
-      for (int u = 0; u < 8; u++) {
+      for (int u = 0; u < kClaimU; u++) {
         bm[u] = __ballot(s[u] != kKnown && o[u] < stamp);
         cnt += __popcll(bm[u]);
       }
@@ -450,7 +454,7 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
       base = __shfl(base, 0);
       const unsigned long long lt = (1ull << lane) - 1ull;
 #pragma unroll
-      for (int u = 0; u < 8; u++) {
+      for (int u = 0; u < kClaimU; u++) {
         if ((bm[u] >> lane) & 1ull) {
           const int pos = base + __popcll(bm[u] & lt);
           if (pos < capC) {
