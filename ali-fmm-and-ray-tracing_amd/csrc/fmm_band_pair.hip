@@ -39,7 +39,10 @@ namespace pair {
 #endif
 constexpr int kThreads = AF_PAIR_THREADS;
 constexpr int kWaves = kThreads / 64;
-constexpr int kStripeLog = 6;
+#ifndef AF_STRIPE_LOG
+#define AF_STRIPE_LOG 6
+#endif
+constexpr int kStripeLog = AF_STRIPE_LOG;
 constexpr int kStripe = 1 << kStripeLog;
 constexpr int kLcap = 2560, kAcap = 1024, kEcap = 1536, kDcap = 1024;
 constexpr int kHashLog = 13;
