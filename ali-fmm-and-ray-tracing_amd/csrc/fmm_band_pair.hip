@@ -108,10 +108,12 @@ AF_DEV bool pair_barrier(int* ctr, int& gen, Lds* sh, bool acquire = false) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores are complete
   __syncthreads();
   if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add((AF_GLOBAL int*)ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int before = __hip_atomic_fetch_add((AF_GLOBAL int*)ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     gen += 2;
     long spins = 0;
-    while (gld_sc1(ctr) < gen) {
+    // the second member to arrive learns it from its own add (no poll round trip on the step's
+    // critical path); the first polls
+    while (before + 1 < gen && gld_sc1(ctr) < gen) {
       __builtin_amdgcn_s_sleep(2);
       if (++spins > (1L << 25)) {  // ~seconds: never reached unless the partner is not resident
         sh->err = 7;
