@@ -48,9 +48,9 @@ int alifmm_set_model(alifmm_ctx* ctx, int nnz, int nnx, const double* veln, cons
 
 /* Tuning: "pair" (1, default: two workgroups per source when the chunk fits the device, results
  * identical to the one-workgroup kernel), "prof" (1: record the band profile, alifmm_band_profile;
- * uses the one-workgroup kernel), "cdelta" (band width in units of dnx/vmax, default 0.5), "r0" (near-source band
+ * either kernel), "cdelta" (band width in units of dnx/vmax, default 0.5), "r0" (near-source band
  * schedule radius in cells, default 40), "exact_r" (radius in cells of the exact heap-ordered
- * main-loop prefix for subgrid 1, 0..48, default 40), "batch" (sources per launch, default 256). */
+ * main-loop prefix, 0..48, default 20), "batch" (sources per launch, default 256). */
 int alifmm_set_option(alifmm_ctx* ctx, const char* name, double value);
 /* Read an option, or "last_pair" (1 if the last alifmm_travel ran the two-workgroup kernel) and
  * "n_cu" (compute units of the device). */
