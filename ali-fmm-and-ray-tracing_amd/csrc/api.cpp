@@ -52,7 +52,9 @@ struct Arena {  // per-chunk scratch, reused across calls
 struct alifmm_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t fill = nullptr;  // field initialisation, overlapped with the source-init kernel
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t ev_fill = nullptr;
   std::string err;
   // model
   bool have_model = false;
@@ -167,6 +169,10 @@ int alifmm_ctx_create(int device, alifmm_ctx** out) {
     return ALIFMM_E_HIP;
   }
   for (auto& e : ctx->ev) (void)hipEventCreate(&e);
+  if (hipStreamCreateWithFlags(&ctx->fill, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_fill, hipEventDisableTiming) != hipSuccess) {
+    ctx->fill = nullptr;  // fills then stay on the main stream
+  }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) ctx->n_cu = prop.multiProcessorCount;
   *out = ctx;
@@ -201,6 +207,11 @@ int alifmm_ctx_destroy(alifmm_ctx* ctx) {
   free_arena(ctx->arena);
   free_model(ctx);
   for (auto& e : ctx->ev) if (e) (void)hipEventDestroy(e);
+  if (ctx->fill) {
+    (void)hipStreamSynchronize(ctx->fill);
+    (void)hipStreamDestroy(ctx->fill);
+  }
+  if (ctx->ev_fill) (void)hipEventDestroy(ctx->ev_fill);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return ALIFMM_OK;
@@ -462,6 +473,14 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
   int rc = ensure_arena(ctx, std::max(n, std::min(ctx->batch, 1)), cells, capL, capC, capS);
   if (rc) return rc;
   Arena& a = ctx->arena;
+  // subgrid 1: the fields are first written by the band kernel, so their initialisation runs on
+  // the fill stream beside the source-init kernel (which uses one CU per source); subgrid > 1:
+  // the exact-stage kernel writes them, so in order on the main stream
+  hipStream_t fs = (sg == 1 && ctx->fill) ? ctx->fill : ctx->stream;
+  if (fs != ctx->stream) {  // the fill stream must not overwrite fields a previous call still reads
+    HIPCHK(hipEventRecord(ctx->ev[3], ctx->stream));
+    HIPCHK(hipStreamWaitEvent(fs, ctx->ev[3], 0));
+  }
   std::vector<af::BandSrc> hs(n);
   for (int i = 0; i < n; i++) {
     int slot = first_slot + i;
@@ -490,10 +509,11 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
       b.Ss[0] = a.Ss + (size_t)i * 2 * a.capS;
       b.Ss[1] = b.Ss[0] + a.capS;
     }
-    HIPCHK(hipMemsetAsync(b.T, 0xFF, (size_t)cells * 8, ctx->stream));  // far: NaN (fields.h)
-    HIPCHK(hipMemsetAsync(b.S, 0xFF, (size_t)cells * 4, ctx->stream));    // kFar = -1
-    HIPCHK(hipMemsetAsync(b.own, 0xFF, (size_t)cells * 4, ctx->stream));  // claim stamps -1
+    HIPCHK(hipMemsetAsync(b.T, 0xFF, (size_t)cells * 8, fs));  // far: NaN (fields.h)
+    HIPCHK(hipMemsetAsync(b.S, 0xFF, (size_t)cells * 4, fs));    // kFar = -1
+    HIPCHK(hipMemsetAsync(b.own, 0xFF, (size_t)cells * 4, fs));  // claim stamps -1
   }
+  if (fs != ctx->stream) HIPCHK(hipEventRecord(ctx->ev_fill, fs));
   HIPCHK(hipMemcpyAsync(a.srcs, hs.data(), sizeof(af::BandSrc) * n, hipMemcpyHostToDevice, ctx->stream));
   af::DevModel M = dev_model(ctx);
   af::BandParams P;
@@ -553,6 +573,7 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
     HIPCHK(af_launch_exact(&P, ctx->stream));
   }
   HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
+  if (fs != ctx->stream) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_fill, 0));
   bool paired = false;
   if (ctx->pair && 16 * ((n + 7) / 8) <= ctx->n_cu) {
     HIPCHK(hipMemsetAsync(a.px, 0, sizeof(af::PairX) * n, ctx->stream));
