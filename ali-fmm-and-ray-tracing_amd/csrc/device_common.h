@@ -163,13 +163,8 @@ AF_DEV double christoffel_group(const double* s, double eff, double vm) {
 
 // Christoffel PHASE velocity (update() :1400-1406).
 AF_DEV double christoffel_phase(const double* s, double eff, double vm) {
-#if AF_SINCOS
-  double sa, ca;
-  sincos(eff * kDeg2Rad, &sa, &ca);
-#else
   double ca = cos(eff * kDeg2Rad);
   double sa = sin(eff * kDeg2Rad);
-#endif
   double A = ca * ca * s[0] + sa * sa * s[3];
   double B = ca * sa * (s[1] + s[3]);
   double C = ca * ca * s[3] + sa * sa * s[2];

@@ -26,9 +26,6 @@ namespace af {
 #ifndef AF_THREADS
 #define AF_THREADS 512
 #endif
-#ifndef AF_FOUDS_NOINLINE
-#define AF_FOUDS_NOINLINE 0
-#endif
 constexpr int kThreads = AF_THREADS;
 constexpr int kWaves = kThreads / 64;
 #ifndef AF_LCAP
@@ -64,13 +61,8 @@ struct BandLds {
   int err;
 };
 
-// fouds18_A() fallback out of line: rare, and inlined its live ranges (~180 VGPRs) would set
-// the whole kernel's register budget
-#if AF_FOUDS_NOINLINE
-__device__ __noinline__
-#else
+// fouds18_A() fallback (rare)
 AF_DEV
-#endif
 double fouds18_global(const GField& F, const DevModel& M, const CellMat& cm, int z, int x, double dnx, double dnz,
                       int nx, int nz, const double* pre) {
   return fouds18(F, M, cm, z, x, dnx, dnz, nx, nz, pre);

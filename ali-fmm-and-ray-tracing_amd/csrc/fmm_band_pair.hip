@@ -12,8 +12,10 @@
 //   P4  commit: interior cells directly; EDGE cells (within 2 columns of a stripe boundary, i.e.
 //       readable by the partner's 12-cell stencil) are deferred to after the next X1, so the
 //       partner never sees a value of this step while it may still be evaluating it.
-// Data the partner reads (edge cells' T and status, exchange lists) is written with sc1 stores,
-// drained (vmcnt 0) before the barrier, and read with sc1 loads.  Results are identical to the
+// Data the partner reads (edge cells' T and status, exchange lists) is written with sc1 stores and
+// drained (vmcnt 0) before the barrier; the exchange scalars and lists are read with sc1 loads, and
+// after X2 one wave invalidates the CU's L1 (agent-scope acquire) so that the claim's status loads
+// and the stencil loads are plain loads in one form for every lane.  Results are identical to the
 // single-workgroup kernel: the same cells are accepted, claimed and evaluated against the same
 // state each step; only which CU does the work differs.
 #include <type_traits>
@@ -24,15 +26,7 @@
 
 namespace af {
 
-
 namespace pair {
-
-#ifndef AF_PAIR_INV
-#define AF_PAIR_INV 1
-#endif
-#ifndef AF_PAIR_PX
-#define AF_PAIR_PX 1
-#endif
 
 #ifndef AF_PAIR_THREADS
 #define AF_PAIR_THREADS 512
@@ -86,16 +80,6 @@ AF_DEV bool rim(int x) {
   const int r = x & (kStripe - 1);
   return r == 0 || r == kStripe - 1;
 }
-#if AF_PAIR_FOUDS_CALL
-// fouds18_A() fallback out of line (rare): its registers stay out of the step loop's budget
-__device__ __noinline__ double fouds18_call(const GFieldSC1& F, const DevModel& M, const CellMat& cm, int z, int x,
-                                            double dnx, double dnz, int nx, int nz, const double* pre) {
-  return fouds18(F, M, cm, z, x, dnx, dnz, nx, nz, pre);
-}
-#define AF_FOUDS18_BAND fouds18_call
-#else
-#define AF_FOUDS18_BAND fouds18
-#endif
 AF_DEV unsigned hslot(int key) { return ((unsigned)key * 2654435761u) >> (32 - kHashLog); }
 // probe stride of key (double hashing): odd, so the sequence visits every slot
 AF_DEV unsigned hstep(int key) { return (((unsigned)key * 0x85ebca6bu) >> (32 - kHashLog)) | 1u; }
@@ -135,12 +119,8 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
   if (src >= P.nsrc) return;  // both members of a pair take this exit together
   BandSrc* B = P.src + src;
   PairX* X = B->px;
-#if AF_LAUNDER
   const int tid0 = threadIdx.x;
   const int tid = tid0, lane = tid & 63, wv = tid >> 6;
-#else
-  const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
-#endif
   const int nz = P.nz, nx = P.nx;
   double* T = B->T;
   int* S = B->S;
@@ -256,14 +236,12 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
 #define AF_SUBT(k, t0)                   \
   if (prof) sub[k] += wall_clock64() - (t0);
   while (true) {
-#if AF_LAUNDER
     // the thread index is re-read each step (opaque to the compiler), so values derived from it
     // (per-lane list addresses) are recomputed in the step instead of being kept live across the
     // whole loop and spilled to scratch (a memory round trip per reload)
     int tid = tid0;
     asm volatile("" : "+v"(tid));
     const int lane = tid & 63, wv = tid >> 6;
-#endif
     const int par = (int)(steps & 1);
     const int hi = sh->hi;
     // ---- P1: local Tmin, exchange ----
@@ -348,21 +326,19 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
     __syncthreads();
     if (tid == 0) gst_sc1(&X->nax[me][par], *nax);
     const long long tx2 = prof ? wall_clock64() : 0;
-    if (!pair_barrier(&X->bar, gen, sh, AF_PAIR_INV)) break;  // X2 (+ L1 invalidate)
+    if (!pair_barrier(&X->bar, gen, sh, true)) break;  // X2 (+ L1 invalidate)
     AF_SUBT(1, tx2)
     AF_TICK(1)
     const int nA = min(sh->nA, capL);
     // the partner's rim count and the head of its list in ONE round trip (entries past the count
     // are stale and never read), staged in LDS
     const int nAp = gld_sc1(&X->nax[pt][par]);
-#if AF_PAIR_PX
     sh->Px[tid] = gld_sc1(AXp + tid);
     __syncthreads();
-#endif
     // ---- P3a: claim own neighbours of own accepted cells and of the partner's rim cells ----
     const int nItems = 4 * (nA + nAp);
     const bool use_hash = nItems <= kHashItems;
-    const bool lds_items = AF_PAIR_PX && nA <= kAcap && nAp <= kThreads;
+    const bool lds_items = nA <= kAcap && nAp <= kThreads;
     const int stamp = (int)steps;
     for (int q0 = wv * 64 * kClaimU; q0 < nItems; q0 += kThreads * kClaimU) {
       int r[kClaimU], s[kClaimU], o[kClaimU];
@@ -389,7 +365,7 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
           if (q < nItems) {
             const int a = q >> 2;
             const int ap = a - nA;
-            const int ac = a < nA ? AL.get(a) : (AF_PAIR_PX && ap < kThreads) ? sh->Px[ap] : gld_sc1(AXp + ap);
+            const int ac = a < nA ? AL.get(a) : ap < kThreads ? sh->Px[ap] : gld_sc1(AXp + ap);
             c = nb_cell(ac, q & 3, nz, nx);
             if (c >= 0 && !mine(pkx(c), me)) c = -1;
           }
@@ -437,11 +413,7 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
 #pragma unroll
       for (int u = 0; u < kClaimU; u++) {
         const long f = r[u] >= 0 ? (long)pkz(r[u]) * nx + pkx(r[u]) : 0;
-#if AF_PAIR_INV
         s[u] = r[u] >= 0 ? gld(S + f) : (int)kKnown;  // L1 invalidated at X2
-#else
-        s[u] = r[u] >= 0 ? gld_sc1(S + f) : (int)kKnown;  // one load form for every lane
-#endif
         o[u] = (!use_hash && r[u] >= 0) ? gatomic_max(own + f, stamp) : -1;
       }
       // u-major list order: consecutive entries are neighbours of consecutive accepted cells, so
@@ -482,12 +454,7 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
       const int r = lds_e ? EL.lds(e) : EL.get(e);
       const int z = pkz(r), x = pkx(r);
       NbFieldT nb;  // stencil loads first, then the material id: one memory round trip
-#if AF_PAIR_INV
       nb.load(T, nz, nx, z, x);  // L1 invalidated at X2: plain loads see the partner's edge cells
-#else
-      if (edge(x)) nb.load_sc1(T, nz, nx, z, x);
-      else nb.load(T, nz, nx, z, x);
-#endif
       const CellMat cm = band_mat<LDSMAT>(M, sh->mat, sh->stab, R.mv, z, x);
       const double v = update(nb, M, cm, z, x, dnx_e, nz, nx);
       if (lds_e) VL.put_lds(e, v);
@@ -501,11 +468,7 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
         const int r = EL.get(e);
         const int z = pkz(r), x = pkx(r);
         const CellMat cm = band_mat<LDSMAT>(M, sh->mat, sh->stab, R.mv, z, x);
-#if AF_FOUDS_STUB  // timing experiment only: register pressure without fouds18_A()
-        VL.put(e, gld_sc1(T + (long)z * nx + x) == gld_sc1(T + (long)z * nx + x) ? gld_sc1(T + (long)z * nx + x) : R.t0 + R.delta);
-#else
-        VL.put(e, AF_FOUDS18_BAND(F, M, cm, z, x, dnx_f, dnz_f, nx, nz, mat_slo(M, R.mv, z, x)));
-#endif
+        VL.put(e, fouds18(F, M, cm, z, x, dnx_f, dnz_f, nx, nz, mat_slo(M, R.mv, z, x)));
       }
     }
     __syncthreads();

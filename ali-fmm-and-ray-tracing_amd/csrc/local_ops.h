@@ -13,9 +13,6 @@
 
 namespace af {
 
-#ifndef AF_FOUDS_DEV
-#define AF_FOUDS_DEV AF_DEV
-#endif
 // fouds18_A()'s stencil-family slowness q (group velocity at 0, 45, -27, +27 deg off the cell's
 // orientation, :281-300 and the three later families); a function of the cell's material only
 AF_DEV double fouds18_slowness(const DevModel& M, const CellMat& cm, int q) {
@@ -30,7 +27,7 @@ AF_DEV double fouds18_slowness(const DevModel& M, const CellMat& cm, int q) {
 // kernels read them from DevModel::mslo: the group-velocity code is the register-heaviest part of
 // fouds18_A(), and the persistent kernels cannot afford its registers in the step loop), or null
 template <class F>
-AF_FOUDS_DEV double fouds18(const F& f, const DevModel& M, const CellMat& cm, long iz, long ix, double dnx, double dnz,
+AF_DEV double fouds18(const F& f, const DevModel& M, const CellMat& cm, long iz, long ix, double dnx, double dnz,
                       long nnx, long nnz, const double* pre = nullptr) {
 #define N_(z, x) f.st((z), (x))
 #define T_(z, x) f.tt((z), (x))
