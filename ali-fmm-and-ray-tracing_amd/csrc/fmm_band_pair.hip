@@ -28,6 +28,9 @@ namespace af {
 
 namespace pair {
 
+#ifndef AF_FBLIST
+#define AF_FBLIST 1
+#endif
 #ifndef AF_PAIR_THREADS
 #define AF_PAIR_THREADS 512
 #endif
@@ -66,7 +69,7 @@ struct Lds {
   alignas(16) int H[kHash];
   int Px[kThreads];  // the partner's rim list, first kThreads entries (prefetched after X2)
   double tmin_g;
-  int nA, nE, nF, hi, taken, nD, nAx, live_g, err_g, err;
+  int nA, nE, nF, hi, taken, nD, nAx, live_g, err_g, err, nFb;
 };
 
 AF_DEV bool mine(int x, int m) { return ((x >> kStripeLog) & 1) == m; }
@@ -265,6 +268,7 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
       sh->nA = 0;
       sh->nAx = 0;
       sh->nE = 0;
+      sh->nFb = 0;
       sh->taken = 0;
     }
     const long long tx1 = prof ? wall_clock64() : 0;
@@ -460,9 +464,46 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
       if (lds_e) VL.put_lds(e, v);
       else VL.put(e, v);
       myupd++;
+#if AF_FBLIST
+      // no usable stencil: queue the cell for the fouds18_A() pass (the claim hash is free now)
+      const unsigned long long fm = __ballot(v == -1.0);
+      if (fm) {
+        const int fl = __ffsll((long long)fm) - 1;
+        int fb = 0;
+        if (lane == fl) fb = atomicAdd(&sh->nFb, __popcll(fm));
+        fb = __shfl(fb, fl) + __popcll(fm & ((1ull << lane) - 1ull));
+        if (v == -1.0 && fb < kHash) sh->H[fb] = e;
+      }
+#endif
     }
     AF_TICK(3)
     const double dnx_f = launder_u(R.dnx), dnz_f = launder_u(R.dnz);
+#if AF_FBLIST
+    // fouds18_A() over the compacted list: every fallback cell of the step in parallel lanes (one
+    // fouds18_A() latency on the critical path instead of one per evaluation round per wavefront)
+    __syncthreads();
+    const int nFb = sh->nFb;
+    for (int f = tid; f < nFb; f += kThreads) {
+      const int e = f < kHash ? sh->H[f] : -1;
+      if (e >= 0) {
+        const int r = EL.get(e);
+        const int z = pkz(r), x = pkx(r);
+        const CellMat cm = band_mat<LDSMAT>(M, sh->mat, sh->stab, R.mv, z, x);
+        VL.put(e, fouds18(F, M, cm, z, x, dnx_f, dnz_f, nx, nz, mat_slo(M, R.mv, z, x)));
+      }
+    }
+    if (nFb > kHash) {  // list overflow (more fallback cells than hash slots): the rest by scan
+      __syncthreads();
+      for (int e = tid; e < nE; e += kThreads) {
+        if (VL.get(e) == -1.0) {
+          const int r = EL.get(e);
+          const int z = pkz(r), x = pkx(r);
+          const CellMat cm = band_mat<LDSMAT>(M, sh->mat, sh->stab, R.mv, z, x);
+          VL.put(e, fouds18(F, M, cm, z, x, dnx_f, dnz_f, nx, nz, mat_slo(M, R.mv, z, x)));
+        }
+      }
+    }
+#else
     for (int e = tid; e < nE; e += kThreads) {
       if (VL.get(e) == -1.0) {
         const int r = EL.get(e);
@@ -471,6 +512,7 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
         VL.put(e, fouds18(F, M, cm, z, x, dnx_f, dnz_f, nx, nz, mat_slo(M, R.mv, z, x)));
       }
     }
+#endif
     __syncthreads();
     AF_TICK(4)
     // ---- P4: commit own cells; edge cells deferred to after the next X1 ----
