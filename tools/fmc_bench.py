@@ -1,0 +1,68 @@
+"""Full-matrix-capture throughput (BASELINE config 5 / SURVEY C5) on one GPU (run on the GPU box).
+
+C5: 4096^2 weld-like grid, 256 top transducers (z = 0, x = 8 + 16 k) firing into 256 bottom
+receivers (z = 4095, same x): one travel-time field per receiver, then one ray per
+(top source, bottom receiver) pair traced through the receiver's resident field
+(`trans_pairs[i, 256 + j] = 1`, Weld_rays.py:52-55).  On 8 GPUs the receivers shard 32 per GPU
+(sharding.deal) and every GPU traces its receivers' 256 x 32 rays; this tool runs the share of
+`--receivers` receivers on one GPU and reports the time, so the 8-GPU FMC time is that share's
+time.  Times only (compact storage): `with_points=False`.
+
+usage: python tools/fmc_bench.py [--receivers 32] [--sources 256]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "ali-fmm-and-ray-tracing_amd"))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+import _alifmm  # noqa: E402
+import workloads as W  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--receivers", type=int, default=32, help="receiver fields on this GPU (C5 on 8 GPUs: 32)")
+    ap.add_argument("--sources", type=int, default=256)
+    a = ap.parse_args()
+    n = 4096
+    veln, velpn, vm, sd = W.weldlike_model(n)
+    dnx = W.weldlike_dnx()
+    vt = W.default_table()
+    ctx = _alifmm.Context(0)
+    ctx.set_model(veln, velpn, vm, sd, vt, vt, dnx)
+    xs = 8 + 16 * np.arange(256)
+    rx = xs[:: 256 // a.receivers][: a.receivers]
+    src = np.stack([xs[: a.sources].astype(float), np.zeros(a.sources)], 1)
+    # warm-up on a small batch (code objects, arena)
+    ctx.travel(dnx * rx[:2].astype(float), np.full(2, dnx * (n - 1)), first_slot=0, copy_out=False)
+    ctx.find_rays([0] * 8, src[:8], np.tile([float(rx[0]), float(n - 1)], (8, 1)), with_points=False)
+    t0 = time.perf_counter()
+    ctx.travel(dnx * rx.astype(float), np.full(len(rx), dnx * (n - 1)), first_slot=0, copy_out=False)
+    t1 = time.perf_counter()
+    slots = np.repeat(np.arange(len(rx)), a.sources)
+    s_xy = np.tile(src, (len(rx), 1))
+    r_xy = np.repeat(np.stack([rx.astype(float), np.full(len(rx), float(n - 1))], 1), a.sources, axis=0)
+    times, lens, flags, _ = ctx.find_rays(slots, s_xy, r_xy, with_points=False)
+    t2 = time.perf_counter()
+    ok = bool(np.all(np.isfinite(times)) and np.all(times > 0))
+    print(json.dumps({
+        "workload": "C5 share: %d bottom-receiver fields (4096^2, subgrid 1) + %d x %d rays on one GPU"
+                    % (len(rx), a.sources, len(rx)),
+        "fields_s": t1 - t0, "rays_s": t2 - t1, "total_s": t2 - t0,
+        "fields_per_s": len(rx) / (t1 - t0), "rays_per_s": len(slots) / (t2 - t1),
+        "rays": int(len(slots)), "mean_points": float(lens.mean()), "early_exit": int(np.sum(flags & 1)),
+        "times_finite_positive": ok,
+        "c5_on_8_gpus_s": (t2 - t0) if a.receivers == 32 and a.sources == 256 else None,
+    }))
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
