@@ -1,13 +1,15 @@
 // fmm_init.hip — source initialisation of travel() (Anis_TTF_rays.py:1508-1993) on gfx950.
 //
-// One workgroup (one wave) per source.  The three refined stage grids (5x5 coarse window x27,
-// 13x13 x9, 27x27 x3; <= 109x109 nodes) live entirely in LDS (147.5 KB of the CU's 160 KB) and
+// One workgroup per source, two wavefronts.  The three refined stage grids (5x5 coarse window x27,
+// 13x13 x9, 27x27 x3; <= 109x109 nodes) live entirely in LDS (154 KB of the CU's 160 KB) and
 // are solved with the reference's own heap-ordered FMM: the heap (with its round-half-even parent,
 // SURVEY B-D3), the stage-1 nnz=nnx1 quirk (:1645, padded reads) and the hand-over order are
 // reproduced exactly, so the init region is the reference's up to device transcendental ulps.
-// The heap walk is inherently serial (lane 0); the 63 other lanes clear LDS, fill the straight-ray
-// footprint and decimate between stages.  Output: the decimated stage-3 nodes that the band
-// kernel hands over to the main grid (:2006-2040), as (cell, ttn, class) triples.
+// The heap walk is inherently serial: one lane of wavefront 0 runs the heap, one lane of
+// wavefront 1 relaxes each pop's neighbours while the heap runs downtree (stage_loop); all lanes
+// clear LDS, fill the straight-ray footprint and decimate between stages.  Output: the decimated
+// stage-3 nodes that the band kernel hands over to the main grid (:2006-2040), as (cell, ttn,
+// class) triples.
 #include "device_common.h"
 #include "local_ops.h"
 #include "kernels.h"
@@ -28,6 +30,10 @@ struct InitLds {
   MatRec mat[kInitMat];
   unsigned short hcell[kInitHeap];  // heap nodes (z << 8) | x
   signed char decC[kInitDec];       // 0 far, 1 known inner, 2 known outer, 3 close
+  // heap role -> relax role hand-off of one pop's neighbours (two-wavefront heap walk)
+  int cmd, done;                    // sequence numbers (cmd -1: stop)
+  int njob;
+  int jz[4], jx[4], jkind[4];       // kind: 1 add (far), 2 upd (close), +4: stage-1 quirk nnz
 };
 
 struct LdsField {
@@ -150,52 +156,103 @@ AF_DEV void relax(InitLds* L, const DevModel& M, const StageCfg& c, int nz, int 
   L->T[iz * nx + ix] = v;
 }
 
-// stage FMM loop (:1620-1674).  The four neighbours' materials are fetched together at each
-// pop (they do not depend on the heap), then relaxed in the reference's order.
+// Two-wavefront heap walk.  The reference relaxes a popped node's neighbours after downtree, and
+// neither depends on the other: downtree only moves heap entries (keys and the positive heap
+// indices in S), while update()/fouds18_A() read T and the validity / known-ness of S.  So lane 0
+// of wavefront 0 (heap role) pops, classifies the neighbours in the reference's order and runs
+// downtree, while lane 0 of wavefront 1 (relax role) relaxes them in that order; the heap role
+// then performs their addtree / updtree in order.  A far neighbour is marked valid (S = 1) right
+// after its relaxation, as the reference's addtree would before the next neighbour is relaxed.
+// Same results as the one-lane walk, with downtree off the critical path.
+constexpr int kJobAdd = 1, kJobUpd = 2, kJobQuirk = 4;
+AF_DEV void post(int* w, int v) { __hip_atomic_store(w, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP); }
+AF_DEV bool await_value(int* w, int v) {  // false: timeout (the other role is gone)
+  for (long spins = 0; __hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != v; spins++)
+    if (spins > (1L << 28)) return false;
+  return true;
+}
+AF_DEV int await_change(int* w, int last) {  // the next value != last, or -2 on timeout
+  for (long spins = 0;; spins++) {
+    const int v = __hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (v != last) return v;
+    if (spins > (1L << 28)) return -2;
+  }
+}
+
+// heap role, one pop: hand the classified neighbours to the relax role, downtree, wait, then the
+// neighbours' addtree / updtree in order.  false: the relax role timed out
+AF_DEV bool pop_two_role(Heap& h, int& seq, int n) {
+  InitLds* L = h.L;
+  if (n == 0) {  // nothing to relax
+    h.down();
+    return true;
+  }
+  L->njob = n;
+  post(&L->cmd, ++seq);
+  h.down();
+  if (!await_value(&L->done, seq)) return false;
+  for (int k = 0; k < n; k++) {
+    if (L->jkind[k] & kJobAdd) h.add(L->jz[k], L->jx[k]);
+    else h.upd(L->jz[k], L->jx[k]);
+  }
+  return true;
+}
+
+// stage FMM loop (:1620-1674) over the two roles (tid 0: heap, tid 64: relax)
 template <bool LDSMAT>
-AF_DEV void stage_loop(Heap& h, const DevModel& M, const StageCfg& c) {
+AF_DEV void stage_loop(Heap& h, const DevModel& M, const StageCfg& c, int tid) {
   InitLds* L = h.L;
   const int nz = h.nz, nx = h.nx;
-  bool finished = false;
-  while (h.ntr > 0 && !finished && !h.err) {
-    int ix = h.bx(1), iz = h.bz(1);
-    L->S[iz * nx + ix] = 0;
-    h.down();
-    CellMat cm[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const int z = k < 2 ? iz : iz + (k == 2 ? -1 : 1), x = k < 2 ? ix + (k == 0 ? -1 : 1) : ix;
-      if (0 <= z && z <= nz - 1 && 0 <= x && x <= nx - 1) cm[k] = init_mat<LDSMAT>(M, L, c.mv, z, x);
-    }
-    for (int s = 0; s < 2; s++) {
-      int i = s == 0 ? ix - 1 : ix + 1;
-      if (0 <= i && i <= nx - 1) {
-        int st = L->S[iz * nx + i];
-        if (st == -1) {
-          relax(L, M, c, nz, nx, iz, i, 0, cm[s]);
-          h.add(iz, i);
-        } else if (st > 0) {
-          relax(L, M, c, nz, nx, iz, i, c.quirk, cm[s]);
-          h.upd(iz, i);
+  if (tid == 0) {
+    int seq = 0;
+    bool finished = false;
+    while (h.ntr > 0 && !finished && !h.err) {
+      const int ix = h.bx(1), iz = h.bz(1);
+      L->S[iz * nx + ix] = 0;
+      int n = 0;
+      for (int s = 0; s < 2; s++) {
+        const int i = s == 0 ? ix - 1 : ix + 1;
+        if (0 <= i && i <= nx - 1) {
+          const int st = L->S[iz * nx + i];
+          if (st == -1 || st > 0) {
+            L->jz[n] = iz;
+            L->jx[n] = i;
+            L->jkind[n] = st == -1 ? kJobAdd : (kJobUpd | (c.quirk ? kJobQuirk : 0));
+            n++;
+          }
+        } else if (abs(c.isx - i) == c.max_dist + 1) {
+          finished = true;
         }
-      } else if (abs(c.isx - i) == c.max_dist + 1) {
-        finished = true;
       }
-    }
-    for (int s = 0; s < 2; s++) {
-      int i = s == 0 ? iz - 1 : iz + 1;
-      if (0 <= i && i <= nz - 1) {
-        int st = L->S[i * nx + ix];
-        if (st == -1) {
-          relax(L, M, c, nz, nx, i, ix, 0, cm[2 + s]);
-          h.add(i, ix);
-        } else if (st > 0) {
-          relax(L, M, c, nz, nx, i, ix, 0, cm[2 + s]);
-          h.upd(i, ix);
+      for (int s = 0; s < 2; s++) {
+        const int i = s == 0 ? iz - 1 : iz + 1;
+        if (0 <= i && i <= nz - 1) {
+          const int st = L->S[i * nx + ix];
+          if (st == -1 || st > 0) {
+            L->jz[n] = i;
+            L->jx[n] = ix;
+            L->jkind[n] = st == -1 ? kJobAdd : kJobUpd;
+            n++;
+          }
+        } else if (abs(c.isz - i) == c.max_dist + 1) {
+          finished = true;
         }
-      } else if (abs(c.isz - i) == c.max_dist + 1) {
-        finished = true;
       }
+      if (!pop_two_role(h, seq, n)) h.err = 1;
+    }
+    post(&L->cmd, -1);
+  } else if (tid == 64) {
+    int last = 0;
+    while (true) {
+      const int cmd = await_change(&L->cmd, last);
+      if (cmd < 0) break;  // stop (or timeout: the heap role is gone)
+      last = cmd;
+      for (int k = 0; k < L->njob; k++) {
+        const int z = L->jz[k], x = L->jx[k], kind = L->jkind[k];
+        relax(L, M, c, nz, nx, z, x, (kind & kJobQuirk) ? 1 : 0, init_mat<LDSMAT>(M, L, c.mv, z, x));
+        if (kind & kJobAdd) L->S[z * nx + x] = 1;  // valid for the next relaxations (addtree sets the index)
+      }
+      post(&L->done, cmd);
     }
   }
 }
@@ -244,69 +301,75 @@ struct WinField {
   }
 };
 
-// main loop :2055-2102 on the LDS window (heap in window-local coordinates)
+// main loop :2055-2102 on the LDS window (heap in window-local coordinates), two roles as above
 template <bool LDSMAT>
-AF_DEV void main_prefix(Heap& h, const DevModel& M, const InitJob& J, int wz0, int wx0, int wz1, int wx1) {
+AF_DEV void main_prefix(Heap& h, const DevModel& M, const InitJob& J, int wz0, int wx0, int wz1, int wx1, int tid) {
   InitLds* L = h.L;
   const int ww = h.nx;
   const int nnz = M.nz0, nnx = M.nx0;
   const MatView ident{1, 0, 0, 1, 0, 0, 1, 0, 0, 0, 0};
-  const WinField F{L->T, L->S, wz0, wx0, wz1, wx1, ww};
-  auto relax_main = [&](int iz, int ix, const CellMat& cm) {
-    NbFieldT nb;
-    nb.load_lds(L->T, L->S, wz0, wx0, wz1, wx1, ww, iz, ix);
-    double v = update(nb, M, cm, iz, ix, J.dnx, nnz, nnx);
-    if (v == -1.0) v = fouds18(F, M, cm, iz, ix, J.dnx, J.dnz, nnx, nnz);
-    L->T[(iz - wz0) * ww + (ix - wx0)] = v;
-  };
-  while (h.ntr > 0 && !h.err) {
-    const int lx = h.bx(1), lz = h.bz(1);
-    if (L->T[lz * ww + lx] >= J.tstop) break;
-    const int iz = lz + wz0, ix = lx + wx0;
-    if ((wz0 > 0 && iz - wz0 < 3) || (wz1 < nnz - 1 && wz1 - iz < 3) || (wx0 > 0 && ix - wx0 < 3) ||
-        (wx1 < nnx - 1 && wx1 - ix < 3))
-      break;
-    L->S[lz * ww + lx] = 0;
-    h.down();
-    CellMat cm[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const int z = k < 2 ? iz : iz + (k == 2 ? -1 : 1), x = k < 2 ? ix + (k == 0 ? -1 : 1) : ix;
-      if (0 <= z && z <= nnz - 1 && 0 <= x && x <= nnx - 1) cm[k] = init_mat<LDSMAT>(M, L, ident, z, x);
-    }
-    for (int s = 0; s < 2; s++) {
-      int i = s == 0 ? ix - 1 : ix + 1;
-      if (0 <= i && i <= nnx - 1) {
-        int li = i - wx0;
-        int st = L->S[lz * ww + li];
-        if (st == -1) {
-          relax_main(iz, i, cm[s]);
-          h.add(lz, li);
-        } else if (st > 0) {
-          relax_main(iz, i, cm[s]);
-          h.upd(lz, li);
+  if (tid == 0) {
+    int seq = 0;
+    while (h.ntr > 0 && !h.err) {
+      const int lx = h.bx(1), lz = h.bz(1);
+      if (L->T[lz * ww + lx] >= J.tstop) break;
+      const int iz = lz + wz0, ix = lx + wx0;
+      if ((wz0 > 0 && iz - wz0 < 3) || (wz1 < nnz - 1 && wz1 - iz < 3) || (wx0 > 0 && ix - wx0 < 3) ||
+          (wx1 < nnx - 1 && wx1 - ix < 3))
+        break;
+      L->S[lz * ww + lx] = 0;
+      int n = 0;
+      for (int s = 0; s < 2; s++) {
+        const int i = s == 0 ? ix - 1 : ix + 1;
+        if (0 <= i && i <= nnx - 1) {
+          const int st = L->S[lz * ww + (i - wx0)];
+          if (st == -1 || st > 0) {
+            L->jz[n] = lz;
+            L->jx[n] = i - wx0;
+            L->jkind[n] = st == -1 ? kJobAdd : kJobUpd;
+            n++;
+          }
         }
       }
-    }
-    for (int s = 0; s < 2; s++) {
-      int i = s == 0 ? iz - 1 : iz + 1;
-      if (0 <= i && i <= nnz - 1) {
-        int li = i - wz0;
-        int st = L->S[li * ww + lx];
-        if (st == -1) {
-          relax_main(i, ix, cm[2 + s]);
-          h.add(li, lx);
-        } else if (st > 0) {
-          relax_main(i, ix, cm[2 + s]);
-          h.upd(li, lx);
+      for (int s = 0; s < 2; s++) {
+        const int i = s == 0 ? iz - 1 : iz + 1;
+        if (0 <= i && i <= nnz - 1) {
+          const int st = L->S[(i - wz0) * ww + lx];
+          if (st == -1 || st > 0) {
+            L->jz[n] = i - wz0;
+            L->jx[n] = lx;
+            L->jkind[n] = st == -1 ? kJobAdd : kJobUpd;
+            n++;
+          }
         }
       }
+      if (!pop_two_role(h, seq, n)) h.err = 1;
+    }
+    post(&L->cmd, -1);
+  } else if (tid == 64) {
+    const WinField F{L->T, L->S, wz0, wx0, wz1, wx1, ww};
+    int last = 0;
+    while (true) {
+      const int cmd = await_change(&L->cmd, last);
+      if (cmd < 0) break;
+      last = cmd;
+      for (int k = 0; k < L->njob; k++) {
+        const int lz = L->jz[k], lx = L->jx[k], iz = lz + wz0, ix = lx + wx0;
+        const CellMat cm = init_mat<LDSMAT>(M, L, ident, iz, ix);
+        NbFieldT nb;
+        nb.load_lds(L->T, L->S, wz0, wx0, wz1, wx1, ww, iz, ix);
+        double v = update(nb, M, cm, iz, ix, J.dnx, nnz, nnx);
+        if (v == -1.0) v = fouds18(F, M, cm, iz, ix, J.dnx, J.dnz, nnx, nnz);
+        L->T[lz * ww + lx] = v;
+        if (L->jkind[k] & kJobAdd) L->S[lz * ww + lx] = 1;
+      }
+      post(&L->done, cmd);
     }
   }
 }
 
 template <bool LDSMAT>
-__global__ __launch_bounds__(64) void fmm_init_kernel(DevModel M, InitJob* jobs, int njobs, HandoverOut* out) {
+__global__ __launch_bounds__(128) void fmm_init_kernel(DevModel M, InitJob* jobs, int njobs, HandoverOut* out) {
   __shared__ InitLds lds;
   InitLds* L = &lds;
   const int src = blockIdx.x;
@@ -382,10 +445,13 @@ __global__ __launch_bounds__(64) void fmm_init_kernel(DevModel M, InitJob* jobs,
         if (cls >= 2) h.add(pz, px);
       }
     }
-    if (lane == 0) {
-      stage_loop<LDSMAT>(h, M, c);
-      err |= h.err;
+    if (lane == 0) {  // control words of the two-role walk
+      L->cmd = 0;
+      L->done = 0;
     }
+    __syncthreads();
+    stage_loop<LDSMAT>(h, M, c, lane);
+    if (lane == 0) err |= h.err;
     __syncthreads();
     decimate(L, nz, nx, lane, nl);
     __syncthreads();
@@ -420,9 +486,12 @@ __global__ __launch_bounds__(64) void fmm_init_kernel(DevModel M, InitJob* jobs,
           if (cls == 1 || cls == 2) L->S[pz * ww + px] = 0;
           if (cls >= 2) h.add(pz, px);
         }
-        main_prefix<LDSMAT>(h, M, J, wz0, wx0, wz1, wx1);
-        err |= h.err;
+        L->cmd = 0;
+        L->done = 0;
       }
+      __syncthreads();
+      main_prefix<LDSMAT>(h, M, J, wz0, wx0, wz1, wx1, lane);
+      if (lane == 0) err |= h.err;
       __syncthreads();
       // emit every touched window node: known (1) / close (3)
       if (lane == 0) {
@@ -466,8 +535,8 @@ __global__ __launch_bounds__(64) void fmm_init_kernel(DevModel M, InitJob* jobs,
 extern "C" hipError_t af_launch_init(const af::DevModel* M, af::InitJob* jobs, int njobs, af::HandoverOut* out,
                                      hipStream_t stream) {
   if (M->mid && M->nmat <= af::kInitMat)
-    hipLaunchKernelGGL(af::fmm_init_kernel<true>, dim3(njobs), dim3(64), 0, stream, *M, jobs, njobs, out);
+    hipLaunchKernelGGL(af::fmm_init_kernel<true>, dim3(njobs), dim3(128), 0, stream, *M, jobs, njobs, out);
   else
-    hipLaunchKernelGGL(af::fmm_init_kernel<false>, dim3(njobs), dim3(64), 0, stream, *M, jobs, njobs, out);
+    hipLaunchKernelGGL(af::fmm_init_kernel<false>, dim3(njobs), dim3(128), 0, stream, *M, jobs, njobs, out);
   return hipGetLastError();
 }
