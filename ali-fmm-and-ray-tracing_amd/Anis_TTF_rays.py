@@ -28,11 +28,17 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import _alifmm  # noqa: E402
 import sharding  # noqa: E402
+from raystore import PackedRayPaths, RayStore  # noqa: E402
 
 # Parameter used to enable/disable progress bars (reference :22-24; kept for API compatibility)
 tqdm_disable = False
 
 _EARLY_MSG = "Travel time to receiver increasing: Finishing ray early"
+
+# Largest dense ray array (bytes, per coordinate) that find_all_TTF_rays* still materialises like
+# the reference (:4286-4289); above it ray_paths_x / ray_paths_y are PackedRayPaths views of the
+# compact RayStore (ALI_FMM.rays), e.g. for the 4096² full-matrix capture (86 GB per dense array).
+ray_dense_limit_bytes = 4 << 30
 
 
 # ------------------------------------------------------------------------------------------------
@@ -304,6 +310,7 @@ class ALI_FMM:
         self.ray_paths_x = None
         self.ray_paths_y = None
         self.ray_len = None
+        self.rays = None  # RayStore of the last find_all_TTF_rays* call (compact layout)
         self._ctxs = {}
 
     # ---- GPU plumbing ----
@@ -534,16 +541,15 @@ class ALI_FMM:
 
     def _rays(self, veln, velpn, vel_map, stif_den, subgrid_size, trans_pairs, save_rays, n_devices, include_self):
         n_trans = len(self.isx)
-        if save_rays:
-            self.ray_paths_x = np.zeros((n_trans, n_trans, 5 * (veln.shape[0] + veln.shape[1])))
-            self.ray_paths_y = np.copy(self.ray_paths_x)
-            self.ray_len = np.zeros((n_trans, n_trans), dtype=int)
+        max_pts = 5 * (veln.shape[0] + veln.shape[1])
+        store = RayStore(n_trans, max_pts) if save_rays else None
         if type(trans_pairs) == type(None):
             trans_pairs = np.zeros((n_trans, n_trans))
             for i in range(n_trans):
                 for j in range(n_trans):
                     if i < j:
                         trans_pairs[i, j] = 1
+        trans_pairs = np.asarray(trans_pairs)
         rec = [j for j in range(n_trans) if np.sum(trans_pairs[:, j]) > 0]
         sg = int(subgrid_size)
         new_trans_x = sg * self.isx
@@ -556,30 +562,30 @@ class ALI_FMM:
 
         def trace(dev):
             try:
-                pairs = []
-                for j, (d, slot, _) in res.items():
+                ii, jj, slots = [], [], []
+                for j, (d, slot, _) in sorted(res.items()):
                     if d != dev:
                         continue
-                    for i in range(n_trans):
-                        if (include_self or i != j) and trans_pairs[i, j] == 1:
-                            pairs.append((i, j, slot))
-                if not pairs:
+                    sel = np.nonzero(trans_pairs[:, j] == 1)[0]
+                    if not include_self:
+                        sel = sel[sel != j]
+                    ii.append(sel)
+                    jj.append(np.full(len(sel), j))
+                    slots.append(np.full(len(sel), slot))
+                if not ii:
+                    return
+                ii, jj, slots = np.concatenate(ii), np.concatenate(jj), np.concatenate(slots)
+                if len(ii) == 0:
                     return
                 ctx = self._ctx(dev)
-                src = np.array([[new_trans_x[i], new_trans_y[i]] for i, _, _ in pairs])
-                dst = np.array([[new_trans_x[j], new_trans_y[j]] for _, j, _ in pairs])
-                t, lens, flags, rays = ctx.find_rays([s for _, _, s in pairs], src, dst, with_points=save_rays)
-                for k, (i, j, _) in enumerate(pairs):
-                    if flags[k] & 1:
-                        print(_EARLY_MSG)
-                    times[i, j] = t[k]
-                    if save_rays:
-                        ray_x = rays[k][0] / sg
-                        ray_y = rays[k][1] / sg
-                        ray_len = len(ray_x)
-                        self.ray_paths_x[i, j, 0:ray_len] = ray_x
-                        self.ray_paths_y[i, j, 0:ray_len] = ray_y
-                        self.ray_len[i, j] = ray_len
+                src = np.stack([new_trans_x[ii], new_trans_y[ii]], axis=1)
+                dst = np.stack([new_trans_x[jj], new_trans_y[jj]], axis=1)
+                t, lens, flags, pts = ctx.find_rays(slots, src, dst, with_points=save_rays, packed=True)
+                for _ in range(int(np.count_nonzero(flags & 1))):
+                    print(_EARLY_MSG)
+                times[ii, jj] = t
+                if save_rays:
+                    store.add(ii, jj, lens, pts / sg)
             except Exception as e:
                 errors.append(e)
 
@@ -595,6 +601,15 @@ class ALI_FMM:
             self._ctx(d).release_fields()
         if errors:
             raise errors[0]
+        if save_rays:
+            self.rays = store
+            self.ray_len = store.ray_len
+            if n_trans * n_trans * max_pts * 8 <= ray_dense_limit_bytes:
+                self.ray_paths_x = store.dense(0)
+                self.ray_paths_y = store.dense(1)
+            else:
+                self.ray_paths_x = PackedRayPaths(store, 0)
+                self.ray_paths_y = PackedRayPaths(store, 1)
         return times
 
     def find_all_TTF_rays(self, veln, velpn, vel_map=None, subgrid_size=9, trans_pairs=None, stif_den=None,
@@ -625,5 +640,15 @@ class ALI_FMM:
         if self.ray_len[i, j] == 0:
             print("Ray path has not been calculated")
             return None, None
+        if self.rays is not None:
+            x, z = self.rays.path(i, j)
+            return x.copy(), z.copy()
         ray_len = self.ray_len[i, j]
         return self.ray_paths_x[i, j, 0:ray_len], self.ray_paths_y[i, j, 0:ray_len]
+
+    def save_ray_store(self, path):
+        """Write the last call's rays in the compact layout (raystore.RayStore.save: ray_len,
+        ray_off, points, max_pts in one .npz, np.load-able without pickles)."""
+        if self.rays is None:
+            raise ValueError("no rays: call find_all_TTF_rays* with save_rays=True first")
+        self.rays.save(path)

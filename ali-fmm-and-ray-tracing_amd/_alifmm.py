@@ -44,6 +44,7 @@ def _load():
             "alifmm_get_field": (_i, [_p, _i, _p]),
             "alifmm_release_fields": (_i, [_p]),
             "alifmm_find_rays": (_i, [_p, _i, _p, _p, _p, _p, _p, _p, _p, _l]),
+            "alifmm_take_rays": (_i, [_p, _p, _l, _p]),
             "alifmm_source_stats": (_i, [_p, _i, _p, _p]),
             "alifmm_last_timing": (_i, [_p, _p, _p, _p]),
             "alifmm_band_profile": (_i, [_p, _i, _p]),
@@ -80,6 +81,9 @@ def _ci64(a):
 
 def _ci32(a):
     return np.ascontiguousarray(a, dtype=np.int32)
+
+
+KEEP_RAYS = -1  # ALIFMM_KEEP_RAYS (include/alifmm.h)
 
 
 def _ptr(a):
@@ -183,8 +187,13 @@ class Context:
     def release_fields(self):
         self._chk(lib().alifmm_release_fields(self._h), "release_fields")
 
-    def find_rays(self, slots, src_xy, rec_xy, with_points=True):
-        """Rays through resident receiver fields; returns (times, lens, flags, list of (x, z) arrays)."""
+    def find_rays(self, slots, src_xy, rec_xy, with_points=True, packed=False):
+        """Rays through resident receiver fields.
+
+        Returns (times, lens, flags, rays): rays is a list of (x, z) arrays per ray, or with
+        packed=True one (sum(lens), 2) array of all points in ray order (ray k starts at row
+        sum(lens[:k])) — no per-ray copies, and the host buffer is sized exactly (the points wait
+        in the context between alifmm_find_rays and alifmm_take_rays)."""
         slots = _ci32(slots)
         n = len(slots)
         src_xy = _c64(src_xy).reshape(n, 2)
@@ -192,22 +201,26 @@ class Context:
         times = np.zeros(n)
         lens = np.zeros(n, dtype=np.int32)
         flags = np.zeros(n, dtype=np.int32)
-        cap = 0
-        pts = None
-        if with_points and n:
-            nnz, nnx = self.shape
-            cap = n * 5 * (nnz + nnx)
-            pts = np.empty(2 * cap)
+        keep = with_points and n > 0
         self._chk(lib().alifmm_find_rays(self._h, n, _ptr(slots), _ptr(src_xy), _ptr(rec_xy), _ptr(times),
-                                         _ptr(lens), _ptr(flags), _ptr(pts), cap), "find_rays")
-        rays = None
-        if with_points:
-            rays = []
-            off = 0
-            for k in range(n):
-                p = pts[2 * off:2 * (off + lens[k])].reshape(-1, 2)
-                rays.append((p[:, 0].copy(), p[:, 1].copy()))
-                off += lens[k]
+                                         _ptr(lens), _ptr(flags), None, KEEP_RAYS if keep else 0), "find_rays")
+        if not with_points:
+            return times, lens, flags, None
+        npts = int(lens.sum(dtype=np.int64))
+        pts = np.empty((npts, 2))
+        if keep:
+            got = ctypes.c_int64(0)
+            self._chk(lib().alifmm_take_rays(self._h, _ptr(pts), npts, ctypes.byref(got)), "take_rays")
+            if got.value != npts:
+                raise AlifmmError("take_rays: %d points kept, %d expected" % (got.value, npts))
+        if packed:
+            return times, lens, flags, pts
+        rays = []
+        off = 0
+        for k in range(n):
+            p = pts[off:off + lens[k]]
+            rays.append((p[:, 0].copy(), p[:, 1].copy()))
+            off += lens[k]
         return times, lens, flags, rays
 
     def source_stats(self, slot):

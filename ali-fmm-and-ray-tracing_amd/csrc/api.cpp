@@ -85,6 +85,10 @@ struct alifmm_ctx {
   std::vector<Field> fields;
   Arena arena;
   double t_init = 0, t_band = 0, t_total = 0;
+  // packed points of the last alifmm_find_rays(ray_xy = NULL, ray_xy_cap = ALIFMM_KEEP_RAYS) call,
+  // per ray in the caller's order, until alifmm_take_rays() copies them out
+  std::vector<std::vector<double>> kept_rays;
+  int64_t kept_pts = 0;
 };
 
 static int fail(alifmm_ctx* c, int code, const char* fmt, ...) {
@@ -743,7 +747,10 @@ int alifmm_find_rays(alifmm_ctx* ctx, int npairs, const int32_t* field_slot, con
   for (auto& g : groups) order.insert(order.end(), g.second.begin(), g.second.end());
   // offsets follow the caller's ray order; we first trace everything (times/lengths), packing each
   // chunk into a host staging area keyed by ray id.
-  std::vector<std::vector<double>> staged(ray_xy ? npairs : 0);
+  const bool keep = !ray_xy && ray_xy_cap == ALIFMM_KEEP_RAYS;
+  ctx->kept_rays.clear();
+  ctx->kept_pts = 0;
+  std::vector<std::vector<double>> staged((ray_xy || keep) ? npairs : 0);
   for (auto& g : groups) {
     const int sg = g.first;
     const auto& ids = g.second;
@@ -793,7 +800,7 @@ int alifmm_find_rays(alifmm_ctx* ctx, int npairs, const int32_t* field_slot, con
         lens[k] = l[i];
         flg[k] = fl[i];
       }
-      if (ray_xy) {
+      if (ray_xy || keep) {
         std::vector<long long> off(n + 1, 0);
         for (int i = 0; i < n; i++) off[i + 1] = off[i] + l[i];
         dfree(d_packed);
@@ -819,9 +826,30 @@ int alifmm_find_rays(alifmm_ctx* ctx, int npairs, const int32_t* field_slot, con
       if (flags) flags[k] = flg[k];
       if (ray_xy) std::copy(staged[k].begin(), staged[k].end(), ray_xy + 2 * offsets[k]);
     }
+    if (keep) {
+      ctx->kept_rays.swap(staged);
+      ctx->kept_pts = offsets[npairs];
+    }
   }
   cleanup();
   return rc;
+}
+
+int alifmm_take_rays(alifmm_ctx* ctx, double* ray_xy, int64_t ray_xy_cap, int64_t* n_points) {
+  if (!ctx) return ALIFMM_E_ARG;
+  if (n_points) *n_points = ctx->kept_pts;
+  if (!ray_xy) return ALIFMM_OK;  // size query
+  if (ray_xy_cap < ctx->kept_pts)
+    return fail(ctx, ALIFMM_E_ARG, "take_rays: ray_xy capacity %lld < %lld", (long long)ray_xy_cap,
+                (long long)ctx->kept_pts);
+  int64_t off = 0;
+  for (auto& r : ctx->kept_rays) {
+    std::copy(r.begin(), r.end(), ray_xy + 2 * off);
+    off += (int64_t)r.size() / 2;
+  }
+  std::vector<std::vector<double>>().swap(ctx->kept_rays);
+  ctx->kept_pts = 0;
+  return ALIFMM_OK;
 }
 
 int alifmm_put_field(alifmm_ctx* ctx, int slot, int subgrid, const double* data) {

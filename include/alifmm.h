@@ -79,10 +79,19 @@ int alifmm_release_fields(alifmm_ctx* ctx);
  *   flags[k]             bit0: reference's early exit ("Travel time to receiver increasing"),
  *                        bit1: point capacity reached, bit2: empty candidate plane
  *   ray_xy (nullable)    packed points: ray k's x at ray_xy[2*off[k] + 2*i], z at +1,
- *                        off[k] = sum of ray_len[0..k-1]; capacity ray_xy_cap points.      */
+ *                        off[k] = sum of ray_len[0..k-1]; capacity ray_xy_cap points.
+ *                        ray_xy == NULL with ray_xy_cap == ALIFMM_KEEP_RAYS keeps the packed
+ *                        points in the context for alifmm_take_rays() (exactly sized buffer).  */
+#define ALIFMM_KEEP_RAYS (-1)
 int alifmm_find_rays(alifmm_ctx* ctx, int npairs, const int32_t* field_slot, const double* src_xy,
                      const double* rec_xy, double* times, int32_t* ray_len, int32_t* flags,
                      double* ray_xy, int64_t ray_xy_cap);
+
+/* Packed points kept by the last alifmm_find_rays(..., NULL, ALIFMM_KEEP_RAYS): *n_points = their
+ * count (sum of ray_len); with ray_xy != NULL (capacity ray_xy_cap points) they are copied out in
+ * the layout of alifmm_find_rays() and released.  Compact ray storage for full-matrix captures
+ * (the reference's dense (n, n, 5(nnz+nnx)) arrays, :4286-4289, do not fit at 4096²). */
+int alifmm_take_rays(alifmm_ctx* ctx, double* ray_xy, int64_t ray_xy_cap, int64_t* n_points);
 
 /* Diagnostics of the last alifmm_travel(): per slot band steps [stage1, stage2, stage3|-, main]
  * and main-grid cell-sweeps (local-operator evaluations); device time of the last call's kernels. */

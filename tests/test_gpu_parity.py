@@ -273,6 +273,23 @@ def test_weld_example_end_to_end(golden, A):
     rx, ry = M.ray_path(15, 46)
     assert len(rx) == k and abs(rx[0] - sx[15] / 0.0002) < 1e-9
     assert abs(ry[0] - 0) < 1e-12 and abs(ry[-1] - 423) < 1e-12 and abs(rx[-1] - 250) < 1e-12
+    # compact ray storage: the same call with the dense arrays disabled gives the same
+    # times, and the packed views read exactly like the dense arrays (Weld_rays.py:64-66 trimming)
+    lim = A.ray_dense_limit_bytes
+    try:
+        A.ray_dense_limit_bytes = 0
+        M2 = A.ALI_FMM(veln, velpn, vel_map, sx, sy, stif_den=stif, dnx=0.0002)
+        t2 = M2.find_all_TTF_rays_parallel(veln, velpn, vel_map, stif_den=stif, n_threads=8, trans_pairs=pairs)
+    finally:
+        A.ray_dense_limit_bytes = lim
+    assert isinstance(M2.ray_paths_x, A.PackedRayPaths)
+    np.testing.assert_array_equal(t2, t)
+    np.testing.assert_array_equal(M2.ray_len, M.ray_len)
+    np.testing.assert_array_equal(M2.ray_paths_x[:, :, 0:max_len], M.ray_paths_x[:, :, 0:max_len])
+    np.testing.assert_array_equal(M2.ray_paths_y[:, :, 0:max_len], M.ray_paths_y[:, :, 0:max_len])
+    rx2, ry2 = M2.ray_path(15, 46)
+    np.testing.assert_array_equal(rx2, rx)
+    np.testing.assert_array_equal(ry2, ry)
 
 
 def test_pair_kernel_identical_to_single_workgroup(ctx):

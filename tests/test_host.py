@@ -151,3 +151,45 @@ def test_sharding_world2_gloo():
     assert not set(a.tolist()) & set(b.tolist())
     assert a.tolist() == [16 + 32 * k for k in range(128)]  # rank 0 = BASELINE C4 sources
     assert m == 1.5 and set(scz) == {0.0}
+
+
+def test_ray_store_matches_dense_layout(tmp_path):
+    """Compact ray storage: PackedRayPaths reads like the reference's dense
+    (n, n, 5(nnz+nnx)) ray arrays (:4286-4289) for the indexing callers use (Weld_rays.py:64-66
+    trims [:, :, 0:max_len]; ray_path :4687-4705 reads [i, j, 0:len]), and save/load round-trips."""
+    from raystore import PackedRayPaths, RayStore
+
+    rng = np.random.default_rng(5)
+    n, cap = 7, 40
+    st = RayStore(n, cap)
+    dense = np.zeros((2, n, n, cap))
+    pairs = [(i, j) for i in range(n) for j in range(n) if rng.random() < 0.6]
+    for chunk in (pairs[: len(pairs) // 2], pairs[len(pairs) // 2:]):
+        lens = rng.integers(1, cap + 1, len(chunk))
+        pts = rng.normal(size=(int(lens.sum()), 2))
+        st.add([p[0] for p in chunk], [p[1] for p in chunk], lens, pts)
+        o = 0
+        for (i, j), L in zip(chunk, lens):
+            dense[:, i, j, :L] = pts[o:o + L].T
+            o += L
+    for ax in (0, 1):
+        P = PackedRayPaths(st, ax)
+        D = dense[ax]
+        assert P.shape == D.shape and len(P) == n
+        np.testing.assert_array_equal(np.asarray(P), D)
+        ml = int(st.ray_len.max())
+        for key in [(slice(None), slice(None), slice(0, ml)), (3,), (2, 5), (2, 5, slice(0, 9)), (1, 4, 7),
+                    (slice(1, 5), 2), (Ellipsis, 3), (np.array([0, 2, 6]), np.array([1, 1, 3])),
+                    (slice(None), np.array([4, 0]), slice(2, 30, 3)), (-1, -2, -3)]:
+            np.testing.assert_array_equal(P[key], D[key], err_msg=str(key))
+    for i, j in pairs:
+        x, z = st.path(i, j)
+        L = st.ray_len[i, j]
+        np.testing.assert_array_equal(x, dense[0, i, j, :L])
+        np.testing.assert_array_equal(z, dense[1, i, j, :L])
+    f = str(tmp_path / "rays.npz")
+    st.save(f)
+    st2 = RayStore.load(f)
+    np.testing.assert_array_equal(st2.ray_len, st.ray_len)
+    np.testing.assert_array_equal(st2.dense(0), dense[0])
+    np.testing.assert_array_equal(st2.dense(1), dense[1])
