@@ -12,8 +12,10 @@
 //   P4  commit: interior cells directly; EDGE cells (within 2 columns of a stripe boundary, i.e.
 //       readable by the partner's 12-cell stencil) are deferred to after the next X1, so the
 //       partner never sees a value of this step while it may still be evaluating it.
-// Data the partner reads (edge cells' T and status, exchange lists) is written with sc1 stores and
-// drained (vmcnt 0) before the barrier; the exchange scalars and lists are read with sc1 loads, and
+// X1 carries no bulk data: each member stores its (Tmin, live, err) as four flagged 8-byte words
+// (step number in the high half) and polls the partner's, so the exchange is one store and one poll
+// round trip.  X2 is a counter barrier: data the partner reads (edge cells' T and status, the rim
+// list) is written with sc1 stores and drained (vmcnt 0) before it; the rim list is read with sc1 loads, and
 // after X2 one wave invalidates the CU's L1 (agent-scope acquire) so that the claim's status loads
 // and the stencil loads are plain loads in one form for every lane.  Results are identical to the
 // single-workgroup kernel: the same cells are accepted, claimed and evaluated against the same
@@ -258,28 +260,47 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
     tmin = wave_min(tmin);
     if (lane == 0) sh->red[wv] = tmin;
     __syncthreads();
+    const long long tx1 = prof ? wall_clock64() : 0;
     if (tid == 0) {
       double t = sh->red[0];
       for (int w = 1; w < kWaves; w++) t = fmin(t, sh->red[w]);
-      gst_sc1(&X->tmin[me][par], t);
-      gst_sc1(&X->live[me][par], hi - sh->nF);
-      gst_sc1(&X->err[me][par], sh->err);
-      sh->tmin_g = t;
       sh->nA = 0;
       sh->nAx = 0;
       sh->nE = 0;
       sh->nFb = 0;
       sh->taken = 0;
+      // X1: flagged words out, the partner's in.  No drain: nothing this member stored is read by
+      // the partner before X2 (which drains); seeing the partner's words means it has finished
+      // the previous step (its evaluation loads were consumed before its commit).
+      const unsigned long long g = (unsigned long long)(steps + 1) << 32;
+      const unsigned long long tb = (unsigned long long)__double_as_longlong(t);
+      const int live = hi - sh->nF;
+      gst_sc1(&X->x1[me][0], g | (tb & 0xffffffffull));
+      gst_sc1(&X->x1[me][1], g | (tb >> 32));
+      gst_sc1(&X->x1[me][2], g | (unsigned)live);
+      gst_sc1(&X->x1[me][3], g | (unsigned)sh->err);
+      unsigned long long w0, w1, w2, w3;
+      long spins = 0;
+      while (true) {
+        w0 = gld_sc1(&X->x1[pt][0]);
+        w1 = gld_sc1(&X->x1[pt][1]);
+        w2 = gld_sc1(&X->x1[pt][2]);
+        w3 = gld_sc1(&X->x1[pt][3]);
+        if (((w0 & w1 & w2 & w3) >> 32) == (g >> 32) && ((w0 | w1 | w2 | w3) >> 32) == (g >> 32)) break;
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1L << 25)) {  // ~seconds: never reached unless the partner is not resident
+          sh->err = 7;
+          break;
+        }
+      }
+      const double tp = __longlong_as_double((long long)((w0 & 0xffffffffull) | (w1 << 32)));
+      sh->tmin_g = fmin(t, tp);
+      sh->live_g = live + (int)(unsigned)w2;
+      sh->err_g = sh->err | (int)(unsigned)w3;
     }
-    const long long tx1 = prof ? wall_clock64() : 0;
-    if (!pair_barrier(&X->bar, gen, sh)) break;  // X1
+    __syncthreads();
     AF_SUBT(0, tx1)
     const long long tap = prof ? wall_clock64() : 0;
-    if (tid == 0) {
-      sh->tmin_g = fmin(sh->tmin_g, gld_sc1(&X->tmin[pt][par]));
-      sh->live_g = (hi - sh->nF) + gld_sc1(&X->live[pt][par]);
-      sh->err_g = sh->err | gld_sc1(&X->err[pt][par]);
-    }
     // apply the previous step's deferred edge commits (the partner finished evaluating it)
     for (int d = tid; d < sh->nD; d += kThreads) {
       const int c = sh->Dc[d];
@@ -289,7 +310,7 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
     }
     __syncthreads();
     AF_TICK(0)
-    if (sh->live_g <= 0 || sh->err_g) break;
+    if (sh->live_g <= 0 || sh->err_g || sh->err == 7) break;
     if (tid == 0) sh->nD = 0;
     tmin = sh->tmin_g;
     const double delta = launder_u(R.delta), t0 = launder_u(R.t0);

@@ -10,10 +10,10 @@ namespace af {
 struct PairX {
   int bar;          // pair barrier counter
   int pad[31];
-  double tmin[2][2];  // [member][step parity]
-  int live[2][2];
-  int err[2][2];
   int nax[2][2];    // accepted cells next to the other member's columns, per step
+  // step-start exchange (X1) as flagged words: (step + 1) << 32 | payload, [member][tmin lo, tmin
+  // hi, live, err]; the payload arrives with the flag, so X1 is one store + polls (no counter)
+  unsigned long long x1[2][4];
 };
 
 struct BandSrc {
