@@ -220,6 +220,8 @@ AF_DEV double tbp(const DevModel& M, double x1, double x2, double y1, double y2,
   double next_x = (double)pyround(start_x) + dir_x * 0.5;
   double next_y = (double)pyround(start_y) + dir_y * 0.5;
   const MatView ident{1, 0, 0, 1, 0, 0, 1, 0, 0, 0, 0};
+  int last_id = -1;
+  double slown = 0.0;
   while (!(fin_x && fin_y)) {
     if (((next_x > end_x && dir_x == 1) || (next_x < end_x && dir_x == -1)) && !fin_x) {
       fin_x = true;
@@ -259,12 +261,19 @@ AF_DEV double tbp(const DevModel& M, double x1, double x2, double y1, double y2,
     long y_pos = pyround((prev_y + nyv) / 2);
     if (x_pos < 0) x_pos += M.nx0;
     if (y_pos < 0) y_pos += M.nz0;
-    CellMat cm = cell_mat(M, ident, (int)y_pos, (int)x_pos);
-    double eff = pymod(cm.veln - angle, 180);
+    // the slowness depends on the cell only through its material record (the angle is fixed for
+    // the segment), so consecutive pieces in the same material reuse it: the same value, without
+    // the group-velocity evaluation (the per-cell material id identifies the record exactly)
+    const int id = M.mid ? gld(M.mid + mv_cell(M, ident, (int)y_pos, (int)x_pos)) : -1;
+    if (id < 0 || id != last_id) {
+      CellMat cm = cell_mat(M, ident, (int)y_pos, (int)x_pos);
+      double eff = pymod(cm.veln - angle, 180);
+      double velocity = group_vel_cell(M, cm, eff);
+      slown = 1.0 / velocity;
+      last_id = id;
+    }
     double ddx = prev_x - nxv, ddy = prev_y - nyv;
     double distance = dnx * sqrt(ddx * ddx + ddy * ddy);
-    double velocity = group_vel_cell(M, cm, eff);
-    double slown = 1.0 / velocity;
     section_time += distance * slown;
     prev_x = nxv;
     prev_y = nyv;

@@ -193,7 +193,6 @@ __global__ __launch_bounds__(64 * kRayWaves) void find_ray_kernel(RayParams P) {
       rxo[ray_len] = nx_;
       ryo[ray_len] = ny_;
     }
-    tt += tbp(P.M, last_x, nx_, last_y, ny_, P.dnx, sg);  // wave-uniform
     lvx = nx_ - last_x;
     last_x = nx_;
     lvy = ny_ - last_y;
@@ -207,7 +206,17 @@ __global__ __launch_bounds__(64 * kRayWaves) void find_ray_kernel(RayParams P) {
     ryo[ray_len] = recy;
   }
   const long npts = ray_len + 1;
-  tt += tbp(P.M, last_x, recx, last_y, recy, P.dnx, sg);
+  // ray_time (:2992-3022) after the walk: the group's lanes evaluate G segments at a time (each a
+  // time_between_points() of consecutive points, read back from the ray buffer) and lane order
+  // gives the reference's left-to-right sum, so the per-step walk carries no serial segment time
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");  // lane 0's point stores, visible to the group
+  for (long k0 = 0; k0 < npts - 1; k0 += G) {
+    const long k = k0 + lane;
+    double seg = 0.0;
+    if (k < npts - 1) seg = tbp(P.M, gld(rxo + k), gld(rxo + k + 1), gld(ryo + k), gld(ryo + k + 1), P.dnx, sg);
+    const int m = (int)min((long)G, npts - 1 - k0);
+    for (int l = 0; l < m; l++) tt += __shfl(seg, l, G);
+  }
   if (lane == 0) {
     P.times[ray] = tt;
     P.ray_len[ray] = (int)npts;

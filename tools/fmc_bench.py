@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--receivers", type=int, default=32, help="receiver fields on this GPU (C5 on 8 GPUs: 32)")
     ap.add_argument("--sources", type=int, default=256)
     ap.add_argument("--dropin", action="store_true", help="through ALI_FMM.find_all_TTF_rays, points kept")
+    ap.add_argument("--dump", default=None, help="save the ray times and lengths (npz) for bit-identity checks")
     a = ap.parse_args()
     if a.dropin:
         return dropin(a)
@@ -58,6 +59,8 @@ def main():
     times, lens, flags, _ = ctx.find_rays(slots, s_xy, r_xy, with_points=False)
     t2 = time.perf_counter()
     ok = bool(np.all(np.isfinite(times)) and np.all(times > 0))
+    if a.dump:
+        np.savez(a.dump, times=times, lens=lens, flags=flags)
     print(json.dumps({
         "workload": "C5 share: %d bottom-receiver fields (4096^2, subgrid 1) + %d x %d rays on one GPU"
                     % (len(rx), a.sources, len(rx)),
