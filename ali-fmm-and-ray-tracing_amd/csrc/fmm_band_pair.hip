@@ -510,7 +510,7 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
         const int r = EL.get(e);
         const int z = pkz(r), x = pkx(r);
         const CellMat cm = band_mat<LDSMAT>(M, sh->mat, sh->stab, R.mv, z, x);
-        VL.put(e, fouds18(F, M, cm, z, x, dnx_f, dnz_f, nx, nz, mat_slo(M, R.mv, z, x)));
+        VL.put(e, fouds18<true>(F, M, cm, z, x, dnx_f, dnz_f, nx, nz, mat_slo(M, R.mv, z, x)));
       }
     }
     if (nFb > kHash) {  // list overflow (more fallback cells than hash slots): the rest by scan
@@ -520,7 +520,7 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
           const int r = EL.get(e);
           const int z = pkz(r), x = pkx(r);
           const CellMat cm = band_mat<LDSMAT>(M, sh->mat, sh->stab, R.mv, z, x);
-          VL.put(e, fouds18(F, M, cm, z, x, dnx_f, dnz_f, nx, nz, mat_slo(M, R.mv, z, x)));
+          VL.put(e, fouds18<true>(F, M, cm, z, x, dnx_f, dnz_f, nx, nz, mat_slo(M, R.mv, z, x)));
         }
       }
     }
@@ -530,7 +530,7 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
         const int r = EL.get(e);
         const int z = pkz(r), x = pkx(r);
         const CellMat cm = band_mat<LDSMAT>(M, sh->mat, sh->stab, R.mv, z, x);
-        VL.put(e, fouds18(F, M, cm, z, x, dnx_f, dnz_f, nx, nz, mat_slo(M, R.mv, z, x)));
+        VL.put(e, fouds18<true>(F, M, cm, z, x, dnx_f, dnz_f, nx, nz, mat_slo(M, R.mv, z, x)));
       }
     }
 #endif
@@ -626,7 +626,8 @@ __global__ __launch_bounds__(kThreads) void fmm_band_pair_kernel(BandParams P) {
 // cooperative launch (all 2*nsrc workgroups resident, one per CU); hipErrorCooperativeLaunchTooLarge
 // (or any launch error) tells the caller to use the single-workgroup kernel instead
 extern "C" hipError_t af_launch_band_pair(const af::BandParams* P, hipStream_t stream) {
-  const bool lds = P->M.mid && P->M.nmat <= af::pair::kMatLds && P->M.nstab <= af::pair::kStabLds &&
+  // (mid => the material table and its fouds18_A() slownesses mslo exist: fouds18<true>)
+  const bool lds = P->M.mid && P->M.mslo && P->M.nmat <= af::pair::kMatLds && P->M.nstab <= af::pair::kStabLds &&
                    361 * P->M.ncol <= af::pair::kPtabLds;
   if (!lds) return hipErrorNotSupported;
   const dim3 g(16 * ((P->nsrc + 7) / 8)), b(af::pair::kThreads);

@@ -25,8 +25,10 @@ AF_DEV double fouds18_slowness(const DevModel& M, const CellMat& cm, int q) {
 
 // pre: the four slownesses of the cell's material precomputed by fouds18_slowness() (the band
 // kernels read them from DevModel::mslo: the group-velocity code is the register-heaviest part of
-// fouds18_A(), and the persistent kernels cannot afford its registers in the step loop), or null
-template <class F>
+// fouds18_A(), and the persistent kernels cannot afford its registers in the step loop), or null.
+// PRE_ONLY: the caller guarantees pre != null, so the group-velocity code is not compiled in at all
+// (fouds18_A() alone then needs 87 VGPRs instead of 181)
+template <bool PRE_ONLY = false, class F>
 AF_DEV double fouds18(const F& f, const DevModel& M, const CellMat& cm, long iz, long ix, double dnx, double dnz,
                       long nnx, long nnz, const double* pre = nullptr) {
 #define N_(z, x) f.st((z), (x))
@@ -36,12 +38,12 @@ AF_DEV double fouds18(const F& f, const DevModel& M, const CellMat& cm, long iz,
     double travm = 0;
     /* the four stencil families' slownesses, computed unconditionally in the reference */
     double slo0 = 0, slo1 = 0, slo2 = 0, slo3 = 0;
-    if (pre) {
+    if (PRE_ONLY || pre) {
         slo0 = gld(pre);
         slo1 = gld(pre + 1);
         slo2 = gld(pre + 2);
         slo3 = gld(pre + 3);
-    } else {
+    } else if constexpr (!PRE_ONLY) {
 #pragma unroll 1
         for (int q = 0; q < 4; q++) {
             double g = fouds18_slowness(M, cm, q);
