@@ -42,6 +42,17 @@ ray_dense_limit_bytes = 4 << 30
 
 
 # ------------------------------------------------------------------------------------------------
+def _device_map():
+    """HIP devices the *_parallel methods spread sources over: all visible GPUs, or the list in
+    ALIFMM_DEVICE_MAP (e.g. "0,0,0": three independent contexts, streams and field sets on GPU 0 —
+    the multi-GPU sharding path exercised on a one-GPU box)."""
+    m = os.environ.get("ALIFMM_DEVICE_MAP")
+    if m:
+        return [int(d) for d in m.split(",") if d.strip() != ""]
+    return list(range(_alifmm.device_count()))
+
+
+# ------------------------------------------------------------------------------------------------
 # model hashing (re-upload only when the arrays change)
 def _digest(*arrays):
     import xxhash
@@ -315,14 +326,15 @@ class ALI_FMM:
 
     # ---- GPU plumbing ----
     def _ctx(self, device=0):
+        """Context of logical GPU `device` (an index into _device_map())."""
         c = self._ctxs.get(device)
         if c is None:
-            c = _alifmm.Context(device)
+            c = _alifmm.Context(_device_map()[device])
             self._ctxs[device] = c
         return c
 
     def _devices(self, n_threads):
-        n = max(1, min(int(n_threads), _alifmm.device_count()))
+        n = max(1, min(int(n_threads), len(_device_map())))
         return list(range(n))
 
     def _fields(self, veln, velpn, vel_map, stif_den, subgrid_size, idx, devices, copy_out=True, slot_of=None):

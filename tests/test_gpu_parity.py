@@ -318,3 +318,34 @@ def test_pair_kernel_identical_to_single_workgroup(ctx):
     Bf = ctx.travel(scx[[0, 46]], scz[[0, 46]], subgrid=3)
     ctx.set_option("pair", 1)
     assert np.array_equal(A, Bf)
+
+
+def test_sharded_contexts_bit_identical(A, monkeypatch):
+    """per-source outputs are bit-identical whatever the number of GPUs the sources
+    are dealt over.  ALIFMM_DEVICE_MAP=0,0,0 gives the *_parallel methods three independent
+    contexts (streams, resident fields, host threads) on the box's one GPU, i.e. the multi-GPU
+    sharding path (sharding.deal, rays traced where the receiver's field lives)."""
+    veln, velpn, vm, sd = W.weld_model()
+    velpn = velpn.astype(int)
+    sx, sy = W.weld_transducers()
+    sel = [0, 7, 20, 31, 40, 46, 55, 61]
+    sx, sy = sx[sel], sy[sel]
+    M1 = A.ALI_FMM(veln, velpn, vm, sx, sy, stif_den=sd, dnx=0.0002)
+    F1 = M1.update(veln, velpn, vm, stif_den=sd, subgrid_size=1)
+    monkeypatch.setenv("ALIFMM_DEVICE_MAP", "0,0,0")
+    M3 = A.ALI_FMM(veln, velpn, vm, sx, sy, stif_den=sd, dnx=0.0002)
+    assert M3._devices(8) == [0, 1, 2]
+    F3 = M3.update_parallel(veln, velpn, vm, stif_den=sd, subgrid_size=1, n_threads=3)
+    np.testing.assert_array_equal(F3, F1)
+    n = len(sel)
+    pairs = np.zeros((n, n))
+    pairs[:4, 4:] = 1  # top transducers -> bottom receivers (Weld_rays.py:52-55)
+    t1 = M1.find_all_TTF_rays(veln, velpn, vm, subgrid_size=1, trans_pairs=pairs, stif_den=sd)
+    t3 = M3.find_all_TTF_rays_parallel(veln, velpn, vm, subgrid_size=1, trans_pairs=pairs, stif_den=sd, n_threads=3)
+    np.testing.assert_array_equal(t3, t1)
+    assert np.all(t1[:4, 4:] > 0)
+    np.testing.assert_array_equal(M3.ray_len, M1.ray_len)
+    for i in range(4):
+        for j in range(4, n):
+            for a, b in zip(M3.ray_path(i, j), M1.ray_path(i, j)):
+                np.testing.assert_array_equal(a, b)
