@@ -349,3 +349,34 @@ def test_sharded_contexts_bit_identical(A, monkeypatch):
         for j in range(4, n):
             for a, b in zip(M3.ray_path(i, j), M1.ray_path(i, j)):
                 np.testing.assert_array_equal(a, b)
+
+
+def test_empty_and_degenerate_requests(A, ctx):
+    """Edge cases of the drop-in surface: no selected sources, no ray pairs, a 1-column grid, a
+    source outside the grid (reference: IndexError-like failure -> the C-ABI's argument error)."""
+    import _alifmm
+
+    n = 41
+    veln = np.zeros((n, n))
+    velpn = np.ones((n, n), dtype=np.int64)
+    vm = np.full((n, n), 5790.0)
+    sx, sz = 1e-3 * np.array([5.0, 20.0, 35.0]), 1e-3 * np.array([0.0, 20.0, 40.0])
+    M = A.ALI_FMM(veln, velpn, vm, sx, sz, dnx=1e-3)
+    F = M.update(veln, velpn, vm, sources=np.zeros(3))
+    assert F.shape == (3, n, n) and not F.any()
+    t = M.find_all_TTF_rays(veln, velpn, vm, subgrid_size=1, trans_pairs=np.zeros((3, 3)))
+    assert t.shape == (3, 3) and not t.any() and not M.ray_len.any()
+    assert M.ray_path(0, 1) == (None, None)
+    # empty batch through the C-ABI
+    vt = W.default_table()
+    ctx.set_model(veln, velpn, vm, None, vt, vt, 1e-3)
+    assert ctx.travel(np.zeros(0), np.zeros(0), copy_out=True).shape[0] == 0
+    # two-column grid (ragged extreme), source in the top corner: against the oracle
+    v2, p2, m2 = np.zeros((n, 2)), np.ones((n, 2), dtype=np.int64), np.full((n, 2), 5790.0)
+    T = A.travel(0.0, 0.0, None, None, 0, np.zeros((n, 2)), v2, p2, m2, None, vt, vt, 0, 0, 1e-3, 1e-3, 2, n)
+    R = O.travel(0.0, 0.0, v2, p2, m2, None, vt, vt, dnx=1e-3)
+    mx, mean = _field_err(T, R, (0, 0))
+    assert mx <= FIELD_MAX and mean <= FIELD_MEAN, (mx, mean)
+    # a source outside the grid is an argument error, not a fault
+    with pytest.raises(_alifmm.AlifmmError):
+        ctx.travel(np.array([1.0]), np.array([0.0]))
