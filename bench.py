@@ -64,7 +64,10 @@ def main():
     veln, velpn, vel_map, stif = W.weldlike_model(n)
     dnx = W.weldlike_dnx()
     vt = W.default_table()
-    ctx = _alifmm.Context(local)
+    # one GPU per rank (LOCAL_RANK); ALIFMM_BENCH_DEVICE pins every rank to one device, only to
+    # rehearse the multi-process path on a one-GPU box
+    dev = int(os.environ.get("ALIFMM_BENCH_DEVICE", local))
+    ctx = _alifmm.Context(dev)
     if args.cdelta is not None:
         ctx.set_option("cdelta", args.cdelta)
     if args.exact_r is not None:
@@ -98,7 +101,11 @@ def main():
     band_avg_s = band_ms / args.steps / 1e3
     achieved = BYTES_PER_SWEEP * sweeps / band_avg_s / 1e9 if band_avg_s > 0 else None
 
-    traffic = traffic_bytes = None  # HBM-side bytes per launch (PMC passes of tools/profile.sh, this library)
+    config = {"workload": "C4: %dx%d weld-like, %d top-surface Tx sources per GPU, subgrid 1" % (n, n, args.sources),
+              "sources_per_gpu": args.sources, "total_sources": args.sources * world, "grid": [n, n], "subgrid": 1,
+              "cdelta": args.cdelta, "exact_r": args.exact_r}
+    # HBM-side bytes per launch: PMC passes of tools/profile.sh on this library AND this workload
+    traffic = traffic_bytes = None
     try:
         import glob
         import hashlib
@@ -106,7 +113,8 @@ def main():
         lib_sha = hashlib.sha256(open(_alifmm.LIB_PATH, "rb").read()).hexdigest()
         for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json"))):
             t = json.load(open(f))
-            if t.get("libalifmm_sha256") == lib_sha and t.get("traffic_bytes_per_launch"):
+            if (t.get("libalifmm_sha256") == lib_sha and t.get("traffic_bytes_per_launch")
+                    and t.get("bench_config") == {k: v for k, v in config.items() if k != "total_sources"}):
                 traffic_bytes = t["traffic_bytes_per_launch"]
                 traffic = traffic_bytes / band_avg_s / 1e9  # GB/s over the same launch time as achieved
     except OSError:
@@ -146,8 +154,7 @@ def main():
             "dtype": "f64",
             "data": "synthetic: weld-like model built from the reference's weld_*.npy (edge-padded, 8x nearest), "
                     "stiffness row of the notebook",
-            "config": {"workload": "C4: %dx%d weld-like, %d top-surface Tx sources per GPU, subgrid 1" % (n, n, args.sources),
-                       "sources_per_gpu": args.sources, "total_sources": total_src, "grid": [n, n], "subgrid": 1},
+            "config": config,
             "sources_per_s": total_src * args.steps / dt,
             "kernel_ms_per_step": {"fmm_init_kernel": init_ms / args.steps, band_kernel: band_ms / args.steps},
             "band_steps_main_mean": float(np.mean(steps_main)),

@@ -34,6 +34,21 @@ def per_launch(d, counter):
 fetch_kb = per_launch("pmc_fetch", "FETCH_SIZE")
 write_kb = per_launch("pmc_write", "WRITE_SIZE")
 lib = os.path.join(repo, "ali-fmm-and-ray-tracing_amd", "lib", "libalifmm.so")
+# the workload the passes profiled (the bench line each pass printed): bench.py applies the
+# figure only to a run of the same configuration
+bench_config = None
+for f in ("pmc_fetch.log", "pmc_write.log"):
+    try:
+        line = [l for l in open(os.path.join(out, f)) if l.startswith('{"metric"')][-1]
+        cfg = json.loads(line)["config"]
+        cfg.pop("total_sources", None)  # per-GPU workload: the same launch at any world size
+        cfg.setdefault("cdelta", None)  # bench lines before these keys ran the defaults
+        cfg.setdefault("exact_r", None)
+        if bench_config is not None and cfg != bench_config:
+            sys.exit("FETCH and WRITE passes profiled different workloads: %s vs %s" % (bench_config, cfg))
+        bench_config = cfg
+    except (OSError, IndexError):
+        pass
 res = {
     "kernel": "fmm_band_pair_kernel / fmm_band_kernel (the band kernel of the run)",
     "fetch_size_kb_per_launch": fetch_kb,
@@ -42,6 +57,7 @@ res = {
     "correction": "read = 2 x FETCH_SIZE (gfx950 128-B requests tallied at 64 B), write = WRITE_SIZE; "
                   "L2 memory-side requests (Infinity-Cache hits included)",
     "libalifmm_sha256": hashlib.sha256(open(lib, "rb").read()).hexdigest(),
+    "bench_config": bench_config,
 }
 json.dump(res, open(os.path.join(repo, "profiles", tag + "_traffic.json"), "w"), indent=1)
 print(json.dumps(res))
