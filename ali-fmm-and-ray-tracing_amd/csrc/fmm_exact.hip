@@ -57,7 +57,8 @@ struct XHeap {
       }
     }
   }
-  AF_DEV void add(int c) {
+  // key = the node's ttn; the relaxation passes the value it has just stored (no reload of T[c])
+  AF_DEV void add(int c, double key) {
     ntr += 1;
     if (ntr >= kXHeap) {
       err = 3;
@@ -66,12 +67,13 @@ struct XHeap {
     }
     S[c] = ntr;
     H->cell[ntr] = c;
-    H->key[ntr] = T[c];
+    H->key[ntr] = key;
     sift_up(c, ntr);
   }
-  AF_DEV void upd(int c) {
-    const int tpc = S[c];
-    H->key[tpc] = T[c];
+  AF_DEV void add(int c) { add(c, T[c]); }
+  // tpc: the node's heap index (its status, read by the caller before the relaxation)
+  AF_DEV void upd(int c, int tpc, double key) {
+    H->key[tpc] = key;
     sift_up(c, tpc);
   }
   AF_DEV void down() {
@@ -138,38 +140,38 @@ AF_DEV long long xloop(XHeap& h, const DevModel& M, const XGrid& g, bool stage, 
     const int c = h.H->cell[1];
     if (tstop > 0 && h.H->key[1] >= tstop) break;
     const int iz = c / nx, ix = c - iz * nx;
+    // the four neighbours' statuses in one round trip, issued before downtree: downtree and the
+    // add / upd of earlier neighbours only move heap indices (positive stays positive) and touch
+    // no other neighbour's far / known state, so the reference's per-neighbour classification
+    // (far -1 -> add, close > 0 -> upd, known 0 -> skip) can be read up front.  (Prefetching the
+    // neighbours' whole stencils as well was measured slower: most neighbours are known.)
+    const int nbz[4] = {iz, iz, iz - 1, iz + 1}, nbx[4] = {ix - 1, ix + 1, ix, ix};
+    bool inb[4];
+    int st[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      inb[k] = k < 2 ? (0 <= nbx[k] && nbx[k] <= nx - 1) : (0 <= nbz[k] && nbz[k] <= nz - 1);
+      st[k] = g.S[inb[k] ? nbz[k] * nx + nbx[k] : c];  // branch-free: the 4 loads issue together
+    }
     g.S[c] = 0;
     h.down();
     pops++;
-    for (int s = 0; s < 2; s++) {
-      const int i = s == 0 ? ix - 1 : ix + 1;
-      if (0 <= i && i <= nx - 1) {
-        const int r = iz * nx + i;
-        const int st = g.S[r];
-        if (st == -1) {
-          g.T[r] = xrelax(M, g, iz, i);
-          h.add(r);
-        } else if (st > 0) {
-          g.T[r] = xrelax(M, g, iz, i);
-          h.upd(r);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      if (inb[k]) {
+        const int r = nbz[k] * nx + nbx[k];
+        if (st[k] == -1) {
+          const double v = xrelax(M, g, nbz[k], nbx[k]);
+          g.T[r] = v;
+          h.add(r, v);
+        } else if (st[k] > 0) {
+          // the heap index read up front is still the node's: only earlier neighbours' sift-ups
+          // move heap entries in between, and they may move this node — re-read it from S then
+          const double v = xrelax(M, g, nbz[k], nbx[k]);
+          g.T[r] = v;
+          h.upd(r, g.S[r], v);
         }
-      } else if (stage && abs(isx_s - i) == max_dist + 1) {
-        finished = true;
-      }
-    }
-    for (int s = 0; s < 2; s++) {
-      const int i = s == 0 ? iz - 1 : iz + 1;
-      if (0 <= i && i <= nz - 1) {
-        const int r = i * nx + ix;
-        const int st = g.S[r];
-        if (st == -1) {
-          g.T[r] = xrelax(M, g, i, ix);
-          h.add(r);
-        } else if (st > 0) {
-          g.T[r] = xrelax(M, g, i, ix);
-          h.upd(r);
-        }
-      } else if (stage && abs(isz_s - i) == max_dist + 1) {
+      } else if (stage && (k < 2 ? abs(isx_s - nbx[k]) : abs(isz_s - nbz[k])) == max_dist + 1) {
         finished = true;
       }
     }
