@@ -119,7 +119,8 @@ struct RunCfg {
 template <bool LDSMAT>
 AF_DEV CellMat band_mat(const DevModel& M, const MatRec* mat, const double* stab, const MatView& v, int z, int x) {
   if (!LDSMAT) return cell_mat(M, v, z, x);
-  const MatRec m = mat[gld(M.mid + mv_cell(M, v, z, x))];
+  const long i = mv_cell(M, v, z, x);
+  const MatRec m = mat[M.mid8 ? (int)gld(M.mid8 + i) : gld(M.mid + i)];
   CellMat r;
   r.velpn = m.velpn;
   r.veln = v.quant ? (double)(int)m.veln : m.veln;

@@ -83,6 +83,7 @@ struct DevModel {
   const double* ptab;    // phase velocity table (361, ncol)
   int ncol;
   const int* mid;        // material id per cell (into mtab), or nullptr when there are too many
+  const unsigned char* mid8;  // the same ids as bytes when nmat <= 256, else nullptr
   const MatRec* mtab;
   int nmat;
   const double* mslo;     // per material and MatView::quant: fouds18_A()'s 4 slownesses [nmat][2][4], or nullptr
