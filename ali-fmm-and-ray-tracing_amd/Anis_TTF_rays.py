@@ -78,11 +78,44 @@ def _prep_model(veln, velpn, vel_map, stif_den, group_tab, phase_tab):
     return veln, velpn, vel_map, stif, gt, pt
 
 
+def _identity(a):
+    """Cheap identity of a model argument: the object, its buffer, shape, dtype and strides, plus a
+    digest of a strided sample of ~4096 elements (so that an in-place edit of a sampled element,
+    or of the first or last row, is noticed without hashing the whole array)."""
+    if a is None:
+        return None
+    if not isinstance(a, np.ndarray):
+        return ("obj", _digest(np.asarray(a)))
+    flat = a.reshape(-1) if a.flags.c_contiguous else np.ravel(a)
+    step = max(1, flat.size // 4096)
+    edge = min(flat.size, a.shape[-1] if a.ndim else 1)
+    return (id(a), a.__array_interface__["data"][0], a.shape, a.dtype.str, a.strides,
+            _digest(flat[::step], flat[:edge], flat[flat.size - edge:]))
+
+
+# identity of the model arguments -> full content digest: module-level calls (travel, find_ray, ...)
+# pass the same arrays over and over; each pass would otherwise re-hash up to ~1 GB (C4 stiffness)
+_digest_cache = {}
+
+
+def _model_digest(arrays):
+    ident = tuple(_identity(a) for a in arrays)
+    d = _digest_cache.get(ident)
+    if d is None:
+        d = _digest(*_prep_model(*arrays))
+        if len(_digest_cache) >= 8:
+            _digest_cache.pop(next(iter(_digest_cache)))
+        _digest_cache[ident] = d
+    return d
+
+
 def _load_model(ctx, veln, velpn, vel_map, stif_den, group_tab, phase_tab, dnx, dnz, gox=0.0, goz=0.0):
-    veln, velpn, vel_map, stif, gt, pt = _prep_model(veln, velpn, vel_map, stif_den, group_tab, phase_tab)
-    key = (_digest(veln, velpn, vel_map, stif, gt, pt), float(dnx), float(dnz), float(gox), float(goz))
-    ctx.set_model(veln, velpn, vel_map, stif, gt, pt, dnx, dnz, gox, goz, key=key)
-    return veln.shape
+    args = (veln, velpn, vel_map, stif_den, group_tab, phase_tab)
+    key = (_model_digest(args), float(dnx), float(dnz), float(gox), float(goz))
+    if ctx.model_key != key:
+        veln, velpn, vel_map, stif, gt, pt = _prep_model(*args)
+        ctx.set_model(veln, velpn, vel_map, stif, gt, pt, dnx, dnz, gox, goz, key=key)
+    return np.shape(veln)
 
 
 _module_ctx = None
@@ -121,9 +154,18 @@ def finer_grid_n_2(data, scale):
     return data[iz][:, ix].astype(np.int64)
 
 
-def _sincos(x):
-    """sin(x), cos(x) from libm's sincos(): numba (LLVM) fuses the reference's sin(2 pa) / cos(2 pa)
-    pair into one sincos() call, which can differ from separate sin() by an ulp."""
+# ------------------------------------------------------------------------------------------------
+# Christoffel velocities of a 2D orthotropic medium (host side).  The reference spells the same
+# closed forms out four times: the module function group_vel (:3521-3558, compiled by numba) and
+# the class's table generators generate_group_vel / generate_phase_vel (:4112-4206, plain
+# Python).  Here one off-axis formula per velocity serves both; every value keeps the reference's
+# operation order, so the tables and group_vel are bit-identical to the reference's
+# (tests/test_host.py pins both against reference-generated vectors).  The one difference
+# between the two callers is how sin/cos of the same argument are evaluated: numba fuses the
+# pair into one libm sincos() call (which can differ from separate sin()/cos() by an ulp), plain
+# Python calls them separately.
+def _libm_sincos(x):
+    """sin(x), cos(x) through libm's sincos() (what numba emits for a sin/cos pair)."""
     import ctypes
     import ctypes.util
 
@@ -140,26 +182,48 @@ def _sincos(x):
 _libm = None
 
 
+def _math_sincos(x):
+    return math.sin(x), math.cos(x)
+
+
+def _group_off_axis(theta, c22, c23, c33, c44, rho, scale, sincos):
+    """Group velocity at group angle theta [deg] away from the symmetry axes: the phase angle
+    solves the Christoffel quadratic (root on the group angle's side of 90 deg), then
+    v = scale * sqrt(lambda / rho) / cos(theta - phase)."""
+    t = math.tan(math.radians(theta))
+    a_ = c22 + c33 - 2 * c44
+    b_ = (c23 + c44) * (t - 1 / t)
+    c_ = c22 - c33
+    root = math.sqrt(b_ ** 2 + a_ ** 2 - c_ ** 2)
+    phase = math.atan(((-b_ - root) if theta < 90 else (-b_ + root)) / (c_ - a_)) % math.pi
+    s2, c2 = sincos(2 * phase)
+    lam = 0.5 * (c2 * (c22 - c44) + s2 * (c23 + c44) * t + c22 + c44)
+    return scale * math.sqrt(lam / rho) / math.cos(math.radians(theta) - phase)
+
+
+def _phase_off_axis(theta, c22, c23, c33, c44, rho):
+    """Phase velocity at phase angle theta [deg]: the larger Christoffel eigenvalue over rho."""
+    ca, sa = math.cos(math.radians(theta)), math.sin(math.radians(theta))
+    a_ = ca ** 2 * c22 + sa ** 2 * c44
+    b_ = ca * sa * (c23 + c44)
+    c_ = ca ** 2 * c44 + sa ** 2 * c33
+    return math.sqrt((a_ + c_ + math.sqrt((a_ - c_) ** 2 + 4 * b_ ** 2)) / (2 * rho))
+
+
+def _velocity_table(off_axis, c22, c33, rho):
+    """361-row table over 0..360 deg in 1-deg steps: on the axes sqrt(c22 / rho) (0 deg) or
+    sqrt(c33 / rho) (90 deg), off-axis `off_axis(angle)`; the curve repeats every 180 deg."""
+    half = [math.sqrt((c33 if a == 90 else c22) / rho) if a % 90 == 0 else off_axis(a) for a in range(180)]
+    return np.array(half + half + half[:1])
+
+
 def group_vel(angle, c_22, c_23, c_33, c_44, sigma, vel_scale=1):
-    """Closed-form 2D orthotropic Christoffel group velocity (reference :3521-3558, a numba
-    function: sin/cos of the same argument go through sincos(), as numba compiles them)."""
-    if angle % 90 < 0.01 or angle % 90 > 90 - 0.01:
-        if abs((angle % 180) - 90) < 1:
-            lambda_val = c_33
-        else:
-            lambda_val = c_22
-        return 1000 * vel_scale * math.sqrt(lambda_val / sigma)
-    tan_ang = math.tan(math.radians(angle))
-    A = c_22 + c_33 - 2 * c_44
-    B = (c_23 + c_44) * (tan_ang - 1 / tan_ang)
-    C = c_22 - c_33
-    if angle < 90:
-        phase_angle_rad = math.atan((-B - math.sqrt(B ** 2 + A ** 2 - C ** 2)) / (C - A)) % math.pi
-    else:
-        phase_angle_rad = math.atan((-B + math.sqrt(B ** 2 + A ** 2 - C ** 2)) / (C - A)) % math.pi
-    s2, c2 = _sincos(2 * phase_angle_rad)
-    lambda_val = 0.5 * (c2 * (c_22 - c_44) + s2 * (c_23 + c_44) * tan_ang + c_22 + c_44)
-    return 1000 * vel_scale * math.sqrt(lambda_val / sigma) / math.cos(math.radians(angle) - phase_angle_rad)
+    """Closed-form 2D orthotropic Christoffel group velocity (reference :3521-3558): within
+    0.01 deg of an axis the on-axis value (c_33 near 90 deg, else c_22), else the off-axis form."""
+    a90 = angle % 90
+    if a90 < 0.01 or a90 > 90 - 0.01:
+        return 1000 * vel_scale * math.sqrt((c_33 if abs((angle % 180) - 90) < 1 else c_22) / sigma)
+    return _group_off_axis(angle, c_22, c_23, c_33, c_44, sigma, 1000 * vel_scale, _libm_sincos)
 
 
 def min_max_vel(veln, velpn, vel_map, stif_den, group_vel_table):
@@ -274,55 +338,62 @@ class ALI_FMM:
     spreads the sources of the *_parallel methods over the visible GPUs).
     """
 
-    def __init__(self, veln, velpn, vel_map, scx, scz, group_vel=None, phase_vel=None, stif_den=None, dnx=1e-3):
-        self.stif_den = stif_den
-        if type(stif_den) != type(None):
-            if type(stif_den[0, 0, 0]) != np.int64:
-                raise TypeError("Stifness tensors and density array must have the type np.int64. 32bit integers will "
-                                "not work correctly.")
-            elif stif_den[0, 0, 0] > 1e9:
-                print("Warning: Stifness tensors must be in MPa, due to 64 bit integer limitations when solving the "
+    _STIF_TYPE_MSG = ("Stifness tensors and density array must have the type np.int64. 32bit integers will not "
+                      "work correctly.")
+    _STIF_UNIT_MSG = ("Warning: Stifness tensors must be in MPa, due to 64 bit integer limitations when solving the "
                       "christoffel equation")
-        if type(group_vel) == type(None):
-            self.velocity_dat = 1 * np.ones((361, 2))
-            self.velocity_dat[:, 0] = np.arange(0, 361)
-            self.phase_vel = np.copy(self.velocity_dat)
+    _VELPN_MSG = "velpn must be a numpy array of integers"
+
+    def __init__(self, veln, velpn, vel_map, scx, scz, group_vel=None, phase_vel=None, stif_den=None, dnx=1e-3):
+        # validation order and messages as the reference's (:3818-3838): stiffness first, then velpn
+        self._check_stiffness(stif_den)
+        if group_vel is None:  # isotropic unit curves; vel_map scales them per cell
+            self.velocity_dat, self.phase_vel = self._unit_tables()
         else:
-            self.velocity_dat = group_vel
-            self.phase_vel = phase_vel
-        self.veln = veln
-        self.velpn = velpn
-        try:
-            if np.issubdtype(velpn[0, 0], np.integer) == False:  # noqa: E712
-                raise TypeError("velpn must be a numpy array of integers")
-        except Exception:
-            raise TypeError("velpn must be a numpy array of integers")
-        self.vel_map = vel_map
-        self.dnx = dnx
-        self.dnz = dnx
-        self.nnx = veln.shape[1]
-        self.nnz = veln.shape[0]
+            self.velocity_dat, self.phase_vel = group_vel, phase_vel
+        self._check_material_index(velpn)
+        self.stif_den, self.veln, self.velpn, self.vel_map = stif_den, veln, velpn, vel_map
+        self.dnx = self.dnz = dnx
+        self.nnz, self.nnx = veln.shape[0], veln.shape[1]
         self.ttn = np.zeros(veln.shape)
-        self.scx = scx
-        self.scz = scz
-        self.gox = 0
-        self.goz = 0
-        self.isx = np.zeros(len(scx))
-        self.isz = np.zeros(len(scx))
-        for i in range(len(scx)):
-            self.isx[i] = round((scx[i] - self.gox) / self.dnx)
-            self.isz[i] = round((scz[i] - self.goz) / self.dnz)
-        self.ntr = 0
+        self.scx, self.scz = scx, scz
+        self.gox = self.goz = 0
+        # transducer nodes: Python round() (half-even) of the grid coordinate, kept as floats
+        self.isx = np.array([float(round((x - self.gox) / self.dnx)) for x in scx])
+        self.isz = np.array([float(round((z - self.goz) / self.dnz)) for z in scz])
         self.nsrc = len(scx)
-        # The reference's CPU heap buffers (nsts, btg) are not used: the GPU owns its work lists.
+        self.ntr = 0
+        # the reference's CPU heap buffers (nsts, btg) have no counterpart: the GPU keeps its own
         self.maxbt = round(0.5 * self.nnx * self.nnz)
-        self.nsts = None
-        self.btg = None
-        self.ray_paths_x = None
-        self.ray_paths_y = None
-        self.ray_len = None
+        self.nsts = self.btg = None
+        self.ray_paths_x = self.ray_paths_y = self.ray_len = None
         self.rays = None  # RayStore of the last find_all_TTF_rays* call (compact layout)
         self._ctxs = {}
+
+    @classmethod
+    def _check_stiffness(cls, stif_den):
+        if stif_den is None:
+            return
+        first = stif_den[0, 0, 0]
+        if type(first) != np.int64:
+            raise TypeError(cls._STIF_TYPE_MSG)
+        if first > 1e9:
+            print(cls._STIF_UNIT_MSG)
+
+    @classmethod
+    def _check_material_index(cls, velpn):
+        try:
+            integral = np.issubdtype(velpn[0, 0], np.integer)
+        except Exception:
+            integral = False
+        if not integral:
+            raise TypeError(cls._VELPN_MSG)
+
+    @staticmethod
+    def _unit_tables():
+        t = np.ones((361, 2))
+        t[:, 0] = np.arange(0, 361)
+        return t, t.copy()
 
     # ---- GPU plumbing ----
     def _ctx(self, device=0):
@@ -354,6 +425,8 @@ class ALI_FMM:
                 x = np.array([float(self.scx[i]) for i in ids])
                 z = np.array([float(self.scz[i]) for i in ids])
                 out = ctx.travel(x, z, subgrid=int(subgrid_size), first_slot=0, copy_out=copy_out)
+                if copy_out:  # the host has the fields: free their device slots
+                    ctx.release_fields()
                 for k, i in enumerate(ids):
                     results[i] = (dev, k, None if out is None else out[k])
             except Exception as e:  # surfaced below
@@ -439,117 +512,60 @@ class ALI_FMM:
         plt.polar(math.pi / 180 * self.velocity_dat[:, 0], self.velocity_dat[:, material_index])
         plt.show()
 
-    def generate_group_vel(self, c_22, c_23, c_33, c_44, density, plot=True):
-        """Group velocity table 0..360 deg (reference :4112-4160)."""
-        group_vel = np.zeros(361)
-        for angle in range(361):
-            if angle < 180:
-                if angle % 90 == 0:
-                    lambda_val = c_33 if angle % 180 == 90 else c_22
-                    velocity = math.sqrt(lambda_val / density)
-                else:
-                    tan_ang = math.tan(math.radians(angle))
-                    A = c_22 + c_33 - 2 * c_44
-                    B = (c_23 + c_44) * (tan_ang - 1 / tan_ang)
-                    C = c_22 - c_33
-                    if angle < 90:
-                        phase_angle_rad = math.atan((-B - math.sqrt(B ** 2 + A ** 2 - C ** 2)) / (C - A)) % math.pi
-                    else:
-                        phase_angle_rad = math.atan((-B + math.sqrt(B ** 2 + A ** 2 - C ** 2)) / (C - A)) % math.pi
-                    lambda_val = 0.5 * (math.cos(2 * phase_angle_rad) * (c_22 - c_44) + math.sin(2 * phase_angle_rad) *
-                                        (c_23 + c_44) * tan_ang + c_22 + c_44)
-                    velocity = math.sqrt(lambda_val / density) / math.cos(math.radians(angle) - phase_angle_rad)
-                group_vel[angle] = velocity
-            else:
-                group_vel[angle] = group_vel[angle - 180]
-        if plot == True:  # noqa: E712
-            import matplotlib.pyplot as plt
+    @staticmethod
+    def _plot_table(values, title):
+        import matplotlib.pyplot as plt
 
-            plt.polar(math.pi / 180 * np.arange(0, 361), group_vel)
-            plt.title("Group Velocity")
-            plt.show()
-        return group_vel
+        plt.polar(math.pi / 180 * np.arange(0, 361), values)
+        plt.title(title)
+        plt.show()
+
+    def generate_group_vel(self, c_22, c_23, c_33, c_44, density, plot=True):
+        """Group velocity table over 0..360 deg (reference :4112-4160)."""
+        table = _velocity_table(lambda a: _group_off_axis(a, c_22, c_23, c_33, c_44, density, 1, _math_sincos),
+                                c_22, c_33, density)
+        if plot == True:  # noqa: E712
+            self._plot_table(table, "Group Velocity")
+        return table
 
     def generate_phase_vel(self, c_22, c_23, c_33, c_44, density, plot=True):
-        """Phase velocity table 0..360 deg (reference :4162-4206)."""
-        phase_vel = np.zeros(361)
-        for angle in range(361):
-            if angle < 180:
-                if angle % 90 == 0:
-                    lambda_val = c_33 if angle % 180 == 90 else c_22
-                    velocity = math.sqrt(lambda_val / density)
-                else:
-                    cos_ang = math.cos(math.radians(angle))
-                    sin_ang = math.sin(math.radians(angle))
-                    A = cos_ang ** 2 * c_22 + sin_ang ** 2 * c_44
-                    B = cos_ang * sin_ang * (c_23 + c_44)
-                    C = cos_ang ** 2 * c_44 + sin_ang ** 2 * c_33
-                    velocity = math.sqrt((A + C + math.sqrt((A - C) ** 2 + 4 * B ** 2)) / (2 * density))
-                phase_vel[angle] = velocity
-            else:
-                phase_vel[angle] = phase_vel[angle - 180]
+        """Phase velocity table over 0..360 deg (reference :4162-4206)."""
+        table = _velocity_table(lambda a: _phase_off_axis(a, c_22, c_23, c_33, c_44, density), c_22, c_33, density)
         if plot == True:  # noqa: E712
-            import matplotlib.pyplot as plt
-
-            plt.polar(math.pi / 180 * np.arange(0, 361), phase_vel)
-            plt.title("Phase Velocity")
-            plt.show()
-        return phase_vel
+            self._plot_table(table, "Phase Velocity")
+        return table
 
     def add_materials(self, materials, keep_materials=False):
-        """Append (or replace) table materials from stiffness/density rows (reference :4208-4256,
-        including its column-count behaviour for 2D input without keep_materials, SURVEY B-D10)."""
+        """Table materials from stiffness/density rows [c22, c23, c33, c44, density] (reference
+        :4208-4256): appended after the current columns (keep_materials=True) or replacing them
+        (column 0 = angle).  The reference's column counts are kept as they are: 2D input adds
+        materials.shape[1] columns when appending, and without keep_materials it sizes the tables
+        and iterates by materials.shape[1] (SURVEY B-D10)."""
+        single = materials.ndim == 1
         if keep_materials == True:  # noqa: E712
-            if materials.ndim == 1:
-                group_vel_data = np.zeros((361, self.velocity_dat.shape[1] + 1))
-                group_vel_data[:, 0:self.velocity_dat.shape[1]] = self.velocity_dat
-                group_vel_data[:, group_vel_data.shape[1] - 1] = self.generate_group_vel(
-                    materials[0], materials[1], materials[2], materials[3], materials[4], False)
-                phase_vel_data = np.zeros((361, self.phase_vel.shape[1] + 1))
-                phase_vel_data[:, 0:self.velocity_dat.shape[1]] = self.phase_vel
-                phase_vel_data[:, group_vel_data.shape[1] - 1] = self.generate_phase_vel(
-                    materials[0], materials[1], materials[2], materials[3], materials[4], False)
-                print("material id of new material is " + str(self.velocity_dat.shape[1]))
-            else:
-                group_vel_data = np.zeros((361, self.velocity_dat.shape[1] + materials.shape[1]))
-                group_vel_data[:, 0:self.velocity_dat.shape[1]] = self.velocity_dat
-                phase_vel_data = np.zeros((361, self.velocity_dat.shape[1] + materials.shape[1]))
-                phase_vel_data[:, 0:self.velocity_dat.shape[1]] = self.phase_vel
-                for i in range(materials.shape[0]):
-                    index = i + self.velocity_dat.shape[1]
-                    group_vel_data[:, index] = self.generate_group_vel(materials[i, 0], materials[i, 1],
-                                                                       materials[i, 2], materials[i, 3],
-                                                                       materials[i, 4], False)
-                    phase_vel_data[:, index] = self.generate_phase_vel(materials[i, 0], materials[i, 1],
-                                                                       materials[i, 2], materials[i, 3],
-                                                                       materials[i, 4], False)
-                print("material id's of new materials are " + str(self.velocity_dat.shape[1]) + " - " +
-                      str(self.velocity_dat.shape[1] + materials.shape[0] - 1))
+            width = self.velocity_dat.shape[1]
+            extra = 1 if single else materials.shape[1]
+            group = np.zeros((361, width + extra))
+            phase = np.zeros((361, (self.phase_vel.shape[1] if single else width) + extra))
+            group[:, 0:width] = self.velocity_dat
+            phase[:, 0:width] = self.phase_vel
+            first, count = width, 1 if single else materials.shape[0]
         else:
-            if materials.ndim == 1:
-                group_vel_data = np.zeros((361, 2))
-                phase_vel_data = np.zeros((361, 2))
+            width = 2 if single else materials.shape[1] + 1
+            group, phase = np.zeros((361, width)), np.zeros((361, width))
+            group[:, 0] = phase[:, 0] = np.arange(0, 361)
+            first, count = 1, 1 if single else materials.shape[1]
+        for k in range(count):
+            m = materials if single else materials[k]
+            group[:, first + k] = self.generate_group_vel(m[0], m[1], m[2], m[3], m[4], False)
+            phase[:, first + k] = self.generate_phase_vel(m[0], m[1], m[2], m[3], m[4], False)
+        if keep_materials == True:  # noqa: E712
+            if single:
+                print("material id of new material is " + str(first))
             else:
-                group_vel_data = np.zeros((361, materials.shape[1] + 1))
-                phase_vel_data = np.zeros((361, materials.shape[1] + 1))
-            group_vel_data[:, 0] = np.arange(0, 361)
-            phase_vel_data[:, 0] = np.arange(0, 361)
-            if materials.ndim == 1:
-                group_vel_data[:, 1] = self.generate_group_vel(materials[0], materials[1], materials[2], materials[3],
-                                                               materials[4], False)
-                phase_vel_data[:, 1] = self.generate_phase_vel(materials[0], materials[1], materials[2], materials[3],
-                                                               materials[4], False)
-            else:
-                for i in range(materials.shape[1]):
-                    index = i + 1
-                    group_vel_data[:, index] = self.generate_group_vel(materials[i, 0], materials[i, 1],
-                                                                       materials[i, 2], materials[i, 3],
-                                                                       materials[i, 4], False)
-                    phase_vel_data[:, index] = self.generate_phase_vel(materials[i, 0], materials[i, 1],
-                                                                       materials[i, 2], materials[i, 3],
-                                                                       materials[i, 4], False)
-        self.velocity_dat = group_vel_data
-        self.phase_vel = phase_vel_data
+                print("material id's of new materials are " + str(first) + " - " + str(first + count - 1))
+        self.velocity_dat = group
+        self.phase_vel = phase
 
     def _rays(self, veln, velpn, vel_map, stif_den, subgrid_size, trans_pairs, save_rays, n_devices, include_self):
         n_trans = len(self.isx)

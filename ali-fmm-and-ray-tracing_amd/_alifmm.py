@@ -21,6 +21,27 @@ class AlifmmError(RuntimeError):
     pass
 
 
+class RayCapacityError(AlifmmError, IndexError):
+    """A ray reached the reference's point capacity 5 (nnz + nnx): the reference writes past its
+    ray arrays there and raises IndexError (Anis_TTF_rays.py:4287, :3440-3442)."""
+
+
+# ray flags (kernels.h RayParams::flags)
+RAY_EARLY_EXIT, RAY_CAPACITY, RAY_BAD_PLANE = 1, 2, 4
+
+
+def check_ray_flags(flags):
+    """Raise for rays the kernel stopped short of the receiver (capacity, empty search plane);
+    bit 0 (the reference's "Travel time to receiver increasing" early exit) is normal output."""
+    flags = np.asarray(flags)
+    bad = np.nonzero(flags & RAY_CAPACITY)[0]
+    if len(bad):
+        raise RayCapacityError("ray %d reached the point capacity 5 (nnz + nnx)" % int(bad[0]))
+    bad = np.nonzero(flags & RAY_BAD_PLANE)[0]
+    if len(bad):
+        raise AlifmmError("ray %d: empty plane-search candidate set" % int(bad[0]))
+
+
 def _load():
     global _lib
     with _lock:
@@ -124,6 +145,11 @@ class Context:
         except Exception:
             pass
 
+    @property
+    def model_key(self):
+        """Key of the resident model (set_model(key=...)), None when unknown."""
+        return self._model_key
+
     def set_option(self, name, value):
         self._chk(lib().alifmm_set_option(self._h, name.encode(), float(value)), "set_option(%s)" % name)
 
@@ -151,6 +177,8 @@ class Context:
         if gt.ndim != 2 or gt.shape[0] != 361 or pt.shape != gt.shape:
             raise ValueError("velocity tables must have shape (361, ncol)")
         dnz = dnx if dnz is None else dnz
+        # forget the resident key first: if the upload fails, the next call must upload again
+        self._model_key = None
         self._chk(lib().alifmm_set_model(self._h, nnz, nnx, _ptr(veln), _ptr(velpn), _ptr(vel_map), _ptr(stif),
                                          _ptr(gt), _ptr(pt), gt.shape[1], float(dnx), float(dnz), float(gox),
                                          float(goz)), "set_model")
@@ -187,13 +215,14 @@ class Context:
     def release_fields(self):
         self._chk(lib().alifmm_release_fields(self._h), "release_fields")
 
-    def find_rays(self, slots, src_xy, rec_xy, with_points=True, packed=False):
+    def find_rays(self, slots, src_xy, rec_xy, with_points=True, packed=False, check=True):
         """Rays through resident receiver fields.
 
         Returns (times, lens, flags, rays): rays is a list of (x, z) arrays per ray, or with
         packed=True one (sum(lens), 2) array of all points in ray order (ray k starts at row
         sum(lens[:k])) — no per-ray copies, and the host buffer is sized exactly (the points wait
-        in the context between alifmm_find_rays and alifmm_take_rays)."""
+        in the context between alifmm_find_rays and alifmm_take_rays).  check: raise
+        (check_ray_flags) for a ray cut short at the point capacity or on an empty search plane."""
         slots = _ci32(slots)
         n = len(slots)
         src_xy = _c64(src_xy).reshape(n, 2)
@@ -204,6 +233,8 @@ class Context:
         keep = with_points and n > 0
         self._chk(lib().alifmm_find_rays(self._h, n, _ptr(slots), _ptr(src_xy), _ptr(rec_xy), _ptr(times),
                                          _ptr(lens), _ptr(flags), None, KEEP_RAYS if keep else 0), "find_rays")
+        if check:
+            check_ray_flags(flags)
         if not with_points:
             return times, lens, flags, None
         npts = int(lens.sum(dtype=np.int64))

@@ -90,7 +90,23 @@ struct alifmm_ctx {
   // per ray in the caller's order, until alifmm_take_rays() copies them out
   std::vector<std::vector<double>> kept_rays;
   int64_t kept_pts = 0;
+  // ray-tracer work buffers, kept across alifmm_find_rays calls (sized for the largest chunk seen)
+  struct RayBufs {
+    size_t pts = 0;  // capacity of rx / ry in doubles
+    int rays = 0;    // capacity of the per-ray arrays
+    double *rx = nullptr, *ry = nullptr, *t = nullptr;
+    int *len = nullptr, *flags = nullptr;
+    af::RayJob* jobs = nullptr;
+    long long* off = nullptr;
+  } rb;
 };
+
+static void free_ray_bufs(alifmm_ctx* c) {
+  auto& b = c->rb;
+  for (void* p : {(void*)b.rx, (void*)b.ry, (void*)b.t, (void*)b.len, (void*)b.flags, (void*)b.jobs, (void*)b.off})
+    if (p) (void)hipFree(p);
+  b = alifmm_ctx::RayBufs();
+}
 
 static int fail(alifmm_ctx* c, int code, const char* fmt, ...) {
   char buf[512];
@@ -149,6 +165,8 @@ static double christoffel_group_host(const double* s, double eff, double vm) {
 
 // material-id table capacity (the band kernel stages <= kMatLds of them in LDS)
 static const int kMaxMatIds = 4096;
+// plane-search candidates per ray the ray kernel holds (rays.hip kMaxCand)
+static const int kMaxRayCand = 256;
 
 extern "C" {
 
@@ -211,6 +229,7 @@ int alifmm_ctx_destroy(alifmm_ctx* ctx) {
   (void)hipStreamSynchronize(ctx->stream);
   alifmm_release_fields(ctx);
   free_arena(ctx->arena);
+  free_ray_bufs(ctx);
   free_model(ctx);
   for (auto& e : ctx->ev) if (e) (void)hipEventDestroy(e);
   if (ctx->fill) {
@@ -260,7 +279,8 @@ int alifmm_set_model(alifmm_ctx* ctx, int nnz, int nnx, const double* veln, cons
     return fail(ctx, ALIFMM_E_ARG, "set_model: bad arguments");
   HIPCHK(hipSetDevice(ctx->device));
   HIPCHK(hipStreamSynchronize(ctx->stream));
-  free_model(ctx);
+  // everything that can reject the model is checked before the resident model is released, so a
+  // rejected call leaves the previous model usable
   const size_t n = (size_t)nnz * nnx;
   std::vector<int> vp(n);
   for (size_t i = 0; i < n; i++) {
@@ -314,6 +334,7 @@ int alifmm_set_model(alifmm_ctx* ctx, int nnz, int nnx, const double* veln, cons
     }
   }
   if (!(vmax > 0)) return fail(ctx, ALIFMM_E_ARG, "model has no positive velocity");
+  free_model(ctx);
   HIPCHK(dalloc(&ctx->d_veln, n));
   HIPCHK(dalloc(&ctx->d_vm, n));
   HIPCHK(dalloc(&ctx->d_velpn, n));
@@ -482,7 +503,8 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
     capL = std::max(capL, std::min(capS, 262144L));
     capC = capL;
   }
-  int rc = ensure_arena(ctx, std::max(n, std::min(ctx->batch, 1)), cells, capL, capC, capS);
+  // the arena is sized for this chunk (reused while later chunks fit in it)
+  int rc = ensure_arena(ctx, n, cells, capL, capC, capS);
   if (rc) return rc;
   Arena& a = ctx->arena;
   // subgrid 1: the fields are first written by the band kernel, so their initialisation runs on
@@ -718,15 +740,32 @@ int alifmm_find_rays(alifmm_ctx* ctx, int npairs, const int32_t* field_slot, con
       return fail(ctx, ALIFMM_E_ARG, "find_rays: ray %d refers to empty slot %d", k, s);
     by_sg[ctx->fields[s].sg].push_back(k);
   }
-  const int chunk = 8192;
-  double *d_rx = nullptr, *d_ry = nullptr, *d_t = nullptr, *d_packed = nullptr;
-  int *d_len = nullptr, *d_flags = nullptr;
-  af::RayJob* d_jobs = nullptr;
-  long long* d_off = nullptr;
+  for (auto& g : by_sg)
+    if (6 * g.first + 3 > kMaxRayCand)  // the plane search keeps <= kMaxRayCand candidates per ray (rays.hip)
+      return fail(ctx, ALIFMM_E_ARG, "find_rays: subgrid %d has %d plane candidates (> %d supported)", g.first,
+                  6 * g.first + 3, kMaxRayCand);
+  // chunk of rays per launch; the point buffers (chunk x max_pts per coordinate) are sized to the
+  // request and kept in the context for the next call
+  const int chunk = std::min(8192, npairs);
+  auto& rb = ctx->rb;
+  if (rb.rays < chunk || rb.pts < (size_t)chunk * max_pts) {
+    free_ray_bufs(ctx);
+    HIPCHK(dalloc(&rb.rx, (size_t)chunk * max_pts));
+    HIPCHK(dalloc(&rb.ry, (size_t)chunk * max_pts));
+    HIPCHK(dalloc(&rb.t, chunk));
+    HIPCHK(dalloc(&rb.len, chunk));
+    HIPCHK(dalloc(&rb.flags, chunk));
+    HIPCHK(dalloc(&rb.jobs, chunk));
+    HIPCHK(dalloc(&rb.off, chunk));
+    rb.rays = chunk;
+    rb.pts = (size_t)chunk * max_pts;
+  }
+  double *d_rx = rb.rx, *d_ry = rb.ry, *d_t = rb.t, *d_packed = nullptr;
+  int *d_len = rb.len, *d_flags = rb.flags;
+  af::RayJob* d_jobs = rb.jobs;
+  long long* d_off = rb.off;
   int rc = ALIFMM_OK;
-  auto cleanup = [&]() {
-    dfree(d_rx); dfree(d_ry); dfree(d_t); dfree(d_len); dfree(d_flags); dfree(d_jobs); dfree(d_off); dfree(d_packed);
-  };
+  auto cleanup = [&]() { dfree(d_packed); };
 #define RCHK(call)                                                                        \
   do {                                                                                    \
     hipError_t e_ = (call);                                                               \
@@ -735,13 +774,6 @@ int alifmm_find_rays(alifmm_ctx* ctx, int npairs, const int32_t* field_slot, con
       return fail(ctx, ALIFMM_E_HIP, "%s: %s", #call, hipGetErrorString(e_));             \
     }                                                                                     \
   } while (0)
-  RCHK(dalloc(&d_rx, (size_t)chunk * max_pts));
-  RCHK(dalloc(&d_ry, (size_t)chunk * max_pts));
-  RCHK(dalloc(&d_t, chunk));
-  RCHK(dalloc(&d_len, chunk));
-  RCHK(dalloc(&d_flags, chunk));
-  RCHK(dalloc(&d_jobs, chunk));
-  RCHK(dalloc(&d_off, chunk));
   std::vector<int64_t> offsets(npairs + 1, 0);
   std::vector<int32_t> lens(npairs, 0);
   std::vector<double> tms(npairs, 0.0);

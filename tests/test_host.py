@@ -193,3 +193,38 @@ def test_ray_store_matches_dense_layout(tmp_path):
     np.testing.assert_array_equal(st2.ray_len, st.ray_len)
     np.testing.assert_array_equal(st2.dense(0), dense[0])
     np.testing.assert_array_equal(st2.dense(1), dense[1])
+
+
+def test_ray_flags_raise():
+    """a ray cut short at the reference's point capacity (the reference raises
+    IndexError there) or on an empty search plane is an error, not a plausible time; the
+    reference's early exit (bit 0) is normal output."""
+    import _alifmm
+
+    _alifmm.check_ray_flags(np.array([0, 1, 0, 1], dtype=np.int32))
+    with pytest.raises(IndexError):
+        _alifmm.check_ray_flags(np.array([0, 2], dtype=np.int32))
+    with pytest.raises(_alifmm.AlifmmError):
+        _alifmm.check_ray_flags(np.array([4, 0], dtype=np.int32))
+
+
+def test_model_key_cache_tracks_content():
+    """Module-level calls reuse the model digest by array identity (no 1 GB re-hash per call),
+    but an in-place edit of the array (sampled elements, first/last row) or a new array changes
+    the key."""
+    import Anis_TTF_rays as A
+
+    rng = np.random.default_rng(3)
+    veln = rng.uniform(0, 180, (64, 80))
+    velpn = np.zeros((64, 80), dtype=np.int64)
+    vm = np.ones((64, 80))
+    vt = np.ones((361, 2))
+    args = [veln, velpn, vm, None, vt, vt]
+    k0 = A._model_digest(args)
+    assert A._model_digest(args) == k0
+    veln[0, 0] += 1.0  # first row
+    k1 = A._model_digest(args)
+    assert k1 != k0
+    veln[-1, -1] += 1.0  # last row
+    assert A._model_digest(args) != k1
+    assert A._model_digest([veln.copy(), velpn, vm, None, vt, vt]) == A._model_digest(args)
