@@ -36,8 +36,14 @@ struct Arena {  // per-chunk scratch, reused across calls
   int* own = nullptr;
   int* ax = nullptr;         // pair mode: 2 exchange lists per source
   af::PairX* px = nullptr;   // pair mode: exchange blocks
-  int* lists = nullptr;    // L0 | L1 | A | C | Cp per source
-  double* dlists = nullptr;  // Lt0 | Lt1 | V per source
+  int* lists = nullptr;    // L0 | L1 | A | C | Cp | L | D | Rx per source
+  double* dlists = nullptr;  // Lt0 | Lt1 | V | Dv per source
+  int K = 0;                 // K-member kernel: members the rim lists are sized for
+  long capR = 0, ecells = 0;
+  int* rimc = nullptr;       // K-member kernel: rim lists [src][K][2][capR]
+  double* rimt = nullptr;
+  double* E = nullptr;       // K-member kernel: edge buffers [src][2][ecells]
+  af::KX* kx = nullptr;      // K-member kernel: exchange blocks
   double* Ts = nullptr;  // stage grids (travel_finer_grid), 2 per source
   int* Ss = nullptr;
   af::BandSrc* srcs = nullptr;
@@ -79,6 +85,10 @@ struct alifmm_ctx {
   int batch = 256;
   int prof = 0;
   int pair = 1;     // two workgroups per source when the chunk fits the device (fmm_band_pair.hip)
+  int kernel = 0;   // band kernel: 0 K-member (fmm_band_k.hip), 1 pair / single (round-1 kernels)
+  int members = 0;  // K-member kernel: workgroups per source (0: as many as the device fits, <= 16)
+  int stripe_log = 6;  // K-member kernel: stripe width log2
+  int last_k = 0;   // members per source of the last band launch
   int n_cu = 0;
   int last_pair = 0;
   long cap_scale = 1;
@@ -134,6 +144,7 @@ static void dfree(void* p) {
 
 static void free_arena(Arena& a) {
   dfree(a.S); dfree(a.own); dfree(a.ax); dfree(a.px); dfree(a.lists); dfree(a.dlists); dfree(a.Ts); dfree(a.Ss); dfree(a.srcs); dfree(a.ho); dfree(a.jobs);
+  dfree(a.rimc); dfree(a.rimt); dfree(a.E); dfree(a.kx);
   dfree(a.dscx); dfree(a.dscz);
   a = Arena();
 }
@@ -252,6 +263,10 @@ int alifmm_set_option(alifmm_ctx* ctx, const char* name, double value) {
   else if (!strcmp(name, "prof")) ctx->prof = value != 0;
   else if (!strcmp(name, "pair")) ctx->pair = value != 0;
   else if (!strcmp(name, "exact_r") && value >= 0 && value <= 48) ctx->exact_r = (int)value;
+  else if (!strcmp(name, "kernel") && (value == 0 || value == 1)) ctx->kernel = (int)value;
+  else if (!strcmp(name, "members") && (value == 0 || value == 1 || value == 2 || value == 4 || value == 8 || value == 16))
+    ctx->members = (int)value;
+  else if (!strcmp(name, "stripe_log") && value >= 3 && value <= 12) ctx->stripe_log = (int)value;
   else return fail(ctx, ALIFMM_E_ARG, "unknown option or bad value: %s=%g", name, value);
   return ALIFMM_OK;
 }
@@ -265,6 +280,10 @@ int alifmm_get_option(alifmm_ctx* ctx, const char* name, double* value) {
   else if (!strcmp(name, "prof")) *value = ctx->prof;
   else if (!strcmp(name, "pair")) *value = ctx->pair;
   else if (!strcmp(name, "last_pair")) *value = ctx->last_pair;
+  else if (!strcmp(name, "kernel")) *value = ctx->kernel;
+  else if (!strcmp(name, "members")) *value = ctx->members;
+  else if (!strcmp(name, "stripe_log")) *value = ctx->stripe_log;
+  else if (!strcmp(name, "last_k")) *value = ctx->last_k;
   else if (!strcmp(name, "n_cu")) *value = ctx->n_cu;
   else return fail(ctx, ALIFMM_E_ARG, "unknown option: %s", name);
   return ALIFMM_OK;
@@ -444,21 +463,33 @@ static af::DevModel dev_model(const alifmm_ctx* c) {
   return M;
 }
 
-static int ensure_arena(alifmm_ctx* ctx, int nsrc, long cells, long capL, long capC, long capS) {
+static int ensure_arena(alifmm_ctx* ctx, int nsrc, long cells, long capL, long capC, long capS, int K, long capR,
+                        long ecells) {
   Arena& a = ctx->arena;
-  if (a.nsrc >= nsrc && a.cells >= cells && a.capL >= capL && a.capC >= capC && a.capS >= capS) return ALIFMM_OK;
+  if (a.nsrc >= nsrc && a.cells >= cells && a.capL >= capL && a.capC >= capC && a.capS >= capS && a.K >= K &&
+      a.capR >= capR && a.ecells >= ecells)
+    return ALIFMM_OK;
   free_arena(a);
   a.nsrc = nsrc;
   a.cells = cells;
   a.capL = capL;
   a.capC = capC;
   a.capS = capS;
+  a.K = K;
+  a.capR = capR;
+  a.ecells = ecells;
   HIPCHK(dalloc(&a.S, (size_t)nsrc * cells));
   HIPCHK(dalloc(&a.own, (size_t)nsrc * cells));
   HIPCHK(dalloc(&a.ax, (size_t)nsrc * 2 * capL));
   HIPCHK(dalloc(&a.px, nsrc));
-  HIPCHK(dalloc(&a.lists, (size_t)nsrc * (3 * capL + 2 * capC)));
-  HIPCHK(dalloc(&a.dlists, (size_t)nsrc * (2 * capL + capC)));
+  HIPCHK(dalloc(&a.lists, (size_t)nsrc * (4 * capL + 4 * capC)));
+  HIPCHK(dalloc(&a.dlists, (size_t)nsrc * (2 * capL + 2 * capC)));
+  if (K > 1) {
+    HIPCHK(dalloc(&a.rimc, (size_t)nsrc * K * 2 * capR));
+    HIPCHK(dalloc(&a.rimt, (size_t)nsrc * K * 2 * capR));
+    HIPCHK(dalloc(&a.E, (size_t)nsrc * 2 * ecells));
+  }
+  HIPCHK(dalloc(&a.kx, nsrc));
   if (capS > 0) {
     HIPCHK(dalloc(&a.Ts, (size_t)nsrc * 2 * capS));
     HIPCHK(dalloc(&a.Ss, (size_t)nsrc * 2 * capS));
@@ -489,6 +520,20 @@ static int ensure_field(alifmm_ctx* ctx, int slot, int sg, int fz, int fx) {
   return ALIFMM_OK;
 }
 
+// members per source of the K-member band kernel: the largest power of two <= kMaxK whose grid
+// (nsrc padded to 8, times K workgroups, one per CU) is co-resident, with >= 2 stripes per member
+// (option "members" forces a value, still capped by residency)
+static int choose_members(const alifmm_ctx* ctx, int n, long nstripes) {
+  const int by_cu = std::max(1, ctx->n_cu / (8 * ((n + 7) / 8)));
+  int K = 1;
+  if (ctx->members > 0) {
+    while (K * 2 <= ctx->members && K * 2 <= by_cu) K *= 2;
+    return K;
+  }
+  while (K * 2 <= af::kMaxK && K * 2 <= by_cu && K * 2 <= std::max(1L, nstripes / 2)) K *= 2;
+  return K;
+}
+
 // one chunk of sources; returns ALIFMM_E_CAPACITY when a work list overflowed
 static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const double* scz, int first_slot, int fz,
                         int fx, float* ms_init, float* ms_band) {
@@ -503,8 +548,15 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
     capL = std::max(capL, std::min(capS, 262144L));
     capC = capL;
   }
+  // K-member band kernel: members per source and the stripe geometry (KGeom)
+  const bool kmode = ctx->kernel == 0;
+  const int wlog = ctx->stripe_log, W = 1 << wlog;
+  const long nstripes = (fx + W - 1) / W;
+  const int K = kmode ? choose_members(ctx, n, nstripes) : 1;
+  const long capR = K > 1 ? 2L * fz * ((nstripes + K - 1) / K) + 64 : 0;
+  const long ecells = K > 1 ? nstripes * 4L * fz : 0;
   // the arena is sized for this chunk (reused while later chunks fit in it)
-  int rc = ensure_arena(ctx, n, cells, capL, capC, capS);
+  int rc = ensure_arena(ctx, n, cells, capL, capC, capS, K, capR, ecells);
   if (rc) return rc;
   Arena& a = ctx->arena;
   // subgrid 1: the fields are first written by the band kernel, so their initialisation runs on
@@ -527,16 +579,32 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
     b.ax[0] = a.ax + (size_t)i * 2 * a.capL;
     b.ax[1] = b.ax[0] + a.capL;
     b.px = a.px + i;
-    int* base = a.lists + (size_t)i * (3 * a.capL + 2 * a.capC);
+    int* base = a.lists + (size_t)i * (4 * a.capL + 4 * a.capC);
     b.L0 = base;
     b.L1 = base + a.capL;
     b.A = base + 2 * a.capL;
-    b.C = base + 3 * a.capL;
-    b.Cp = base + 3 * a.capL + a.capC;
-    double* dbase = a.dlists + (size_t)i * (2 * a.capL + a.capC);
+    b.L = base + 3 * a.capL;
+    b.C = base + 4 * a.capL;
+    b.Cp = b.C + a.capC;
+    b.D = b.C + 2 * a.capC;
+    b.Rx = b.C + 3 * a.capC;
+    double* dbase = a.dlists + (size_t)i * (2 * a.capL + 2 * a.capC);
     b.Lt0 = dbase;
     b.Lt1 = dbase + a.capL;
     b.V = dbase + 2 * a.capL;
+    b.Dv = b.V + a.capC;
+    // K-member kernel: the hand-over input stays in L0 (fmm_exact_kernel writes it there), the
+    // member lists go elsewhere (a member rewrites its slice while another may still read input)
+    b.Lin = b.L0;
+    b.Lt = b.Lt0;
+    b.FS = b.L1;
+    b.kx = a.kx + i;
+    if (K > 1) {
+      b.rimc = a.rimc + (size_t)i * K * 2 * capR;
+      b.rimt = a.rimt + (size_t)i * K * 2 * capR;
+      b.E = a.E + (size_t)i * 2 * ecells;
+      HIPCHK(hipMemsetAsync(b.E, 0xFF, (size_t)2 * ecells * 8, fs));  // far: NaN
+    }
     if (capS > 0) {
       b.Ts[0] = a.Ts + (size_t)i * 2 * a.capS;
       b.Ts[1] = b.Ts[0] + a.capS;
@@ -569,6 +637,10 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
   P.gox = ctx->gox;
   P.goz = ctx->goz;
   P.prof = ctx->prof;
+  P.K = K;
+  P.wlog = wlog;
+  P.capR = (int)capR;
+  P.ecells = ecells;
   HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
   if (sg == 1) {
     std::vector<af::InitJob> jobs(n);
@@ -609,13 +681,18 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
   HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
   if (fs != ctx->stream) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_fill, 0));
   bool paired = false;
-  if (ctx->pair && 16 * ((n + 7) / 8) <= ctx->n_cu) {
+  ctx->last_k = 0;
+  if (kmode) {
+    HIPCHK(hipMemsetAsync(a.kx, 0, sizeof(af::KX) * n, ctx->stream));
+    HIPCHK(af_launch_band_k(&P, ctx->stream));
+    ctx->last_k = K;
+  } else if (ctx->pair && 16 * ((n + 7) / 8) <= ctx->n_cu) {
     HIPCHK(hipMemsetAsync(a.px, 0, sizeof(af::PairX) * n, ctx->stream));
     paired = af_launch_band_pair(&P, ctx->stream) == hipSuccess;
     if (!paired) (void)hipGetLastError();  // not co-resident / model too large for LDS: single kernel
   }
   ctx->last_pair = paired;
-  if (!paired) HIPCHK(af_launch_band(&P, ctx->stream));
+  if (!kmode && !paired) HIPCHK(af_launch_band(&P, ctx->stream));
   HIPCHK(hipEventRecord(ctx->ev[2], ctx->stream));
   if (sg > 1)
     for (int i = 0; i < n; i++) HIPCHK(af_launch_scale(hs[i].T, cells, (double)sg, ctx->stream));
@@ -661,7 +738,9 @@ int alifmm_travel(alifmm_ctx* ctx, int subgrid, int nsrc, const double* scx, con
   HIPCHK(hipEventCreate(&t_begin));
   HIPCHK(hipEventRecord(t_begin, ctx->stream));
   // chunk: two workgroups per source need 2n CUs (pair mode), one per source otherwise
-  const int chunk = (ctx->pair && ctx->n_cu >= 16) ? std::min(ctx->batch, ctx->n_cu / 16 * 8) : ctx->batch;
+  // K-member kernel: at least one workgroup per source (sources padded to 8) on the device
+  const int chunk = ctx->kernel == 0 ? std::max(1, std::min(ctx->batch, ctx->n_cu / 8 * 8))
+                    : (ctx->pair && ctx->n_cu >= 16) ? std::min(ctx->batch, ctx->n_cu / 16 * 8) : ctx->batch;
   for (int s0 = 0; s0 < nsrc; s0 += chunk) {
     int n = std::min(chunk, nsrc - s0);
     int rc;

@@ -1,0 +1,742 @@
+// fmm_band_k.hip — band-synchronous FMM over the main grid with K workgroups ("members", one per
+// CU) per source, K = 1, 2, 4, 8 or 16.  Replaces the reference's heap-ordered main
+// loop (travel :2055-2102, travel_finer_grid :2775-2817).
+//
+// Ownership.  The grid is cut into column stripes of W = 2^wlog columns; stripe s belongs to member
+// (s mod K).  A member keeps the close set, accepted / claimed lists and claim hash of its own cells
+// in LDS, and evaluates and commits only its own cells.  Per step (one cross-member exchange):
+//   P1  local Tmin over the own close set (LDS); publish the own close RIM cells (next to a stripe
+//       boundary) with T <= thr_ub = Tmin_loc + delta(Tmin_loc) — an upper bound of this step's
+//       acceptance threshold — then X1: every member stores (Tmin, live, err, #rim) as flagged
+//       words and reads everybody's -> global Tmin, threshold, termination
+//   P0  (after X1) copy-forward: last step's commits of EDGE cells (within 2 columns of a stripe
+//       boundary, i.e. readable by another member's 12-point / 5x5 stencils) into this step's
+//       edge buffer — after X1, because another member may read that buffer until it reaches X1
+//   P2  accept own close cells with T <= thr (-> known, slot freed)
+//   P3  claim own non-known 4-neighbours of own accepted cells and of the neighbour members'
+//       accepted rim cells (read from their published lists: T <= thr), deduplicated (LDS hash)
+//   P4  evaluate update() (fallback fouds18_A()) Jacobi-style against the state of the end of the
+//       previous step: own cells from T, other members' cells from the previous step's edge
+//       buffer (members write only the other parity during the step, so no second exchange)
+//   P5  commit: T, own slots, and edge cells also into this step's edge buffer
+// Why one exchange is enough: evaluation reads T (unchanged by acceptance) and validity
+// (known or close, unchanged by acceptance), so only WHICH cells are evaluated depends on this
+// step's acceptance — and another member's acceptance of a rim cell is decided by data that member
+// published before X1.  fouds18_A() reads known-ness after acceptance: another member's cell is
+// known iff its status is known, or close with T_prev <= thr (exactly that member's accept rule).
+// Results are identical to the one-workgroup kernel (and to any K): the same cells are accepted,
+// claimed and evaluated against the same state every step; only which CU does the work differs.
+//
+// Cross-CU data (flags, rim lists, edge buffers, statuses of edge cells) is stored with sc1 stores,
+// drained (vmcnt 0) by every wave before the flag, and read with sc1 loads after the flag
+// (MI355X_MICROARCH.md "inter-workgroup visibility", Valid forms).  Flags, rim lists and edge
+// buffers are double-buffered by step parity: a member can be at most one step ahead of another.
+#include <type_traits>
+#include "kernels.h"
+#include "local_ops.h"
+#include "fields.h"
+#include "band_common.h"
+
+namespace af {
+namespace kb {
+
+constexpr int kThreads = 512;
+constexpr int kWaves = kThreads / 64;
+constexpr int kLcap = 2560, kAcap = 1024, kEcap = 1536, kDcap = 1024, kRcap = 1024;
+constexpr int kHashLog = 13;
+constexpr int kHash = 1 << kHashLog;
+constexpr int kClaimU = 4;        // claim items per lane per pass
+constexpr int kHashItems = 6144;  // claim items deduplicated in the LDS hash (more: global stamps)
+constexpr int kStabLds = 64, kPtabLds = 722, kMatLds = 256;
+
+struct Lds {
+  double red[kWaves];
+  double Lt[kLcap];  // close set: T of the slot (+inf: free)
+  double Vl[kEcap];  // evaluated values
+  double Dv[kDcap];  // edge commits of the step: value (copied forward next step)
+  double stab[kStabLds * 5];
+  double ptab[kPtabLds];
+  MatRec mat[kMatLds];
+  int Ll[kLcap];  // close set: cell of the slot
+  int Fs[kLcap];  // free slots
+  int Al[kAcap];  // accepted cells
+  int El[kEcap];  // claimed cells
+  int Ep[kEcap];  // slot of a claimed close cell, -1 for a far cell
+  int Dc[kDcap];  // edge commits of the step: cell
+  int Rx[kRcap];  // claim items from the neighbour members' accepted rim cells
+  alignas(16) int H[kHash];
+  double tmin_g, thr;
+  int nA, nE, nF, hi, taken, nD, nR, nRx, live_g, err_g, err, nFb;
+  int nrim[2];  // rim-list lengths of the neighbour members (left, right) this step
+};
+
+AF_DEV unsigned hslot(int key) { return ((unsigned)key * 2654435761u) >> (32 - kHashLog); }
+AF_DEV unsigned hstep(int key) { return (((unsigned)key * 0x85ebca6bu) >> (32 - kHashLog)) | 1u; }
+
+// Stencil neighbourhood (NbFieldT) at the state of the end of the previous step: own columns from
+// T, other members' columns from the previous step's edge buffer.  12 independent loads in ONE form
+// (sc1: the edge buffer needs it, and one load instruction per point beats a divergent pair),
+// issued together; out-of-grid positions read the cell itself (update() never uses them).
+AF_DEV void load_nb(NbFieldT& nb, const double* T, const double* Eprev, const KGeom& g, int me, int z, int x) {
+  const int dz[12] = {0, 0, 0, 0, -2, -1, 1, 2, -1, -1, 1, 1};
+  const int dx[12] = {-2, -1, 1, 2, 0, 0, 0, 0, -1, 1, -1, 1};
+  nb.iz = z;
+  nb.ix = x;
+  const long p = (long)z * g.nx + x;
+  double t[12];
+#pragma unroll
+  for (int k = 0; k < 12; k++) {
+    const int zz = z + dz[k], xx = x + dx[k];
+    const bool in = zz >= 0 && zz < g.nz && xx >= 0 && xx < g.nx;
+    const bool other = in && g.owner(xx) != me;
+    t[k] = gld_sc1(other ? Eprev + g.eidx(zz, xx) : T + (in ? (long)zz * g.nx + xx : p));
+  }
+  unsigned m = 0;
+#pragma unroll
+  for (int k = 0; k < 12; k++)
+    if (z + dz[k] < g.nz && t[k] == t[k]) m |= 1u << k;
+  nb.vm = m;
+  nb.t0 = t[0]; nb.t1 = t[1]; nb.t2 = t[2]; nb.t3 = t[3]; nb.t4 = t[4]; nb.t5 = t[5];
+  nb.t6 = t[6]; nb.t7 = t[7]; nb.t8 = t[8]; nb.t9 = t[9]; nb.t10 = t[10]; nb.t11 = t[11];
+}
+
+// fouds18_A() reads a 5x5 neighbourhood with "known" = status 0 after this step's acceptance.  The
+// (rare) fallback cells are processed in rounds: all threads stage each cell's neighbourhood
+// into LDS — T at the end of the previous step (own cells from T, other members' from the
+// previous edge buffer; NaN -> 0 as GField) and known-ness (own: status 0; another member's:
+// status 0, or close with T_prev <= thr, exactly that member's accept rule) — then one lane per
+// cell runs fouds18_A() on the staged window (few registers: the accessor is two LDS reads).
+constexpr int kFbRound = 128;  // cells per staging round (25 doubles each in the claim-hash space)
+struct Win5 {
+  const double* t;  // 25 values, row-major (dz + 2) * 5 + (dx + 2)
+  unsigned known;   // bit (dz + 2) * 5 + (dx + 2)
+  int iz, ix;
+  AF_DEV int st(long z, long x) const { return (known >> ((z - iz + 2) * 5 + (x - ix + 2))) & 1u ? (int)kKnown : -1; }
+  AF_DEV double tt(long z, long x) const { return t[(z - iz + 2) * 5 + (x - ix + 2)]; }
+};
+
+// X1 read side (wave 0): lane l polls word l & 3 of member l >> 2 (K <= kMaxK = 16 members, one
+// word per lane) until every member's words carry this step's tag, then the wave reduces them:
+// global Tmin, live close cells (sum), error (or), and the neighbour members' rim-list lengths.
+// false on timeout (a member is not resident)
+AF_DEV bool x1_poll(KX* X, int K, int par, unsigned tag, Lds* sh, int me) {
+  const int lane = threadIdx.x & 63;
+  const int nw = 4 * K;
+  unsigned long long v = 0;
+  long spins = 0;
+  while (true) {
+    bool ok = true;
+    if (lane < nw) {
+      v = gld_sc1(&X->x1[lane >> 2][par][lane & 3]);
+      ok = (unsigned)(v >> 32) == tag;
+    }
+    if (__all(ok)) break;
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins > (1L << 25)) return false;
+  }
+  const unsigned w = (unsigned)v;
+  const unsigned w1 = __shfl_down(w, 1), w2 = __shfl_down(w, 2), w3 = __shfl_down(w, 3);
+  double tmin = INFINITY;
+  int live = 0, err = 0;
+  if ((lane & 3) == 0 && lane < nw) {
+    const int q = lane >> 2;
+    tmin = __longlong_as_double((long long)(((unsigned long long)w1 << 32) | w));
+    live = (int)w2;
+    err = (int)(w3 >> 24);
+    if (q == ((me - 1) & (K - 1))) sh->nrim[0] = (int)(w3 & 0xffffffu);
+    if (K > 2 && q == ((me + 1) & (K - 1))) sh->nrim[1] = (int)(w3 & 0xffffffu);
+  }
+  tmin = wave_min(tmin);
+  for (int o = 32; o > 0; o >>= 1) {
+    live += __shfl_xor(live, o);
+    err |= __shfl_xor(err, o);
+  }
+  if (lane == 0) {
+    sh->tmin_g = tmin;
+    sh->live_g = live;
+    sh->err_g = err;
+  }
+  return true;
+}
+
+template <int MODE, bool LDSMAT, bool PROF>
+__global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
+  __shared__ Lds sh_;
+  Lds* sh = &sh_;
+  const int K = P.K;
+  // block -> (source, member): the K members of a source have equal blockIdx % 8 (one XCD under
+  // the observed round-robin placement: a speed preference, never relied on for correctness)
+  const int b = blockIdx.x, xq = b & 7, j = b >> 3;
+  const int src = (j / K) * 8 + xq, me = j % K;
+  if (src >= P.nsrc) return;  // all members of a padding source exit together
+  BandSrc* B = P.src + src;
+  KX* X = B->kx;
+  const int tid0 = threadIdx.x;
+  const int tid = tid0, lane = tid & 63, wv = tid >> 6;
+  const int nz = P.nz, nx = P.nx;
+  const KGeom g{K, P.wlog, nz, nx};
+  double* T = B->T;
+  int* S = B->S;
+  int* own = B->own;
+  DevModel M = P.M;
+  if (LDSMAT) {
+    for (int k = tid; k < 5 * M.nstab; k += kThreads) sh->stab[k] = M.stab[k];
+    for (int k = tid; k < 361 * M.ncol; k += kThreads) sh->ptab[k] = M.ptab[k];
+    for (int k = tid; k < M.nmat; k += kThreads) sh->mat[k] = M.mtab[k];
+    M.ptab = sh->ptab;
+  }
+  // per-member slices of the global spill arrays of the LDS lists
+  const long hL = P.capL / K, hC = P.capC / K;
+  const HList<int, kLcap> L{sh->Ll, B->L + me * hL};
+  const HList<double, kLcap> Lt{sh->Lt, B->Lt + me * hL};
+  const HList<int, kLcap> FS{sh->Fs, B->FS + me * hL};
+  const HList<int, kAcap> AL{sh->Al, B->A + me * hL};
+  const HList<int, kEcap> EL{sh->El, B->C + me * hC};
+  const HList<int, kEcap> EP{sh->Ep, B->Cp + me * hC};
+  const HList<double, kEcap> VL{sh->Vl, B->V + me * hC};
+  const HList<int, kDcap> DC{sh->Dc, B->D + me * hC};
+  const HList<double, kDcap> DV{sh->Dv, B->Dv + me * hC};
+  const HList<int, kRcap> RX{sh->Rx, B->Rx + me * hC};
+  const int capL = (int)hL, capC = (int)hC;
+  // rim lists [member][parity][capR]; edge buffers [parity][ecells] (selected by arithmetic on the
+  // step parity: no dynamically indexed private arrays, which would live in scratch)
+  int* const rimc = B->rimc;
+  double* const rimt = B->rimt;
+  double* const E0 = B->E;
+  const long ecells = P.ecells;
+  if (tid == 0) {
+    sh->hi = 0;
+    sh->nF = 0;
+    sh->nD = 0;
+    sh->err = 0;
+    sh->nrim[0] = sh->nrim[1] = 0;
+  }
+  __syncthreads();
+  // ---------------- hand-over: own cells only ----------------
+  if (MODE == 0) {
+    const HandoverOut* H = P.ho + src;
+    if (tid == 0 && H->err) sh->err = 3;
+    const int n = H->n;
+    for (int k0 = wv * 64; k0 < n; k0 += kThreads) {
+      const int k = k0 + lane;
+      bool push = false;
+      int c = 0, z = 0, x = 0;
+      double t = 0.0;
+      if (k < n) {
+        c = H->cell[k];
+        z = c / nx;
+        x = c - z * nx;
+        if (g.owner(x) == me) {
+          t = H->ttn[k];
+          gst(T + c, t);
+          if (g.edge(x)) {
+            gst_sc1(E0 + g.eidx(z, x), t);
+            gst_sc1(E0 + ecells + g.eidx(z, x), t);
+          }
+          if (H->cls[k] == 1) gst_sc1(S + c, (int)kKnown);
+          else push = true;
+        }
+      }
+      const int s = wave_push(&sh->hi, push, capL, &sh->err);
+      if (s >= 0) {
+        L.put(s, pk(z, x));
+        Lt.put(s, t);
+        gst_sc1(S + c, 1 + s);
+      }
+    }
+  } else {
+    // travel_finer_grid(): fmm_exact_kernel wrote T / S of the exact region and its close cells in
+    // Lin; the edge buffers get the region's edge cells (T is NaN outside what it touched)
+    if (tid == 0 && B->err) sh->err = B->err;
+    if (K > 1) {
+      const int z0 = max(0, B->bbox[0]), z1 = min(nz - 1, B->bbox[1]);
+      const int x0 = max(0, B->bbox[2]), x1 = min(nx - 1, B->bbox[3]);
+      const int w = x1 - x0 + 1;
+      const long nb = (z1 >= z0 && w > 0) ? (long)(z1 - z0 + 1) * w : 0;
+      for (long k = tid; k < nb; k += kThreads) {
+        const int z = z0 + (int)(k / w), x = x0 + (int)(k % w);
+        if (g.owner(x) == me && g.edge(x)) {
+          const double t = gld(T + (long)z * nx + x);
+          gst_sc1(E0 + g.eidx(z, x), t);
+          gst_sc1(E0 + ecells + g.eidx(z, x), t);
+        }
+      }
+    }
+    const int n = B->nl0;
+    for (int k0 = wv * 64; k0 < n; k0 += kThreads) {
+      const int k = k0 + lane;
+      bool push = false;
+      int c = 0, z = 0, x = 0;
+      if (k < n) {
+        c = gld(B->Lin + k);
+        z = c / nx;
+        x = c - z * nx;
+        push = g.owner(x) == me;
+      }
+      const int s = wave_push(&sh->hi, push, capL, &sh->err);
+      if (s >= 0) {
+        L.put(s, pk(z, x));
+        Lt.put(s, gld(T + c));
+        gst_sc1(S + c, 1 + s);
+      }
+    }
+  }
+  __syncthreads();
+  RunCfg R;
+  R.nz = nz;
+  R.nx = nx;
+  R.dnx = P.dnx;
+  R.dnz = P.dnz;
+  if (MODE == 0)
+    R.mv = MatView{1, 0, 0, 1, 0, 0, 1, 0, 0, 0, 0};
+  else
+    R.mv = MatView{P.sg, (P.sg - 1) / 2, 0, P.sg, (P.sg - 1) / 2, 0, 1, 0, 0, 0, 1};
+  R.delta = launder_u(P.cdelta * P.dnx / P.vmax);
+  R.t0 = launder_u(P.r0 * P.dnx / P.vmax);
+  long long steps = 0, myupd = 0;
+  // profile (P.prof): thread 0 of member 0; phases [P0+P1+X1, accept, claim (incl. rim read),
+  // evaluate, fallback, commit], sub [X1 wait, rim read, claim dedupe, claim status loads]
+  const bool prof = PROF && tid == 0 && me == 0;
+  long long ph[6] = {0, 0, 0, 0, 0, 0}, sub[4] = {0, 0, 0, 0}, ls[3] = {0, 0, 0}, lmax = 0;
+  long long tk = prof ? wall_clock64() : 0;
+#define AF_TICK(k)                 \
+  if (prof) {                      \
+    long long t_ = wall_clock64(); \
+    ph[k] += t_ - tk;              \
+    tk = t_;                       \
+  }
+#define AF_SUBT(k, t0)                   \
+  if (prof) sub[k] += wall_clock64() - (t0);
+  while (true) {
+    // the thread index is re-read each step (opaque to the compiler), so values derived from it are
+    // recomputed in the step instead of being kept live across the loop (and spilled)
+    int tid = tid0;
+    asm volatile("" : "+v"(tid));
+    const int lane = tid & 63, wv = tid >> 6;
+    const int par = (int)(steps & 1), prv = par ^ 1;
+    double* const Epar = E0 + par * ecells;
+    const double* const Eprv = E0 + prv * ecells;
+    const int hi = sh->hi;
+    // ---- P1: local Tmin over the close set (LDS); clear the claim hash ----
+    double tmin = INFINITY;
+    if (hi <= kLcap) {
+      for (int e = tid; e < hi; e += kThreads) tmin = fmin(tmin, Lt.lds(e));
+    } else {
+      for (int e = tid; e < hi; e += kThreads) tmin = fmin(tmin, Lt.get(e));
+    }
+    for (int k = tid * 4; k < kHash; k += kThreads * 4) *(int4*)&sh->H[k] = make_int4(0, 0, 0, 0);
+    tmin = wave_min(tmin);
+    if (lane == 0) sh->red[wv] = tmin;
+    if (tid == 0) {
+      sh->nA = 0;
+      sh->nE = 0;
+      sh->nFb = 0;
+      sh->taken = 0;
+      sh->nR = 0;
+      sh->nRx = 0;
+    }
+    __syncthreads();
+    tmin = sh->red[0];
+    for (int w = 1; w < kWaves; w++) tmin = fmin(tmin, sh->red[w]);
+    const double delta = launder_u(R.delta), t0 = launder_u(R.t0);
+    // publish own close rim cells that may be accepted this step (T <= thr_ub >= thr)
+    if (K > 1) {
+      const double thr_ub = tmin + ((t0 > 0 && tmin < t0) ? delta * (tmin / t0) : delta);
+      for (int e0 = wv * 64; e0 < hi; e0 += kThreads) {
+        const int e = e0 + lane;
+        const double t = e < hi ? Lt.get(e) : INFINITY;
+        const int c = t <= thr_ub ? L.get(e) : 0;
+        const bool pub = t <= thr_ub && g.rim(pkx(c));
+        const int s = wave_push(&sh->nR, pub, P.capR, &sh->err);
+        if (s >= 0) {
+          gst_sc1(rimc + ((long)me * 2 + par) * P.capR + s, c);
+          gst_sc1(rimt + ((long)me * 2 + par) * P.capR + s, t);
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores have completed
+    __syncthreads();
+    const long long tx1 = prof ? wall_clock64() : 0;
+    if (K > 1) {
+      if (tid == 0) {
+        // X1: flagged words (step + 1 in the high half), one store each; the payload arrives with the flag
+        const unsigned long long gtag = (unsigned long long)(unsigned)(steps + 1) << 32;
+        const unsigned long long tb = (unsigned long long)__double_as_longlong(tmin);
+        gst_sc1(&X->x1[me][par][0], gtag | (tb & 0xffffffffull));
+        gst_sc1(&X->x1[me][par][1], gtag | (tb >> 32));
+        gst_sc1(&X->x1[me][par][2], gtag | (unsigned)(hi - sh->nF));
+        gst_sc1(&X->x1[me][par][3], gtag | ((unsigned)min(sh->err, 255) << 24) | (unsigned)min(sh->nR, 0xffffff));
+      }
+      if (wv == 0 && !x1_poll(X, K, par, (unsigned)(steps + 1), sh, me)) {
+        if (lane == 0) sh->err = 7;
+      }
+    } else if (tid == 0) {
+      sh->tmin_g = tmin;
+      sh->live_g = hi - sh->nF;
+      sh->err_g = sh->err;
+    }
+    __syncthreads();
+    AF_SUBT(0, tx1)
+    AF_TICK(0)
+    if (sh->live_g <= 0 || sh->err_g || sh->err) break;
+    // ---- P0: copy last step's edge commits forward into this step's edge buffer.  Only now: every
+    // member has passed this step's X1, i.e. finished the previous step, whose evaluation read this
+    // buffer as the state of two steps ago ----
+    if (K > 1) {
+      const int nD = min(sh->nD, capC);
+      for (int d = tid; d < nD; d += kThreads) {
+        const int c = DC.get(d);
+        gst_sc1(Epar + g.eidx(pkz(c), pkx(c)), DV.get(d));
+      }
+    }
+    tmin = sh->tmin_g;
+    double dl = delta;
+    if (t0 > 0 && tmin < t0) dl = delta * (tmin / t0);
+    const double thr = tmin + dl;
+    if (tid == 0) {
+      sh->thr = thr;
+      sh->nD = 0;
+    }
+    // ---- P2: accept own close cells ----
+    auto accept = [&](auto lds_only) {
+      constexpr bool LO = decltype(lds_only)::value;
+      for (int e0 = wv * 64; e0 < hi; e0 += kThreads) {
+        const int e = e0 + lane;
+        const double t = e < hi ? (LO ? Lt.lds(e) : Lt.get(e)) : INFINITY;
+        const bool acc = t <= thr;
+        const int c = acc ? (LO ? L.lds(e) : L.get(e)) : 0;
+        int sa, sf;
+        wave_push2(&sh->nA, &sh->nF, acc, capL, &sh->err, sa, sf);
+        if (sa >= 0) {
+          AL.put(sa, c);
+          const long f = (long)pkz(c) * nx + pkx(c);
+          if (g.edge(pkx(c))) gst_sc1(S + f, (int)kKnown);
+          else gst(S + f, (int)kKnown);
+          if (LO) {
+            Lt.put_lds(e, INFINITY);
+            FS.put_lds(sf, e);
+          } else {
+            Lt.put(e, INFINITY);
+            FS.put(sf, e);
+          }
+        }
+      }
+    };
+    if (hi <= kLcap) accept(std::true_type{});
+    else accept(std::false_type{});
+    // the copy-forward stores above precede this step's edge commits to the same addresses
+    if (K > 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // ---- P3a: the neighbour members' accepted rim cells -> claim items (their cross neighbour) ----
+    const long long trr = prof ? wall_clock64() : 0;
+    if (K > 1) {
+      const int nq = K == 2 ? 1 : 2;
+      for (int side = 0; side < nq; side++) {
+        const int q = (me + (side == 0 ? -1 : 1)) & (K - 1);
+        const int nr = min(sh->nrim[side], P.capR);
+        const int* rc = rimc + ((long)q * 2 + par) * P.capR;
+        const double* rt = rimt + ((long)q * 2 + par) * P.capR;
+        for (int e0 = wv * 64; e0 < nr; e0 += kThreads) {
+          const int e = e0 + lane;
+          int c = -1;
+          if (e < nr) {
+            const int pc = gld_sc1(rc + e);
+            const double pt = gld_sc1(rt + e);
+            if (pt <= thr) {
+              const int px = pkx(pc), r = px & ((1 << g.wlog) - 1);
+              const int cx = r == 0 ? px - 1 : px + 1;  // across the stripe boundary
+              if (cx >= 0 && cx < nx && g.owner(cx) == me) c = pk(pkz(pc), cx);
+            }
+          }
+          const int s = wave_push(&sh->nRx, c >= 0, capC, &sh->err);
+          if (s >= 0) RX.put(s, c);
+        }
+      }
+    }
+    __syncthreads();
+    AF_SUBT(1, trr)
+    AF_TICK(1)
+    const int nA = min(sh->nA, capL), nRx = min(sh->nRx, capC);
+    // ---- P3b: claim ----
+    const int nItems = 4 * nA + nRx;
+    const bool use_hash = nItems <= kHashItems;
+    const bool lds_items = nA <= kAcap && nRx <= kRcap;
+    const int stamp = (int)steps;
+    for (int q0 = wv * 64 * kClaimU; q0 < nItems; q0 += kThreads * kClaimU) {
+      int r[kClaimU], s[kClaimU], o[kClaimU];
+      const long long tdd = prof ? wall_clock64() : 0;
+      unsigned hh[kClaimU];
+      int pv[kClaimU];
+#pragma unroll
+      for (int u = 0; u < kClaimU; u++) {
+        const int q = q0 + u * 64 + lane;
+        int c = -1;
+        if (q < nItems) {
+          if (q < 4 * nA) {
+            c = nb_cell(lds_items ? AL.lds(q >> 2) : AL.get(q >> 2), q & 3, nz, nx);
+            if (c >= 0 && g.owner(pkx(c)) != me) c = -1;  // claimed by its owner (from my rim list)
+          } else {
+            c = lds_items ? RX.lds(q - 4 * nA) : RX.get(q - 4 * nA);
+          }
+        }
+        r[u] = c;
+        hh[u] = hslot(c);
+      }
+      if (use_hash) {
+#pragma unroll
+        for (int u = 0; u < kClaimU; u++) pv[u] = r[u] >= 0 ? atomicCAS(&sh->H[hh[u]], 0, r[u] + 1) : 0;
+        unsigned pend = 0;
+#pragma unroll
+        for (int u = 0; u < kClaimU; u++) {
+          if (pv[u] != 0) {
+            if (pv[u] == r[u] + 1) r[u] = -1;  // already claimed
+            else pend |= 1u << u;
+          }
+        }
+        for (int probe = 1; pend; probe++) {
+          if (probe >= kHash) {
+            sh->err = 5;
+#pragma unroll
+            for (int u = 0; u < kClaimU; u++)
+              if ((pend >> u) & 1u) r[u] = -1;
+            break;
+          }
+#pragma unroll
+          for (int u = 0; u < kClaimU; u++) {
+            if ((pend >> u) & 1u) {
+              hh[u] = (hh[u] + hstep(r[u])) & (kHash - 1);
+              pv[u] = atomicCAS(&sh->H[hh[u]], 0, r[u] + 1);
+              if (pv[u] == 0 || pv[u] == r[u] + 1) {
+                if (pv[u] != 0) r[u] = -1;
+                pend &= ~(1u << u);
+              }
+            }
+          }
+        }
+      }
+      if (prof) __builtin_amdgcn_s_waitcnt(0);
+      AF_SUBT(2, tdd)
+      const long long tcl = prof ? wall_clock64() : 0;
+#pragma unroll
+      for (int u = 0; u < kClaimU; u++) {
+        const long f = r[u] >= 0 ? (long)pkz(r[u]) * nx + pkx(r[u]) : 0;
+        // own cells; sc1: edge cells' statuses are stored sc1 (for other members), and an sc1 store
+        // does not refresh this CU's L1 copy of the line
+        s[u] = r[u] >= 0 ? gld_sc1(S + f) : (int)kKnown;
+        o[u] = (!use_hash && r[u] >= 0) ? gatomic_max(own + f, stamp) : -1;
+      }
+      // u-major list order: consecutive entries are neighbours of consecutive accepted cells, so
+      // the lanes of an evaluating wave read overlapping stencils (fewer distinct cache lines)
+      unsigned long long bm[kClaimU];
+      int cnt = 0;
+#pragma unroll
+      for (int u = 0; u < kClaimU; u++) {
+        bm[u] = __ballot(s[u] != kKnown && o[u] < stamp);
+        cnt += __popcll(bm[u]);
+      }
+      AF_SUBT(3, tcl)
+      int base = 0;
+      if (lane == 0 && cnt) base = atomicAdd(&sh->nE, cnt);
+      base = __shfl(base, 0);
+      const unsigned long long lt = (1ull << lane) - 1ull;
+#pragma unroll
+      for (int u = 0; u < kClaimU; u++) {
+        if ((bm[u] >> lane) & 1ull) {
+          const int pos = base + __popcll(bm[u] & lt);
+          if (pos < capC) {
+            EL.put(pos, r[u]);
+            EP.put(pos, s[u] > 0 ? s[u] - 1 : -1);
+          } else {
+            sh->err = 2;
+          }
+        }
+        base += __popcll(bm[u]);
+      }
+    }
+    __syncthreads();
+    AF_TICK(2)
+    const int nE = min(sh->nE, capC);
+    // ---- P4: evaluate ----
+    const bool lds_e = nE <= kEcap;
+    const double dnx_e = launder_u(R.dnx);
+    for (int e = tid; e < nE; e += kThreads) {
+      const int r = lds_e ? EL.lds(e) : EL.get(e);
+      const int z = pkz(r), x = pkx(r);
+      NbFieldT nb;  // stencil loads first, then the material id: one memory round trip
+      load_nb(nb, T, Eprv, g, me, z, x);
+      const CellMat cm = band_mat<LDSMAT>(M, sh->mat, sh->stab, R.mv, z, x);
+      const double v = update(nb, M, cm, z, x, dnx_e, nz, nx);
+      if (lds_e) VL.put_lds(e, v);
+      else VL.put(e, v);
+      myupd++;
+      // no usable stencil: queue the cell for the fouds18_A() pass (Rx is free after the claim)
+      const unsigned long long fm = __ballot(v == -1.0);
+      if (fm) {
+        const int fl = __ffsll((long long)fm) - 1;
+        int fb = 0;
+        if (lane == fl) fb = atomicAdd(&sh->nFb, __popcll(fm));
+        fb = __shfl(fb, fl) + __popcll(fm & ((1ull << lane) - 1ull));
+        if (v == -1.0 && fb < kRcap) sh->Rx[fb] = e;
+      }
+    }
+    AF_TICK(3)
+    // ---- P4b: fouds18_A() over the compacted fallback list, in staged rounds ----
+    __syncthreads();
+    {
+      const int nFb = sh->nFb;
+      const double thr_f = sh->thr;
+      double* const win = reinterpret_cast<double*>(sh->H);  // kFbRound x 25 doubles
+      unsigned* const wmask = reinterpret_cast<unsigned*>(sh->Al);
+      const int nlist = min(nFb, kRcap);
+      // cells past the list capacity (more fallback cells than list slots) are found by a scan
+      const int nscan = nFb > kRcap ? nE : 0;
+      for (int r0 = 0; r0 < nlist + nscan; r0 += kFbRound) {
+        const int nr = min(kFbRound, nlist + nscan - r0);
+        if (tid < nr) wmask[tid] = 0u;
+        __syncthreads();
+        for (int i = tid; i < nr * 25; i += kThreads) {
+          const int q = r0 + i / 25, o = i % 25;
+          const int e = q < nlist ? sh->Rx[q] : q - nlist;
+          if (q >= nlist && VL.get(e) != -1.0) continue;  // scan part: fallback cells only
+          const int c = EL.get(e);
+          const int zz = pkz(c) + o / 5 - 2, xx = pkx(c) + o % 5 - 2;
+          double t = 0.0;
+          bool kn = false;
+          if (zz >= 0 && zz < nz && xx >= 0 && xx < nx) {
+            const long f = (long)zz * nx + xx;
+            const bool mine = g.owner(xx) == me;
+            const double tp = mine ? gld(T + f) : gld_sc1(Eprv + g.eidx(zz, xx));
+            const int st = gld_sc1(S + f);
+            t = far0(tp);
+            kn = st == kKnown || (!mine && st > 0 && tp <= thr_f);
+          }
+          win[i] = t;
+          if (kn) atomicOr(&wmask[i / 25], 1u << o);
+        }
+        __syncthreads();
+        if (tid < nr) {
+          const int q = r0 + tid;
+          const int e = q < nlist ? sh->Rx[q] : q - nlist;
+          if (q < nlist || VL.get(e) == -1.0) {
+            const int c = EL.get(e);
+            const int z = pkz(c), x = pkx(c);
+            const Win5 F{win + 25 * tid, wmask[tid], z, x};
+            const CellMat cm = band_mat<LDSMAT>(M, sh->mat, sh->stab, R.mv, z, x);
+            const double dnx_f = launder_u(R.dnx), dnz_f = launder_u(R.dnz);
+            double v;
+            if constexpr (LDSMAT) v = fouds18<true>(F, M, cm, z, x, dnx_f, dnz_f, nx, nz, mat_slo(M, R.mv, z, x));
+            else v = fouds18<false>(F, M, cm, z, x, dnx_f, dnz_f, nx, nz, mat_slo(M, R.mv, z, x));
+            VL.put(e, v);
+          }
+        }
+        __syncthreads();
+      }
+    }
+    AF_TICK(4)
+    // ---- P5: commit own cells; edge cells also into this step's edge buffer ----
+    const int nF = sh->nF;
+    auto commit = [&](auto lds_only) {
+      constexpr bool LO = decltype(lds_only)::value;
+      for (int e0 = wv * 64; e0 < nE; e0 += kThreads) {
+        const int e = e0 + lane;
+        bool fresh = false, ed = false;
+        int r = 0;
+        double v = 0.0;
+        if (e < nE) {
+          r = LO ? EL.lds(e) : EL.get(e);
+          v = LO ? VL.lds(e) : VL.get(e);
+          const int p = LO ? EP.lds(e) : EP.get(e);
+          const int z = pkz(r), x = pkx(r);
+          gst(T + (long)z * nx + x, v);
+          ed = g.edge(x);
+          if (ed) gst_sc1(Epar + g.eidx(z, x), v);
+          if (p >= 0) {
+            if (LO) Lt.put_lds(p, v);
+            else Lt.put(p, v);
+          } else {
+            fresh = true;
+          }
+        }
+        const int k = wave_push(&sh->taken, fresh, 1 << 30, &sh->err);
+        if (k >= 0) {
+          const int slot = k < nF ? (LO ? FS.lds(nF - 1 - k) : FS.get(nF - 1 - k)) : hi + (k - nF);
+          if (slot >= capL) {
+            sh->err = 2;
+          } else {
+            if (LO) {
+              L.put_lds(slot, r);
+              Lt.put_lds(slot, v);
+            } else {
+              L.put(slot, r);
+              Lt.put(slot, v);
+            }
+            const long f = (long)pkz(r) * nx + pkx(r);
+            if (ed) gst_sc1(S + f, 1 + slot);
+            else gst(S + f, 1 + slot);
+          }
+        }
+        const int ds = wave_push(&sh->nD, ed, capC, &sh->err);
+        if (ds >= 0) {
+          DC.put(ds, r);
+          DV.put(ds, v);
+        }
+      }
+    };
+    if (nE <= kEcap && hi + nE <= kLcap) commit(std::true_type{});
+    else commit(std::false_type{});
+    __syncthreads();
+    if (tid == 0) {
+      const int tk_ = sh->taken;
+      sh->nF = max(0, nF - tk_);
+      sh->hi = hi + max(0, tk_ - nF);
+    }
+    if (prof) {
+      ls[0] += hi - sh->nF;
+      ls[1] += nA;
+      ls[2] += nE;
+      lmax = max(lmax, (long long)hi);
+    }
+    steps++;
+    __syncthreads();
+    AF_TICK(5)
+  }
+#undef AF_TICK
+#undef AF_SUBT
+  if (prof) {
+    for (int k = 0; k < 6; k++) B->ph[k] += ph[k];
+    for (int k = 0; k < 4; k++) B->sub[k] += sub[k];
+    for (int k = 0; k < 3; k++) B->lsum[k] += ls[k];
+    B->lmax = max(B->lmax, lmax);
+  }
+  for (int o = 32; o > 0; o >>= 1) myupd += __shfl_xor(myupd, o);
+  if (lane == 0 && myupd) atomicAdd((unsigned long long*)&B->nupd, (unsigned long long)myupd);
+  if (tid == 0) {
+    if (me == 0) B->steps[3] = steps;
+    const int e = sh->err ? sh->err : sh->err_g;
+    if (e) atomicMax(&B->err, e);
+  }
+}
+
+}  // namespace kb
+}  // namespace af
+
+// cooperative launch: nsrc (padded to a multiple of 8) x K workgroups, one per CU, all resident
+extern "C" hipError_t af_launch_band_k(const af::BandParams* P, hipStream_t stream) {
+  const bool lds = P->M.mid && P->M.mslo && P->M.nmat <= af::kb::kMatLds && P->M.nstab <= af::kb::kStabLds &&
+                   361 * P->M.ncol <= af::kb::kPtabLds;
+  const dim3 g(8 * ((P->nsrc + 7) / 8) * P->K), b(af::kb::kThreads);
+  af::BandParams Pc = *P;
+  void* args[] = {&Pc};
+  const void* fn;
+  if (P->mode == 0) {
+    fn = lds ? (P->prof ? (const void*)af::kb::fmm_band_k_kernel<0, true, true>
+                        : (const void*)af::kb::fmm_band_k_kernel<0, true, false>)
+             : (P->prof ? (const void*)af::kb::fmm_band_k_kernel<0, false, true>
+                        : (const void*)af::kb::fmm_band_k_kernel<0, false, false>);
+  } else {
+    fn = lds ? (P->prof ? (const void*)af::kb::fmm_band_k_kernel<1, true, true>
+                        : (const void*)af::kb::fmm_band_k_kernel<1, true, false>)
+             : (P->prof ? (const void*)af::kb::fmm_band_k_kernel<1, false, true>
+                        : (const void*)af::kb::fmm_band_k_kernel<1, false, false>);
+  }
+  return hipLaunchCooperativeKernel(fn, g, b, args, 0, stream);
+}

@@ -116,6 +116,17 @@ struct XGrid {
   double dnx, dnz;  // update() spacing, fouds18 dnz
 };
 
+// bounding box of the nodes written into a grid ({z0, z1, x0, x1}; empty: z0 > z1)
+struct XBox {
+  int b[4] = {1 << 30, -1, 1 << 30, -1};
+  AF_DEV void add(int z, int x) {
+    b[0] = min(b[0], z);
+    b[1] = max(b[1], z);
+    b[2] = min(b[2], x);
+    b[3] = max(b[3], x);
+  }
+};
+
 // update() then fouds18_A() (:2326-2329 / :2790-2793)
 AF_DEV double xrelax(const DevModel& M, const XGrid& g, int iz, int ix) {
   CellMat cm = cell_mat(M, g.mv, iz, ix);
@@ -132,7 +143,7 @@ AF_DEV double xrelax(const DevModel& M, const XGrid& g, int iz, int ix) {
 // the reference's FMM loop (oracle fmm_loop): stage grids stop when a neighbour step leaves the
 // window at max_dist + 1 from the source; the main grid stops when the root reaches tstop
 AF_DEV long long xloop(XHeap& h, const DevModel& M, const XGrid& g, bool stage, int isx_s, int isz_s, int max_dist,
-                       double tstop) {
+                       double tstop, XBox* box = nullptr) {
   long long pops = 0;
   bool finished = false;
   const int nz = g.nz, nx = g.nx;
@@ -160,6 +171,7 @@ AF_DEV long long xloop(XHeap& h, const DevModel& M, const XGrid& g, bool stage, 
     for (int k = 0; k < 4; k++) {
       if (inb[k]) {
         const int r = nbz[k] * nx + nbx[k];
+        if (box && st[k] != 0) box->add(nbz[k], nbx[k]);
         if (st[k] == -1) {
           const double v = xrelax(M, g, nbz[k], nbx[k]);
           g.T[r] = v;
@@ -181,12 +193,14 @@ AF_DEV long long xloop(XHeap& h, const DevModel& M, const XGrid& g, bool stage, 
 
 // hand-over of every 3rd node of a stage grid into the next grid, in row-major order (:2391-2425,
 // :2725-2759): ttn copied, known nodes stay known, "outer" known nodes and close nodes -> heap
-AF_DEV void xhandover(XHeap& h, const XGrid& s, int isz_s, int isx_s, const XGrid& d, int isz_d, int isx_d) {
+AF_DEV void xhandover(XHeap& h, const XGrid& s, int isz_s, int isx_s, const XGrid& d, int isz_d, int isx_d,
+                      XBox* box = nullptr) {
   for (int i = 0; i < s.nz + 1; i += 3) {
     for (int j = 0; j < s.nx + 1; j += 3) {
       const int pz = isz_d + (i - isz_s) / 3, px = isx_d + (j - isx_s) / 3;
       const int dc = pz * d.nx + px;
       d.T[dc] = s.T[i * s.nx + j];
+      if (box) box->add(pz, px);
       const int st = s.S[i * s.nx + j];
       if (st == 0) {
         d.S[dc] = 0;
@@ -301,8 +315,10 @@ __global__ __launch_bounds__(64) void fmm_exact_kernel(BandParams P) {
       g.dnx = P.dnx;  // the coarse spacing on the fine grid (:2790; field divided by sg at the end)
       g.dnz = P.dnz;
       XHeap h{&lds, g.S, g.T, 0, 0};
-      xhandover(h, prev, pisz, pisx, g, (int)isz, (int)isx);
-      B->steps[2] = xloop(h, M, g, false, 0, 0, 0, P.tstop);
+      XBox box;  // what the K-member band kernel copies into its edge buffers
+      xhandover(h, prev, pisz, pisx, g, (int)isz, (int)isx, &box);
+      B->steps[2] = xloop(h, M, g, false, 0, 0, 0, P.tstop, &box);
+      for (int q = 0; q < 4; q++) B->bbox[q] = box.b[q];
       err = h.err;
       // heap -> band close list (statuses: heap index > 0 -> close 1)
       for (int k = 1; k <= h.ntr && k <= P.capL; k++) {

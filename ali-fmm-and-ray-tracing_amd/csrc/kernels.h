@@ -16,6 +16,15 @@ struct PairX {
   unsigned long long x1[2][4];
 };
 
+// per-source exchange block of the K-member band kernel (fmm_band_k.hip); zeroed by the host
+// before each launch.  x1[member][step parity] = (step + 1) << 32 | payload words
+// [Tmin lo, Tmin hi, live close cells, err << 24 | rim-list length], each written by its member
+// with one sc1 store per step.
+constexpr int kMaxK = 16;
+struct KX {
+  unsigned long long x1[kMaxK][2][4];
+};
+
 struct BandSrc {
   double* T;      // field (main grid)
   int* S;         // status: far -1, known 0, close 1 + close-list slot
@@ -42,6 +51,20 @@ struct BandSrc {
   long long lsum[3];
   long long lmax;
   long long sub[4];  // thread 0 inside phases: claim [neighbour+dedupe, loads, pushes], evaluate loads  // close cells handed to the band kernel in L0 (mode 1: fmm_exact_kernel)
+  // K-member kernel (fmm_band_k.hip): per-member slices (capL / K, capC / K) of the spill arrays
+  // of its LDS lists, the hand-over input list, rim lists and edge buffers
+  int* Lin;       // mode 1: close cells handed over by fmm_exact_kernel (nl0 of them)
+  int* L;         // close set: cells
+  double* Lt;     // close set: T
+  int* FS;        // free close-set slots
+  int* D;         // edge commits of the step: cells
+  double* Dv;     //   and values
+  int* Rx;        // claim items from other members' rim cells
+  int* rimc;      // [K][2][capR] published close rim cells (packed cell)
+  double* rimt;   //   and their T
+  double* E;      // edge buffers [2][ecells] (column-major edge columns, KGeom::eidx)
+  KX* kx;
+  int bbox[4];    // mode 1: rows / columns [z0, z1, x0, x1] of the main grid fmm_exact_kernel wrote
 };
 
 struct BandParams {
@@ -60,6 +83,10 @@ struct BandParams {
   const double* scz;
   double gox, goz;
   int prof;  // record BandSrc::ph / lsum (thread 0 reads the wall clock after each barrier)
+  int K;     // fmm_band_k: members per source (power of two <= kMaxK)
+  int wlog;  // fmm_band_k: stripe width log2
+  int capR;  // fmm_band_k: rim-list capacity per member and parity
+  long ecells;  // fmm_band_k: cells per edge buffer
 };
 
 struct RayJob {
@@ -111,6 +138,7 @@ hipError_t af_launch_init(const af::DevModel* M, af::InitJob* jobs, int njobs, a
 hipError_t af_launch_exact(const af::BandParams* P, hipStream_t stream);
 hipError_t af_launch_band(const af::BandParams* P, hipStream_t stream);
 hipError_t af_launch_band_pair(const af::BandParams* P, hipStream_t stream);
+hipError_t af_launch_band_k(const af::BandParams* P, hipStream_t stream);
 hipError_t af_launch_scale(double* T, long n, double sg, hipStream_t stream);
 hipError_t af_launch_rays(const af::RayParams* P, hipStream_t stream);
 hipError_t af_launch_pack_rays(const double* rx, const double* ry, const int* len, const long long* off, int nrays,
