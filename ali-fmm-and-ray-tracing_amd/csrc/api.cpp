@@ -22,7 +22,8 @@ namespace {
 
 struct Field {
   double* d = nullptr;
-  size_t bytes = 0;
+  size_t bytes = 0;  // the field (fnz x fnx doubles)
+  size_t alloc = 0;  // allocated: the field + the K-member band kernel's edge buffers after it
   int sg = 0, nz = 0, nx = 0;
   int64_t steps[4] = {0, 0, 0, 0};
   int64_t sweeps = 0;
@@ -36,13 +37,12 @@ struct Arena {  // per-chunk scratch, reused across calls
   int* own = nullptr;
   int* ax = nullptr;         // pair mode: 2 exchange lists per source
   af::PairX* px = nullptr;   // pair mode: exchange blocks
-  int* lists = nullptr;    // L0 | L1 | A | C | Cp | L | D | Rx per source
+  int* lists = nullptr;    // L0 | L1 | A | L | C | Cp | D | Rx | Bl | Bp per source
   double* dlists = nullptr;  // Lt0 | Lt1 | V | Dv per source
   int K = 0;                 // K-member kernel: members the rim lists are sized for
   long capR = 0, ecells = 0;
   int* rimc = nullptr;       // K-member kernel: rim lists [src][K][2][capR]
   double* rimt = nullptr;
-  double* E = nullptr;       // K-member kernel: edge buffers [src][2][ecells]
   af::KX* kx = nullptr;      // K-member kernel: exchange blocks
   double* Ts = nullptr;  // stage grids (travel_finer_grid), 2 per source
   int* Ss = nullptr;
@@ -144,7 +144,7 @@ static void dfree(void* p) {
 
 static void free_arena(Arena& a) {
   dfree(a.S); dfree(a.own); dfree(a.ax); dfree(a.px); dfree(a.lists); dfree(a.dlists); dfree(a.Ts); dfree(a.Ss); dfree(a.srcs); dfree(a.ho); dfree(a.jobs);
-  dfree(a.rimc); dfree(a.rimt); dfree(a.E); dfree(a.kx);
+  dfree(a.rimc); dfree(a.rimt); dfree(a.kx);
   dfree(a.dscx); dfree(a.dscz);
   a = Arena();
 }
@@ -482,12 +482,11 @@ static int ensure_arena(alifmm_ctx* ctx, int nsrc, long cells, long capL, long c
   HIPCHK(dalloc(&a.own, (size_t)nsrc * cells));
   HIPCHK(dalloc(&a.ax, (size_t)nsrc * 2 * capL));
   HIPCHK(dalloc(&a.px, nsrc));
-  HIPCHK(dalloc(&a.lists, (size_t)nsrc * (4 * capL + 4 * capC)));
+  HIPCHK(dalloc(&a.lists, (size_t)nsrc * (4 * capL + 6 * capC)));
   HIPCHK(dalloc(&a.dlists, (size_t)nsrc * (2 * capL + 2 * capC)));
   if (K > 1) {
     HIPCHK(dalloc(&a.rimc, (size_t)nsrc * K * 2 * capR));
     HIPCHK(dalloc(&a.rimt, (size_t)nsrc * K * 2 * capR));
-    HIPCHK(dalloc(&a.E, (size_t)nsrc * 2 * ecells));
   }
   HIPCHK(dalloc(&a.kx, nsrc));
   if (capS > 0) {
@@ -502,18 +501,19 @@ static int ensure_arena(alifmm_ctx* ctx, int nsrc, long cells, long capL, long c
   return ALIFMM_OK;
 }
 
-static int ensure_field(alifmm_ctx* ctx, int slot, int sg, int fz, int fx) {
+static int ensure_field(alifmm_ctx* ctx, int slot, int sg, int fz, int fx, long extra_cells = 0) {
   if ((int)ctx->fields.size() <= slot) ctx->fields.resize(slot + 1);
   Field& f = ctx->fields[slot];
-  size_t bytes = (size_t)fz * fx * sizeof(double);
-  if (f.d && f.bytes != bytes) {
+  const size_t bytes = (size_t)fz * fx * sizeof(double), need = bytes + (size_t)extra_cells * sizeof(double);
+  if (f.d && f.alloc < need) {
     dfree(f.d);
     f.d = nullptr;
   }
   if (!f.d) {
-    HIPCHK(hipMalloc((void**)&f.d, bytes));
-    f.bytes = bytes;
+    HIPCHK(hipMalloc((void**)&f.d, need));
+    f.alloc = need;
   }
+  f.bytes = bytes;
   f.sg = sg;
   f.nz = fz;
   f.nx = fx;
@@ -554,7 +554,7 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
   const long nstripes = (fx + W - 1) / W;
   const int K = kmode ? choose_members(ctx, n, nstripes) : 1;
   const long capR = K > 1 ? 2L * fz * ((nstripes + K - 1) / K) + 64 : 0;
-  const long ecells = K > 1 ? nstripes * 4L * fz : 0;
+  const long ecells = K > 1 ? nstripes * 4L * fz : 0;  // per edge buffer (4 columns per stripe)
   // the arena is sized for this chunk (reused while later chunks fit in it)
   int rc = ensure_arena(ctx, n, cells, capL, capC, capS, K, capR, ecells);
   if (rc) return rc;
@@ -570,7 +570,7 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
   std::vector<af::BandSrc> hs(n);
   for (int i = 0; i < n; i++) {
     int slot = first_slot + i;
-    if ((rc = ensure_field(ctx, slot, sg, fz, fx))) return rc;
+    if ((rc = ensure_field(ctx, slot, sg, fz, fx, 2 * ecells))) return rc;  // + the edge buffers
     af::BandSrc& b = hs[i];
     memset(&b, 0, sizeof b);
     b.T = ctx->fields[slot].d;
@@ -579,7 +579,7 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
     b.ax[0] = a.ax + (size_t)i * 2 * a.capL;
     b.ax[1] = b.ax[0] + a.capL;
     b.px = a.px + i;
-    int* base = a.lists + (size_t)i * (4 * a.capL + 4 * a.capC);
+    int* base = a.lists + (size_t)i * (4 * a.capL + 6 * a.capC);
     b.L0 = base;
     b.L1 = base + a.capL;
     b.A = base + 2 * a.capL;
@@ -588,6 +588,8 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
     b.Cp = b.C + a.capC;
     b.D = b.C + 2 * a.capC;
     b.Rx = b.C + 3 * a.capC;
+    b.Bl = b.C + 4 * a.capC;
+    b.Bp = b.C + 5 * a.capC;
     double* dbase = a.dlists + (size_t)i * (2 * a.capL + 2 * a.capC);
     b.Lt0 = dbase;
     b.Lt1 = dbase + a.capL;
@@ -602,7 +604,7 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
     if (K > 1) {
       b.rimc = a.rimc + (size_t)i * K * 2 * capR;
       b.rimt = a.rimt + (size_t)i * K * 2 * capR;
-      b.E = a.E + (size_t)i * 2 * ecells;
+      b.E = b.T + cells;  // edge buffers after the field (fmm_band_k.hip indexes both from T)
       HIPCHK(hipMemsetAsync(b.E, 0xFF, (size_t)2 * ecells * 8, fs));  // far: NaN
     }
     if (capS > 0) {
@@ -641,6 +643,7 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
   P.wlog = wlog;
   P.capR = (int)capR;
   P.ecells = ecells;
+  P.max_steps = 200L * (fz + fx) + 100000;
   HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
   if (sg == 1) {
     std::vector<af::InitJob> jobs(n);

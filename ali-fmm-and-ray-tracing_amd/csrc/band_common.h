@@ -111,8 +111,8 @@ AF_DEV int wave_excl_scan(int v, int& total) {
 // Column-stripe ownership of the K-member band kernel (fmm_band_k.hip): stripe s = x >> wlog
 // (W = 2^wlog columns, W >= 8) belongs to member s mod K (K a power of two).  EDGE cells lie
 // within 2 columns of a stripe boundary (another member's 12-point / 5x5 stencils read them; they
-// live in the edge buffers too, 4 columns per stripe, column-major: eidx), RIM cells next to one
-// (their 4-neighbour across the boundary belongs to another member).  K = 1: no edges, no rims.
+// are mirrored in the edge buffers: 4 columns per stripe, column-major, eidx), RIM cells next to
+// one (their 4-neighbour across the boundary belongs to another member).  K = 1: no edges, no rims.
 struct KGeom {
   int K, wlog, nz, nx;
   AF_DEV int owner(int x) const { return (x >> wlog) & (K - 1); }
@@ -124,10 +124,16 @@ struct KGeom {
     const int r = x & ((1 << wlog) - 1);
     return K > 1 && ((r == 0 && x > 0) || (r == (1 << wlog) - 1 && x < nx - 1));
   }
-  AF_DEV long eidx(int z, int x) const {
+  // edge-buffer column of an edge column x, and the entry of cell (z, x)
+  AF_DEV int ecol(int x) const {
     const int r = x & ((1 << wlog) - 1);
-    const int c = ((x >> wlog) << 2) + (r < 2 ? r : r - ((1 << wlog) - 4));
-    return (long)c * nz + z;
+    return ((x >> wlog) << 2) + (r < 2 ? r : r - ((1 << wlog) - 4));
+  }
+  AF_DEV int eidx(int z, int x) const { return ecol(x) * nz + z; }
+  // column x + dx (|dx| <= 2) of an own cell at column x lies in another member's stripe
+  AF_DEV bool other(int x, int dx) const {
+    const int r = (x & ((1 << wlog) - 1)) + dx;
+    return K > 1 && (r < 0 || r >= (1 << wlog)) && x + dx >= 0 && x + dx < nx;
   }
 };
 

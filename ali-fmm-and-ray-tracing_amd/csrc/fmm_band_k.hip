@@ -6,31 +6,37 @@
 // (s mod K).  A member keeps the close set, accepted / claimed lists and claim hash of its own cells
 // in LDS, and evaluates and commits only its own cells.  Per step (one cross-member exchange):
 //   P1  local Tmin over the own close set (LDS); publish the own close RIM cells (next to a stripe
-//       boundary) with T <= thr_ub = Tmin_loc + delta(Tmin_loc) — an upper bound of this step's
-//       acceptance threshold — then X1: every member stores (Tmin, live, err, #rim) as flagged
+//       boundary) with their T; then X1: every member stores (Tmin, live, err, #rim) as flagged
 //       words and reads everybody's -> global Tmin, threshold, termination
-//   P0  (after X1) copy-forward: last step's commits of EDGE cells (within 2 columns of a stripe
-//       boundary, i.e. readable by another member's 12-point / 5x5 stencils) into this step's
-//       edge buffer — after X1, because another member may read that buffer until it reaches X1
-//   P2  accept own close cells with T <= thr (-> known, slot freed)
+//   P2  accept own close cells with T <= thr (-> known, slot freed); bring this step's edge buffer
+//       up to date (below)
 //   P3  claim own non-known 4-neighbours of own accepted cells and of the neighbour members'
-//       accepted rim cells (read from their published lists: T <= thr), deduplicated (LDS hash)
+//       accepted rim cells (read from their published lists: T <= thr), deduplicated (LDS hash);
+//       cells whose stencil reaches another member's columns go to the end of the list
 //   P4  evaluate update() (fallback fouds18_A()) Jacobi-style against the state of the end of the
-//       previous step: own cells from T, other members' cells from the previous step's edge
-//       buffer (members write only the other parity during the step, so no second exchange)
-//   P5  commit: T, own slots, and edge cells also into this step's edge buffer
+//       previous step: own cells from T, other members' cells from the previous step's edge buffer
+//   P5  commit: T, own slots, and EDGE cells (within 2 columns of a stripe boundary: another
+//       member's 12-point / 5x5 stencils read them) also into this step's edge buffer
 // Why one exchange is enough: evaluation reads T (unchanged by acceptance) and validity
 // (known or close, unchanged by acceptance), so only WHICH cells are evaluated depends on this
-// step's acceptance — and another member's acceptance of a rim cell is decided by data that member
-// published before X1.  fouds18_A() reads known-ness after acceptance: another member's cell is
-// known iff its status is known, or close with T_prev <= thr (exactly that member's accept rule).
-// Results are identical to the one-workgroup kernel (and to any K): the same cells are accepted,
-// claimed and evaluated against the same state every step; only which CU does the work differs.
+// step's acceptance — and another member's acceptance of a rim cell (close, T <= thr) is decided
+// by data that member published before X1.  fouds18_A() reads known-ness after acceptance: another member's cell is
+// known iff it was known at the end of the previous step, or close with T <= thr (exactly that
+// member's accept rule).  Results are identical to the one-workgroup kernel (and to any K): the
+// same cells are accepted, claimed and evaluated against the same state every step; only which CU
+// does the work differs (tests/test_gpu_parity.py).
 //
-// Cross-CU data (flags, rim lists, edge buffers, statuses of edge cells) is stored with sc1 stores,
-// drained (vmcnt 0) by every wave before the flag, and read with sc1 loads after the flag
-// (MI355X_MICROARCH.md "inter-workgroup visibility", Valid forms).  Flags, rim lists and edge
-// buffers are double-buffered by step parity: a member can be at most one step ahead of another.
+// Edge buffers E[parity] (after T in the field's allocation; 4 columns per stripe, column-major):
+// E[k & 1] holds the state of the end
+// of step k, written during step k (a member may still read E[(k - 1) & 1] until every member has
+// passed step k's X1).  An edge cell's entry is T, with the sign bit set once the cell is known, so
+// the statuses of edge cells never cross CUs.  Keeping E[k & 1] complete: this step's commits and
+// acceptances write it directly; last step's commits (close cells whose slot carries the DIRTY
+// bit) are copied forward by the accept scan, last step's acceptances by a short list (P0).
+//
+// Cross-CU data (flags, rim lists, edge buffers) is stored with sc1 stores, drained (vmcnt 0) by
+// every wave before the flag, and read with sc1 loads after the flag (MI355X_MICROARCH.md
+// "inter-workgroup visibility", Valid forms).  Flags and rim lists are double-buffered by parity.
 #include <type_traits>
 #include "kernels.h"
 #include "local_ops.h"
@@ -42,31 +48,36 @@ namespace kb {
 
 constexpr int kThreads = 512;
 constexpr int kWaves = kThreads / 64;
-constexpr int kLcap = 2560, kAcap = 1024, kEcap = 1536, kDcap = 1024, kRcap = 1024;
+constexpr int kLcap = 2560, kAcap = 1024, kEcap = 1536, kBcap = 512, kDcap = 512, kRcap = 1024;
 constexpr int kHashLog = 13;
 constexpr int kHash = 1 << kHashLog;
 constexpr int kClaimU = 4;        // claim items per lane per pass
 constexpr int kHashItems = 6144;  // claim items deduplicated in the LDS hash (more: global stamps)
 constexpr int kStabLds = 64, kPtabLds = 722, kMatLds = 256;
+constexpr int kDirty = (int)0x80000000u;  // close-set slot: committed last step (edge cell)
+constexpr int kCell = 0x7fffffff;
 
 struct Lds {
   double red[kWaves];
   double Lt[kLcap];  // close set: T of the slot (+inf: free)
   double Vl[kEcap];  // evaluated values
-  double Dv[kDcap];  // edge commits of the step: value (copied forward next step)
   double stab[kStabLds * 5];
   double ptab[kPtabLds];
   MatRec mat[kMatLds];
-  int Ll[kLcap];  // close set: cell of the slot
+  int Ll[kLcap];  // close set: cell of the slot (| kDirty)
   int Fs[kLcap];  // free slots
   int Al[kAcap];  // accepted cells
-  int El[kEcap];  // claimed cells
+  int El[kEcap];  // claimed cells (interior first, then the boundary cells of Bl)
   int Ep[kEcap];  // slot of a claimed close cell, -1 for a far cell
-  int Dc[kDcap];  // edge commits of the step: cell
-  int Rx[kRcap];  // claim items from the neighbour members' accepted rim cells
+  int Bl[kBcap];  // claimed cells whose stencil reaches another member's columns
+  int Bp[kBcap];
+  int Dc[kDcap];  // edge cells accepted this step (copied forward next step) ...
+  double Dv[kDcap];  // ... and their T
+  int Rx[kRcap];  // claim items from the neighbour members' accepted rim cells; fallback list
   alignas(16) int H[kHash];
   double tmin_g, thr;
-  int nA, nE, nF, hi, taken, nD, nR, nRx, live_g, err_g, err, nFb;
+  unsigned long long nE2;  // claimed-list lengths: interior (low half), boundary (high half)
+  int nA, nF, hi, taken, nD, nR, nRx, live_g, err_g, err, nFb;
   int nrim[2];  // rim-list lengths of the neighbour members (left, right) this step
 };
 
@@ -74,22 +85,36 @@ AF_DEV unsigned hslot(int key) { return ((unsigned)key * 2654435761u) >> (32 - k
 AF_DEV unsigned hstep(int key) { return (((unsigned)key * 0x85ebca6bu) >> (32 - kHashLog)) | 1u; }
 
 // Stencil neighbourhood (NbFieldT) at the state of the end of the previous step: own columns from
-// T, other members' columns from the previous step's edge buffer.  12 independent loads in ONE form
-// (sc1: the edge buffer needs it, and one load instruction per point beats a divergent pair),
-// issued together; out-of-grid positions read the cell itself (update() never uses them).
-AF_DEV void load_nb(NbFieldT& nb, const double* T, const double* Eprev, const KGeom& g, int me, int z, int x) {
+// T, other members' columns from the previous step's edge buffer (the known sign dropped).  The
+// edge buffers follow T in the field's allocation, so every point is T[idx] with a 32-bit index
+// from one base (the loads keep the scalar-base + 32-bit-offset form): 12 independent loads in one
+// form (sc1: the edge buffer needs it), issued together.  Out-of-grid positions read a clamped
+// index (update() never uses them: it bounds-checks).
+AF_DEV void load_nb(NbFieldT& nb, const double* T, int eprv, int total, const KGeom& g, int z, int x) {
   const int dz[12] = {0, 0, 0, 0, -2, -1, 1, 2, -1, -1, 1, 1};
   const int dx[12] = {-2, -1, 1, 2, 0, 0, 0, 0, -1, 1, -1, 1};
   nb.iz = z;
   nb.ix = x;
-  const long p = (long)z * g.nx + x;
+  int zc[5], ro[5], cb[5];
+  bool ot[5];
+#pragma unroll
+  for (int r = 0; r < 5; r++) {  // rows z-2 .. z+2 (clamped)
+    zc[r] = min(max(z + r - 2, 0), g.nz - 1);
+    ro[r] = zc[r] * g.nx;
+  }
+#pragma unroll
+  for (int c = 0; c < 5; c++) {  // columns x-2 .. x+2: own (row-major T) or edge buffer (column-major)
+    ot[c] = g.other(x, c - 2);
+    cb[c] = ot[c] ? eprv + g.ecol(x + c - 2) * g.nz : x + c - 2;
+  }
   double t[12];
 #pragma unroll
   for (int k = 0; k < 12; k++) {
-    const int zz = z + dz[k], xx = x + dx[k];
-    const bool in = zz >= 0 && zz < g.nz && xx >= 0 && xx < g.nx;
-    const bool other = in && g.owner(xx) != me;
-    t[k] = gld_sc1(other ? Eprev + g.eidx(zz, xx) : T + (in ? (long)zz * g.nx + xx : p));
+    const int r = dz[k] + 2, c = dx[k] + 2;
+    int idx = cb[c] + (ot[c] ? zc[r] : ro[r]);
+    idx = idx < 0 ? 0 : idx >= total ? total - 1 : idx;
+    // 32-bit byte offset: the compiler can then use the scalar base + vector offset form
+    t[k] = fabs(gld_sc1((const double*)((const char*)T + ((unsigned)idx << 3))));
   }
   unsigned m = 0;
 #pragma unroll
@@ -101,10 +126,9 @@ AF_DEV void load_nb(NbFieldT& nb, const double* T, const double* Eprev, const KG
 }
 
 // fouds18_A() reads a 5x5 neighbourhood with "known" = status 0 after this step's acceptance.  The
-// (rare) fallback cells are processed in rounds: all threads stage each cell's neighbourhood
-// into LDS — T at the end of the previous step (own cells from T, other members' from the
-// previous edge buffer; NaN -> 0 as GField) and known-ness (own: status 0; another member's:
-// status 0, or close with T_prev <= thr, exactly that member's accept rule) — then one lane per
+// (rare) fallback cells are processed in rounds: all threads stage each cell's neighbourhood into
+// LDS — T at the end of the previous step (NaN -> 0 as GField) and known-ness (own cell: status 0;
+// another member's: known in the previous edge buffer, or close with T <= thr) — then one lane per
 // cell runs fouds18_A() on the staged window (few registers: the accessor is two LDS reads).
 constexpr int kFbRound = 128;  // cells per staging round (25 doubles each in the claim-hash space)
 struct Win5 {
@@ -194,20 +218,24 @@ __global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
   const HList<int, kEcap> EL{sh->El, B->C + me * hC};
   const HList<int, kEcap> EP{sh->Ep, B->Cp + me * hC};
   const HList<double, kEcap> VL{sh->Vl, B->V + me * hC};
+  const HList<int, kBcap> BL{sh->Bl, B->Bl + me * hC};
+  const HList<int, kBcap> BP{sh->Bp, B->Bp + me * hC};
   const HList<int, kDcap> DC{sh->Dc, B->D + me * hC};
   const HList<double, kDcap> DV{sh->Dv, B->Dv + me * hC};
   const HList<int, kRcap> RX{sh->Rx, B->Rx + me * hC};
   const int capL = (int)hL, capC = (int)hC;
-  // rim lists [member][parity][capR]; edge buffers [parity][ecells] (selected by arithmetic on the
+  // rim lists [member][parity][capR]; edge buffers [parity][cells] (selected by arithmetic on the
   // step parity: no dynamically indexed private arrays, which would live in scratch)
   int* const rimc = B->rimc;
   double* const rimt = B->rimt;
-  double* const E0 = B->E;
-  const long ecells = P.ecells;
+  // edge buffer of parity p: T + cells + p * ecells, compact (KGeom::eidx)
+  const int cells = nz * nx, ecells = (int)P.ecells;
+  double* const E0 = T + cells;
   if (tid == 0) {
     sh->hi = 0;
     sh->nF = 0;
     sh->nD = 0;
+    sh->nR = 0;
     sh->err = 0;
     sh->nrim[0] = sh->nrim[1] = 0;
   }
@@ -228,12 +256,13 @@ __global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
         x = c - z * nx;
         if (g.owner(x) == me) {
           t = H->ttn[k];
+          const bool known = H->cls[k] == 1;
           gst(T + c, t);
           if (g.edge(x)) {
-            gst_sc1(E0 + g.eidx(z, x), t);
-            gst_sc1(E0 + ecells + g.eidx(z, x), t);
+            gst_sc1(E0 + g.eidx(z, x), known ? -t : t);
+            gst_sc1(E0 + ecells + g.eidx(z, x), known ? -t : t);
           }
-          if (H->cls[k] == 1) gst_sc1(S + c, (int)kKnown);
+          if (known) gst(S + c, (int)kKnown);
           else push = true;
         }
       }
@@ -241,7 +270,7 @@ __global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
       if (s >= 0) {
         L.put(s, pk(z, x));
         Lt.put(s, t);
-        gst_sc1(S + c, 1 + s);
+        gst(S + c, 1 + s);
       }
     }
   } else {
@@ -256,9 +285,11 @@ __global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
       for (long k = tid; k < nb; k += kThreads) {
         const int z = z0 + (int)(k / w), x = x0 + (int)(k % w);
         if (g.owner(x) == me && g.edge(x)) {
-          const double t = gld(T + (long)z * nx + x);
-          gst_sc1(E0 + g.eidx(z, x), t);
-          gst_sc1(E0 + ecells + g.eidx(z, x), t);
+          const long f = (long)z * nx + x;
+          const double t = gld(T + f);
+          const double e = gld(S + f) == kKnown ? -t : t;
+          gst_sc1(E0 + g.eidx(z, x), e);
+          gst_sc1(E0 + ecells + g.eidx(z, x), e);
         }
       }
     }
@@ -277,7 +308,7 @@ __global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
       if (s >= 0) {
         L.put(s, pk(z, x));
         Lt.put(s, gld(T + c));
-        gst_sc1(S + c, 1 + s);
+        gst(S + c, 1 + s);
       }
     }
   }
@@ -294,8 +325,8 @@ __global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
   R.delta = launder_u(P.cdelta * P.dnx / P.vmax);
   R.t0 = launder_u(P.r0 * P.dnx / P.vmax);
   long long steps = 0, myupd = 0;
-  // profile (P.prof): thread 0 of member 0; phases [P0+P1+X1, accept, claim (incl. rim read),
-  // evaluate, fallback, commit], sub [X1 wait, rim read, claim dedupe, claim status loads]
+  // profile (P.prof): thread 0 of member 0; phases [P1 + X1, accept + rim read, claim,
+  // evaluate, fallback, commit], sub [X1 wait, rim read, claim dedupe, drain before X1]
   const bool prof = PROF && tid == 0 && me == 0;
   long long ph[6] = {0, 0, 0, 0, 0, 0}, sub[4] = {0, 0, 0, 0}, ls[3] = {0, 0, 0}, lmax = 0;
   long long tk = prof ? wall_clock64() : 0;
@@ -316,37 +347,19 @@ __global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
     const int par = (int)(steps & 1), prv = par ^ 1;
     double* const Epar = E0 + par * ecells;
     const double* const Eprv = E0 + prv * ecells;
+    const int eprv = cells + prv * ecells;  // Eprv as an index from T
     const int hi = sh->hi;
-    // ---- P1: local Tmin over the close set (LDS); clear the claim hash ----
+    // ---- P1: local Tmin over the close set (LDS); publish every own close RIM cell (cell, T) for
+    // the neighbour members, which keep those with T <= thr; clear the claim hash ----
     double tmin = INFINITY;
-    if (hi <= kLcap) {
-      for (int e = tid; e < hi; e += kThreads) tmin = fmin(tmin, Lt.lds(e));
-    } else {
-      for (int e = tid; e < hi; e += kThreads) tmin = fmin(tmin, Lt.get(e));
-    }
-    for (int k = tid * 4; k < kHash; k += kThreads * 4) *(int4*)&sh->H[k] = make_int4(0, 0, 0, 0);
-    tmin = wave_min(tmin);
-    if (lane == 0) sh->red[wv] = tmin;
-    if (tid == 0) {
-      sh->nA = 0;
-      sh->nE = 0;
-      sh->nFb = 0;
-      sh->taken = 0;
-      sh->nR = 0;
-      sh->nRx = 0;
-    }
-    __syncthreads();
-    tmin = sh->red[0];
-    for (int w = 1; w < kWaves; w++) tmin = fmin(tmin, sh->red[w]);
-    const double delta = launder_u(R.delta), t0 = launder_u(R.t0);
-    // publish own close rim cells that may be accepted this step (T <= thr_ub >= thr)
-    if (K > 1) {
-      const double thr_ub = tmin + ((t0 > 0 && tmin < t0) ? delta * (tmin / t0) : delta);
+    {
+      const bool lo = hi <= kLcap;  // (uniform) close set in LDS
       for (int e0 = wv * 64; e0 < hi; e0 += kThreads) {
         const int e = e0 + lane;
-        const double t = e < hi ? Lt.get(e) : INFINITY;
-        const int c = t <= thr_ub ? L.get(e) : 0;
-        const bool pub = t <= thr_ub && g.rim(pkx(c));
+        const double t = e < hi ? (lo ? Lt.lds(e) : Lt.get(e)) : INFINITY;
+        tmin = fmin(tmin, t);
+        const int c = (K > 1 && t < INFINITY) ? ((lo ? L.lds(e) : L.get(e)) & kCell) : 0;
+        const bool pub = K > 1 && t < INFINITY && g.rim(pkx(c));
         const int s = wave_push(&sh->nR, pub, P.capR, &sh->err);
         if (s >= 0) {
           gst_sc1(rimc + ((long)me * 2 + par) * P.capR + s, c);
@@ -354,8 +367,24 @@ __global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
         }
       }
     }
+    for (int k = tid * 4; k < kHash; k += kThreads * 4) *(int4*)&sh->H[k] = make_int4(0, 0, 0, 0);
+    tmin = wave_min(tmin);
+    if (lane == 0) sh->red[wv] = tmin;
+    if (tid == 0) {
+      sh->nA = 0;
+      sh->nE2 = 0;
+      sh->nFb = 0;
+      sh->taken = 0;
+      sh->nRx = 0;
+    }
+    __syncthreads();
+    tmin = sh->red[0];
+    for (int w = 1; w < kWaves; w++) tmin = fmin(tmin, sh->red[w]);
+    const double delta = launder_u(R.delta), t0 = launder_u(R.t0);
+    const long long tdr = prof ? wall_clock64() : 0;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores have completed
     __syncthreads();
+    AF_SUBT(3, tdr)
     const long long tx1 = prof ? wall_clock64() : 0;
     if (K > 1) {
       if (tid == 0) {
@@ -375,19 +404,20 @@ __global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
       sh->live_g = hi - sh->nF;
       sh->err_g = sh->err;
     }
+    if (tid == 0 && steps >= P.max_steps) sh->err = 8;  // a band that never finishes (cannot happen
+                                                       // with valid inputs): stop instead of hanging
     __syncthreads();
     AF_SUBT(0, tx1)
     AF_TICK(0)
     if (sh->live_g <= 0 || sh->err_g || sh->err) break;
-    // ---- P0: copy last step's edge commits forward into this step's edge buffer.  Only now: every
-    // member has passed this step's X1, i.e. finished the previous step, whose evaluation read this
-    // buffer as the state of two steps ago ----
+    // ---- P0: last step's accepted edge cells into this step's edge buffer.  Only now: every member
+    // has passed this step's X1, i.e. finished the previous step, which read this buffer ----
     if (K > 1) {
       const int nD = min(sh->nD, capC);
       for (int d = tid; d < nD; d += kThreads) {
-        const int c = DC.get(d);
-        gst_sc1(Epar + g.eidx(pkz(c), pkx(c)), DV.get(d));
+        gst_sc1(Epar + g.eidx(pkz(DC.get(d)), pkx(DC.get(d))), -DV.get(d));
       }
+      __syncthreads();  // the list is refilled by this step's acceptance
     }
     tmin = sh->tmin_g;
     double dl = delta;
@@ -397,21 +427,49 @@ __global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
       sh->thr = thr;
       sh->nD = 0;
     }
-    // ---- P2: accept own close cells ----
+    __syncthreads();
+    // the neighbour members' rim lists: loads issued now, consumed after the accept scan (P3a)
+    int rpc = -1;
+    double rpt = INFINITY;
+    const int nq = K == 1 ? 0 : K == 2 ? 1 : 2;
+    const int nr0 = nq > 0 ? min(sh->nrim[0], P.capR) : 0;
+    const int nr1 = nq > 1 ? min(sh->nrim[1], P.capR) : 0;
+    if (tid < nr0 + nr1) {
+      const int side = tid < nr0 ? 0 : 1, e = tid < nr0 ? tid : tid - nr0;
+      const int q = (me + (side == 0 ? -1 : 1)) & (K - 1);
+      rpc = gld_sc1(rimc + ((long)q * 2 + par) * P.capR + e);
+      rpt = gld_sc1(rimt + ((long)q * 2 + par) * P.capR + e);
+    }
+    // ---- P2: accept own close cells; copy last step's commits of edge cells forward ----
     auto accept = [&](auto lds_only) {
       constexpr bool LO = decltype(lds_only)::value;
       for (int e0 = wv * 64; e0 < hi; e0 += kThreads) {
         const int e = e0 + lane;
         const double t = e < hi ? (LO ? Lt.lds(e) : Lt.get(e)) : INFINITY;
+        const bool live = t < INFINITY;
         const bool acc = t <= thr;
-        const int c = acc ? (LO ? L.lds(e) : L.get(e)) : 0;
+        const int raw = live ? (LO ? L.lds(e) : L.get(e)) : 0;
+        const int c = raw & kCell;
+        if (K > 1 && live) {
+          const bool ed = g.edge(pkx(c));
+          if (raw < 0 || (acc && ed)) {  // dirty (committed last step) or accepted edge cell
+            gst_sc1(Epar + g.eidx(pkz(c), pkx(c)), acc ? -t : t);
+            if (raw < 0 && !acc) {
+              if (LO) L.put_lds(e, c);
+              else L.put(e, c);
+            }
+          }
+          const int d = wave_push(&sh->nD, acc && ed, capC, &sh->err);
+          if (d >= 0) {
+            DC.put(d, c);
+            DV.put(d, t);
+          }
+        }
         int sa, sf;
         wave_push2(&sh->nA, &sh->nF, acc, capL, &sh->err, sa, sf);
         if (sa >= 0) {
           AL.put(sa, c);
-          const long f = (long)pkz(c) * nx + pkx(c);
-          if (g.edge(pkx(c))) gst_sc1(S + f, (int)kKnown);
-          else gst(S + f, (int)kKnown);
+          gst(S + pk_flat(c, nx), (int)kKnown);
           if (LO) {
             Lt.put_lds(e, INFINITY);
             FS.put_lds(sf, e);
@@ -424,32 +482,31 @@ __global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
     };
     if (hi <= kLcap) accept(std::true_type{});
     else accept(std::false_type{});
-    // the copy-forward stores above precede this step's edge commits to the same addresses
-    if (K > 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // ---- P3a: the neighbour members' accepted rim cells -> claim items (their cross neighbour) ----
     const long long trr = prof ? wall_clock64() : 0;
     if (K > 1) {
-      const int nq = K == 2 ? 1 : 2;
-      for (int side = 0; side < nq; side++) {
-        const int q = (me + (side == 0 ? -1 : 1)) & (K - 1);
-        const int nr = min(sh->nrim[side], P.capR);
-        const int* rc = rimc + ((long)q * 2 + par) * P.capR;
-        const double* rt = rimt + ((long)q * 2 + par) * P.capR;
-        for (int e0 = wv * 64; e0 < nr; e0 += kThreads) {
-          const int e = e0 + lane;
-          int c = -1;
-          if (e < nr) {
-            const int pc = gld_sc1(rc + e);
-            const double pt = gld_sc1(rt + e);
-            if (pt <= thr) {
-              const int px = pkx(pc), r = px & ((1 << g.wlog) - 1);
-              const int cx = r == 0 ? px - 1 : px + 1;  // across the stripe boundary
-              if (cx >= 0 && cx < nx && g.owner(cx) == me) c = pk(pkz(pc), cx);
-            }
-          }
-          const int s = wave_push(&sh->nRx, c >= 0, capC, &sh->err);
-          if (s >= 0) RX.put(s, c);
+      auto rim_item = [&](int pc, double pt) {  // the cross-boundary neighbour of an accepted rim cell
+        int c = -1;
+        if (pt <= thr) {
+          const int px = pkx(pc), r = px & ((1 << g.wlog) - 1);
+          const int cx = r == 0 ? px - 1 : px + 1;
+          if (cx >= 0 && cx < nx && g.owner(cx) == me) c = pk(pkz(pc), cx);
         }
+        const int s = wave_push(&sh->nRx, c >= 0, capC, &sh->err);
+        if (s >= 0) RX.put(s, c);
+      };
+      rim_item(rpc, rpt);  // the prefetched first kThreads entries
+      for (int e0 = kThreads + wv * 64; e0 < nr0 + nr1; e0 += kThreads) {  // the rest (long lists)
+        const int e = e0 + lane;
+        int pc = -1;
+        double pt = INFINITY;
+        if (e < nr0 + nr1) {
+          const int side = e < nr0 ? 0 : 1, i = e < nr0 ? e : e - nr0;
+          const int q = (me + (side == 0 ? -1 : 1)) & (K - 1);
+          pc = gld_sc1(rimc + ((long)q * 2 + par) * P.capR + i);
+          pt = gld_sc1(rimt + ((long)q * 2 + par) * P.capR + i);
+        }
+        rim_item(pc, pt);
       }
     }
     __syncthreads();
@@ -515,46 +572,74 @@ __global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
       }
       if (prof) __builtin_amdgcn_s_waitcnt(0);
       AF_SUBT(2, tdd)
-      const long long tcl = prof ? wall_clock64() : 0;
 #pragma unroll
       for (int u = 0; u < kClaimU; u++) {
         const long f = r[u] >= 0 ? (long)pkz(r[u]) * nx + pkx(r[u]) : 0;
-        // own cells; sc1: edge cells' statuses are stored sc1 (for other members), and an sc1 store
-        // does not refresh this CU's L1 copy of the line
-        s[u] = r[u] >= 0 ? gld_sc1(S + f) : (int)kKnown;
+        s[u] = r[u] >= 0 ? gld(S + f) : (int)kKnown;  // own cells, stored by this workgroup only
         o[u] = (!use_hash && r[u] >= 0) ? gatomic_max(own + f, stamp) : -1;
       }
       // u-major list order: consecutive entries are neighbours of consecutive accepted cells, so
-      // the lanes of an evaluating wave read overlapping stencils (fewer distinct cache lines)
-      unsigned long long bm[kClaimU];
-      int cnt = 0;
+      // the lanes of an evaluating wave read overlapping stencils (fewer distinct cache lines).
+      // Cells next to another member's columns go to the boundary list, evaluated last: their
+      // stencils read the edge buffer, whose lines come from further away (sc1 stores leave L2)
+      unsigned long long bi[kClaimU], bb[kClaimU];
+      int ci = 0, cb = 0;
 #pragma unroll
       for (int u = 0; u < kClaimU; u++) {
-        bm[u] = __ballot(s[u] != kKnown && o[u] < stamp);
-        cnt += __popcll(bm[u]);
+        const bool take = s[u] != kKnown && o[u] < stamp;
+        const bool bnd = take && g.edge(pkx(r[u]));
+        bi[u] = __ballot(take && !bnd);
+        bb[u] = __ballot(bnd);
+        ci += __popcll(bi[u]);
+        cb += __popcll(bb[u]);
       }
-      AF_SUBT(3, tcl)
-      int base = 0;
-      if (lane == 0 && cnt) base = atomicAdd(&sh->nE, cnt);
-      base = __shfl(base, 0);
+      // one LDS atomic per wave and pass for both lists (counters packed in 64 bits)
+      unsigned long long base2 = 0;
+      if (lane == 0 && (ci | cb))
+        base2 = atomicAdd(&sh->nE2, (unsigned long long)ci | ((unsigned long long)cb << 32));
+      base2 = __shfl(base2, 0);
+      int basei = (int)(unsigned)base2, baseb = (int)(unsigned)(base2 >> 32);
       const unsigned long long lt = (1ull << lane) - 1ull;
 #pragma unroll
       for (int u = 0; u < kClaimU; u++) {
-        if ((bm[u] >> lane) & 1ull) {
-          const int pos = base + __popcll(bm[u] & lt);
+        const int slot = s[u] > 0 ? s[u] - 1 : -1;
+        if ((bi[u] >> lane) & 1ull) {
+          const int pos = basei + __popcll(bi[u] & lt);
           if (pos < capC) {
             EL.put(pos, r[u]);
-            EP.put(pos, s[u] > 0 ? s[u] - 1 : -1);
+            EP.put(pos, slot);
           } else {
             sh->err = 2;
           }
         }
-        base += __popcll(bm[u]);
+        if ((bb[u] >> lane) & 1ull) {
+          const int pos = baseb + __popcll(bb[u] & lt);
+          if (pos < capC) {
+            BL.put(pos, r[u]);
+            BP.put(pos, slot);
+          } else {
+            sh->err = 2;
+          }
+        }
+        basei += __popcll(bi[u]);
+        baseb += __popcll(bb[u]);
       }
     }
+    // this step's edge-buffer stores (accept scan, P0) precede this step's commits to the same
+    // addresses (a wave that issued no load since has not waited for them yet)
+    if (K > 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    const int nEi = min((int)(unsigned)sh->nE2, capC);
+    const int nEb = min((int)(unsigned)(sh->nE2 >> 32), capC - nEi);
+    if (nEb > 0) {  // boundary cells after the interior ones
+      for (int j2 = tid; j2 < nEb; j2 += kThreads) {
+        EL.put(nEi + j2, BL.get(j2));
+        EP.put(nEi + j2, BP.get(j2));
+      }
+      __syncthreads();
+    }
     AF_TICK(2)
-    const int nE = min(sh->nE, capC);
+    const int nE = nEi + nEb;
     // ---- P4: evaluate ----
     const bool lds_e = nE <= kEcap;
     const double dnx_e = launder_u(R.dnx);
@@ -562,7 +647,8 @@ __global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
       const int r = lds_e ? EL.lds(e) : EL.get(e);
       const int z = pkz(r), x = pkx(r);
       NbFieldT nb;  // stencil loads first, then the material id: one memory round trip
-      load_nb(nb, T, Eprv, g, me, z, x);
+      if (e - lane + 64 <= nEi) nb.load(T, nz, nx, z, x);  // (wave-uniform) interior cells: T only
+      else load_nb(nb, T, eprv, cells + 2 * ecells, g, z, x);
       const CellMat cm = band_mat<LDSMAT>(M, sh->mat, sh->stab, R.mv, z, x);
       const double v = update(nb, M, cm, z, x, dnx_e, nz, nx);
       if (lds_e) VL.put_lds(e, v);
@@ -603,11 +689,14 @@ __global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
           bool kn = false;
           if (zz >= 0 && zz < nz && xx >= 0 && xx < nx) {
             const long f = (long)zz * nx + xx;
-            const bool mine = g.owner(xx) == me;
-            const double tp = mine ? gld(T + f) : gld_sc1(Eprv + g.eidx(zz, xx));
-            const int st = gld_sc1(S + f);
-            t = far0(tp);
-            kn = st == kKnown || (!mine && st > 0 && tp <= thr_f);
+            if (g.owner(xx) == me) {
+              t = far0(gld(T + f));
+              kn = gld(S + f) == kKnown;
+            } else {  // known at the end of the last step (sign), or accepted now (close, T <= thr)
+              const double ev = gld_sc1(Eprv + g.eidx(zz, xx));
+              t = far0(fabs(ev));
+              kn = ev == ev && (signbit(ev) || ev <= thr_f);
+            }
           }
           win[i] = t;
           if (kn) atomicOr(&wmask[i / 25], 1u << o);
@@ -631,8 +720,10 @@ __global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
         __syncthreads();
       }
     }
+    __syncthreads();
     AF_TICK(4)
-    // ---- P5: commit own cells; edge cells also into this step's edge buffer ----
+    // ---- P5: commit own cells; edge cells also into this step's edge buffer (slot marked DIRTY:
+    // the next step's accept scan copies them forward) ----
     const int nF = sh->nF;
     auto commit = [&](auto lds_only) {
       constexpr bool LO = decltype(lds_only)::value;
@@ -645,13 +736,18 @@ __global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
           r = LO ? EL.lds(e) : EL.get(e);
           v = LO ? VL.lds(e) : VL.get(e);
           const int p = LO ? EP.lds(e) : EP.get(e);
-          const int z = pkz(r), x = pkx(r);
-          gst(T + (long)z * nx + x, v);
-          ed = g.edge(x);
-          if (ed) gst_sc1(Epar + g.eidx(z, x), v);
+          const long f = (long)pkz(r) * nx + pkx(r);
+          gst(T + f, v);
+          ed = g.edge(pkx(r));
+          if (ed) gst_sc1(Epar + g.eidx(pkz(r), pkx(r)), v);
           if (p >= 0) {
-            if (LO) Lt.put_lds(p, v);
-            else Lt.put(p, v);
+            if (LO) {
+              Lt.put_lds(p, v);
+              if (ed) L.put_lds(p, r | kDirty);
+            } else {
+              Lt.put(p, v);
+              if (ed) L.put(p, r | kDirty);
+            }
           } else {
             fresh = true;
           }
@@ -663,21 +759,14 @@ __global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
             sh->err = 2;
           } else {
             if (LO) {
-              L.put_lds(slot, r);
+              L.put_lds(slot, ed ? (r | kDirty) : r);
               Lt.put_lds(slot, v);
             } else {
-              L.put(slot, r);
+              L.put(slot, ed ? (r | kDirty) : r);
               Lt.put(slot, v);
             }
-            const long f = (long)pkz(r) * nx + pkx(r);
-            if (ed) gst_sc1(S + f, 1 + slot);
-            else gst(S + f, 1 + slot);
+            gst(S + (long)pkz(r) * nx + pkx(r), 1 + slot);
           }
-        }
-        const int ds = wave_push(&sh->nD, ed, capC, &sh->err);
-        if (ds >= 0) {
-          DC.put(ds, r);
-          DV.put(ds, v);
         }
       }
     };
@@ -688,6 +777,7 @@ __global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
       const int tk_ = sh->taken;
       sh->nF = max(0, nF - tk_);
       sh->hi = hi + max(0, tk_ - nF);
+      sh->nR = 0;  // the next step's rim list
     }
     if (prof) {
       ls[0] += hi - sh->nF;

@@ -60,6 +60,8 @@ struct BandSrc {
   int* D;         // edge commits of the step: cells
   double* Dv;     //   and values
   int* Rx;        // claim items from other members' rim cells
+  int* Bl;        // claimed cells next to other members' columns
+  int* Bp;        //   and their close-set slots
   int* rimc;      // [K][2][capR] published close rim cells (packed cell)
   double* rimt;   //   and their T
   double* E;      // edge buffers [2][ecells] (column-major edge columns, KGeom::eidx)
@@ -87,6 +89,7 @@ struct BandParams {
   int wlog;  // fmm_band_k: stripe width log2
   int capR;  // fmm_band_k: rim-list capacity per member and parity
   long ecells;  // fmm_band_k: cells per edge buffer
+  long max_steps;  // fmm_band_k: a band still running after this many steps stops with error 8
 };
 
 struct RayJob {

@@ -1,0 +1,57 @@
+"""Time the K-member band kernel on C4 (128 sources, auto K; 16 sources, auto K) with the phase
+profile, and fingerprint the fields (bit-identity across variants).  ALIFMM_LIB selects the library.
+python tools/kbench.py NAME  -> one JSON line"""
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "ali-fmm-and-ray-tracing_amd"))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+import _alifmm  # noqa: E402
+import workloads as W  # noqa: E402
+
+PH = ["p1_x1", "accept_rim", "claim", "evaluate", "fallback", "commit"]
+SUB = ["x1_wait", "rim_read", "dedupe", "drain"]
+
+
+def main():
+    name = sys.argv[1]
+    sizes = [int(a) for a in sys.argv[2:]] or [128, 16]
+    ctx = _alifmm.Context(0)
+    for opt in ("kernel", "members", "stripe_log", "cdelta"):  # ALIFMM_OPT_<NAME>=value
+        v = os.environ.get("ALIFMM_OPT_" + opt.upper())
+        if v is not None:
+            ctx.set_option(opt, float(v))
+    vt = W.default_table()
+    ctx.set_model(*W.weldlike_model(), vt, vt, W.weldlike_dnx())
+    sx, sz = W.c4_sources(128)
+    out = {"variant": name}
+    for ns in sizes:
+        ctx.travel(sx[:ns], sz[:ns], copy_out=False)
+        best = None
+        for _ in range(2):
+            ctx.travel(sx[:ns], sz[:ns], copy_out=False)
+            ti, tb, tt = ctx.last_timing()
+            best = tb if best is None else min(best, tb)
+        h = hashlib.sha256()
+        for i in (0, ns // 2, ns - 1):
+            h.update(ctx.get_field(i, 1).tobytes())
+        ctx.set_option("prof", 1)
+        ctx.travel(sx[:ns], sz[:ns], copy_out=False)
+        ctx.set_option("prof", 0)
+        p = ctx.band_profile(0)
+        st = int(ctx.source_stats(0)[0][3])
+        prof = {k: round(p[i] / 100.0 / st, 2) for i, k in enumerate(PH)}
+        prof.update({k: round(p[10 + i] / 100.0 / st, 2) for i, k in enumerate(SUB)})
+        out[str(ns)] = {"k": int(ctx.get_option("last_k")), "band_ms": round(best, 1), "init_ms": round(ti, 1),
+                        "fields": h.hexdigest()[:16], "us_per_step": prof}
+    print(json.dumps(out), flush=True)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
