@@ -64,6 +64,7 @@ def _load():
             "alifmm_travel": (_i, [_p, _i, _i, _p, _p, _i, _p]),
             "alifmm_get_field": (_i, [_p, _i, _p]),
             "alifmm_release_fields": (_i, [_p]),
+            "alifmm_copy_fields": (_i, [_p, _i, _i, _p, _i, _p]),
             "alifmm_find_rays": (_i, [_p, _i, _p, _p, _p, _p, _p, _p, _p, _l]),
             "alifmm_take_rays": (_i, [_p, _p, _l, _p]),
             "alifmm_source_stats": (_i, [_p, _i, _p, _p]),
@@ -73,6 +74,7 @@ def _load():
             "alifmm_time_between_points": (_i, [_p, _i, _p, _p, _p, _p, _i, _p]),
             "alifmm_local_ops": (_i, [_p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i,
                                       _p]),
+            "alifmm_fouds18_band": (_i, [_p, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _p]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -212,6 +214,26 @@ class Context:
             raise ValueError("field shape %s does not match subgrid %d" % (data.shape, subgrid))
         self._chk(lib().alifmm_put_field(self._h, int(slot), int(subgrid), _ptr(data)), "put_field")
 
+    def copy_fields(self, first_slot, n, subgrid, out=None, dst_kind=0):
+        """Resident fields of slots first_slot .. first_slot+n-1 as one (n, fnz, fnx) host array
+        (alifmm_copy_fields: pageable destinations go through the pinned staging ring).
+        Returns (array, GB/s)."""
+        fz, fx = self.field_shape(subgrid)
+        if out is None:
+            out = np.empty((n, fz, fx))
+        g = ctypes.c_double(0)
+        self._chk(lib().alifmm_copy_fields(self._h, int(first_slot), int(n), _ptr(out), int(dst_kind), ctypes.byref(g)),
+                  "copy_fields")
+        return out, g.value
+
+    def copy_fields_to_device(self, first_slot, n, dev_ptr):
+        """Copy resident fields into device memory of this GPU at dev_ptr (e.g. a torch tensor's
+        data_ptr(), for an RCCL gather).  Returns GB/s."""
+        g = ctypes.c_double(0)
+        self._chk(lib().alifmm_copy_fields(self._h, int(first_slot), int(n), ctypes.c_void_p(int(dev_ptr)), 2,
+                                           ctypes.byref(g)), "copy_fields")
+        return g.value
+
     def release_fields(self):
         self._chk(lib().alifmm_release_fields(self._h), "release_fields")
 
@@ -290,6 +312,18 @@ class Context:
                 _ci64(cvelpn), _c64(cvm)]
         self._chk(lib().alifmm_local_ops(self._h, int(op), n, pz, px, _ptr(ttn), _ptr(nsts), *[_ptr(a) for a in args],
                                          _ptr(cst), _ptr(tab), tab.shape[1], _ptr(out)), "local_ops")
+        return out
+
+    def fouds18_band(self, ttn, nsts, iz, ix, dnx, dnz, nnz_arg, nnx_arg, mz, mx, quant=0):
+        """fouds18_A() as the band kernel evaluates it: material of resident-model cell (mz, mx)
+        through the per-material record and precomputed slownesses (alifmm_fouds18_band)."""
+        ttn = _c64(ttn)
+        n, pz, px = ttn.shape
+        out = np.empty(n)
+        nsts = _ci32(nsts)
+        args = [_ci32(iz), _ci32(ix), _c64(dnx), _c64(dnz), _ci32(nnz_arg), _ci32(nnx_arg), _ci32(mz), _ci32(mx)]
+        self._chk(lib().alifmm_fouds18_band(self._h, n, pz, px, _ptr(ttn), _ptr(nsts), *[_ptr(a) for a in args],
+                                            int(quant), _ptr(out)), "fouds18_band")
         return out
 
 

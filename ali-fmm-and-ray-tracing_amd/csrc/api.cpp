@@ -11,8 +11,11 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <atomic>
+#include <chrono>
 #include <map>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/alifmm.h"
@@ -35,10 +38,8 @@ struct Arena {  // per-chunk scratch, reused across calls
   long cells = 0, capL = 0, capC = 0, capS = 0;
   int* S = nullptr;
   int* own = nullptr;
-  int* ax = nullptr;         // pair mode: 2 exchange lists per source
-  af::PairX* px = nullptr;   // pair mode: exchange blocks
-  int* lists = nullptr;    // L0 | L1 | A | L | C | Cp | D | Rx | Bl | Bp per source
-  double* dlists = nullptr;  // Lt0 | Lt1 | V | Dv per source
+  int* lists = nullptr;    // Lin | FS | A | L | C | Cp | D | Rx | Bl | Bp per source
+  double* dlists = nullptr;  // Lt | V | Dv per source
   int K = 0;                 // K-member kernel: members the rim lists are sized for
   long capR = 0, ecells = 0;
   int* rimc = nullptr;       // K-member kernel: rim lists [src][K][2][capR]
@@ -84,13 +85,10 @@ struct alifmm_ctx {
   int exact_r = 20;
   int batch = 256;
   int prof = 0;
-  int pair = 1;     // two workgroups per source when the chunk fits the device (fmm_band_pair.hip)
-  int kernel = 0;   // band kernel: 0 K-member (fmm_band_k.hip), 1 pair / single (round-1 kernels)
-  int members = 0;  // K-member kernel: workgroups per source (0: as many as the device fits, <= 16)
-  int stripe_log = 6;  // K-member kernel: stripe width log2
-  int last_k = 0;   // members per source of the last band launch
+  int members = 0;     // band kernel: workgroups per source (0: as many as the device fits, <= 16)
+  int stripe_log = 0;  // band kernel: stripe width log2 (0: 6 for K <= 4, 4 for K >= 8)
+  int last_k = 0;      // members per source of the last band launch
   int n_cu = 0;
-  int last_pair = 0;
   long cap_scale = 1;
   // state
   std::vector<Field> fields;
@@ -109,6 +107,11 @@ struct alifmm_ctx {
     af::RayJob* jobs = nullptr;
     long long* off = nullptr;
   } rb;
+  // pinned staging ring of alifmm_copy_fields (pageable destinations)
+  static constexpr int kPinBufs = 4;
+  static constexpr size_t kPinBytes = 32u << 20;
+  void* pin[kPinBufs] = {};
+  hipEvent_t pin_ev[kPinBufs] = {};
 };
 
 static void free_ray_bufs(alifmm_ctx* c) {
@@ -143,7 +146,7 @@ static void dfree(void* p) {
 }
 
 static void free_arena(Arena& a) {
-  dfree(a.S); dfree(a.own); dfree(a.ax); dfree(a.px); dfree(a.lists); dfree(a.dlists); dfree(a.Ts); dfree(a.Ss); dfree(a.srcs); dfree(a.ho); dfree(a.jobs);
+  dfree(a.S); dfree(a.own); dfree(a.lists); dfree(a.dlists); dfree(a.Ts); dfree(a.Ss); dfree(a.srcs); dfree(a.ho); dfree(a.jobs);
   dfree(a.rimc); dfree(a.rimt); dfree(a.kx);
   dfree(a.dscx); dfree(a.dscz);
   a = Arena();
@@ -241,6 +244,10 @@ int alifmm_ctx_destroy(alifmm_ctx* ctx) {
   alifmm_release_fields(ctx);
   free_arena(ctx->arena);
   free_ray_bufs(ctx);
+  for (int b = 0; b < alifmm_ctx::kPinBufs; b++) {
+    if (ctx->pin[b]) (void)hipHostFree(ctx->pin[b]);
+    if (ctx->pin_ev[b]) (void)hipEventDestroy(ctx->pin_ev[b]);
+  }
   free_model(ctx);
   for (auto& e : ctx->ev) if (e) (void)hipEventDestroy(e);
   if (ctx->fill) {
@@ -261,12 +268,10 @@ int alifmm_set_option(alifmm_ctx* ctx, const char* name, double value) {
   else if (!strcmp(name, "r0") && value >= 0) ctx->r0 = value;
   else if (!strcmp(name, "batch") && value >= 1) ctx->batch = (int)value;
   else if (!strcmp(name, "prof")) ctx->prof = value != 0;
-  else if (!strcmp(name, "pair")) ctx->pair = value != 0;
   else if (!strcmp(name, "exact_r") && value >= 0 && value <= 48) ctx->exact_r = (int)value;
-  else if (!strcmp(name, "kernel") && (value == 0 || value == 1)) ctx->kernel = (int)value;
   else if (!strcmp(name, "members") && (value == 0 || value == 1 || value == 2 || value == 4 || value == 8 || value == 16))
     ctx->members = (int)value;
-  else if (!strcmp(name, "stripe_log") && value >= 3 && value <= 12) ctx->stripe_log = (int)value;
+  else if (!strcmp(name, "stripe_log") && (value == 0 || (value >= 3 && value <= 12))) ctx->stripe_log = (int)value;
   else return fail(ctx, ALIFMM_E_ARG, "unknown option or bad value: %s=%g", name, value);
   return ALIFMM_OK;
 }
@@ -278,18 +283,17 @@ int alifmm_get_option(alifmm_ctx* ctx, const char* name, double* value) {
   else if (!strcmp(name, "batch")) *value = ctx->batch;
   else if (!strcmp(name, "exact_r")) *value = ctx->exact_r;
   else if (!strcmp(name, "prof")) *value = ctx->prof;
-  else if (!strcmp(name, "pair")) *value = ctx->pair;
-  else if (!strcmp(name, "last_pair")) *value = ctx->last_pair;
-  else if (!strcmp(name, "kernel")) *value = ctx->kernel;
   else if (!strcmp(name, "members")) *value = ctx->members;
   else if (!strcmp(name, "stripe_log")) *value = ctx->stripe_log;
   else if (!strcmp(name, "last_k")) *value = ctx->last_k;
   else if (!strcmp(name, "n_cu")) *value = ctx->n_cu;
+  else if (!strcmp(name, "vmax")) *value = ctx->vmax;  // model's fastest speed (set_model; the exact-walk stop)
   else return fail(ctx, ALIFMM_E_ARG, "unknown option: %s", name);
   return ALIFMM_OK;
 }
 
 static af::DevModel dev_model(const alifmm_ctx* c);
+int alifmm_copy_fields(alifmm_ctx* ctx, int first_slot, int n, double* dst, int dst_kind, double* gbps);
 
 int alifmm_set_model(alifmm_ctx* ctx, int nnz, int nnx, const double* veln, const int64_t* velpn,
                      const double* vel_map, const int64_t* stif_den, const double* group_tab,
@@ -480,10 +484,8 @@ static int ensure_arena(alifmm_ctx* ctx, int nsrc, long cells, long capL, long c
   a.ecells = ecells;
   HIPCHK(dalloc(&a.S, (size_t)nsrc * cells));
   HIPCHK(dalloc(&a.own, (size_t)nsrc * cells));
-  HIPCHK(dalloc(&a.ax, (size_t)nsrc * 2 * capL));
-  HIPCHK(dalloc(&a.px, nsrc));
   HIPCHK(dalloc(&a.lists, (size_t)nsrc * (4 * capL + 6 * capC)));
-  HIPCHK(dalloc(&a.dlists, (size_t)nsrc * (2 * capL + 2 * capC)));
+  HIPCHK(dalloc(&a.dlists, (size_t)nsrc * (capL + 2 * capC)));
   if (K > 1) {
     HIPCHK(dalloc(&a.rimc, (size_t)nsrc * K * 2 * capR));
     HIPCHK(dalloc(&a.rimt, (size_t)nsrc * K * 2 * capR));
@@ -520,17 +522,19 @@ static int ensure_field(alifmm_ctx* ctx, int slot, int sg, int fz, int fx, long 
   return ALIFMM_OK;
 }
 
-// members per source of the K-member band kernel: the largest power of two <= kMaxK whose grid
-// (nsrc padded to 8, times K workgroups, one per CU) is co-resident, with >= 2 stripes per member
-// (option "members" forces a value, still capped by residency)
-static int choose_members(const alifmm_ctx* ctx, int n, long nstripes) {
+// members per source of the band kernel: the largest power of two <= kMaxK whose grid (nsrc padded
+// to 8, times K workgroups, one per CU) is co-resident, with >= 2 stripes per member (option
+// "members" forces a value, still capped by residency)
+static int choose_members(const alifmm_ctx* ctx, int n, int fx) {
   const int by_cu = std::max(1, ctx->n_cu / (8 * ((n + 7) / 8)));
   int K = 1;
   if (ctx->members > 0) {
     while (K * 2 <= ctx->members && K * 2 <= by_cu) K *= 2;
     return K;
   }
-  while (K * 2 <= af::kMaxK && K * 2 <= by_cu && K * 2 <= std::max(1L, nstripes / 2)) K *= 2;
+  // >= 2 stripes per member at the stripe width the member count selects
+  auto stripes = [&](int k) { return (long)(fx + (1 << (k >= 8 ? 4 : 6)) - 1) >> (k >= 8 ? 4 : 6); };
+  while (K * 2 <= af::kMaxK && K * 2 <= by_cu && 2L * K * 2 <= stripes(K * 2)) K *= 2;
   return K;
 }
 
@@ -548,11 +552,10 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
     capL = std::max(capL, std::min(capS, 262144L));
     capC = capL;
   }
-  // K-member band kernel: members per source and the stripe geometry (KGeom)
-  const bool kmode = ctx->kernel == 0;
-  const int wlog = ctx->stripe_log, W = 1 << wlog;
+  // band kernel: members per source and the stripe geometry (KGeom)
+  const int K = choose_members(ctx, n, fx);
+  const int wlog = ctx->stripe_log ? ctx->stripe_log : (K >= 8 ? 4 : 6), W = 1 << wlog;
   const long nstripes = (fx + W - 1) / W;
-  const int K = kmode ? choose_members(ctx, n, nstripes) : 1;
   const long capR = K > 1 ? 2L * fz * ((nstripes + K - 1) / K) + 64 : 0;
   const long ecells = K > 1 ? nstripes * 4L * fz : 0;  // per edge buffer (4 columns per stripe)
   // the arena is sized for this chunk (reused while later chunks fit in it)
@@ -576,12 +579,9 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
     b.T = ctx->fields[slot].d;
     b.S = a.S + (size_t)i * a.cells;
     b.own = a.own + (size_t)i * a.cells;
-    b.ax[0] = a.ax + (size_t)i * 2 * a.capL;
-    b.ax[1] = b.ax[0] + a.capL;
-    b.px = a.px + i;
     int* base = a.lists + (size_t)i * (4 * a.capL + 6 * a.capC);
-    b.L0 = base;
-    b.L1 = base + a.capL;
+    b.Lin = base;
+    b.FS = base + a.capL;
     b.A = base + 2 * a.capL;
     b.L = base + 3 * a.capL;
     b.C = base + 4 * a.capL;
@@ -590,16 +590,10 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
     b.Rx = b.C + 3 * a.capC;
     b.Bl = b.C + 4 * a.capC;
     b.Bp = b.C + 5 * a.capC;
-    double* dbase = a.dlists + (size_t)i * (2 * a.capL + 2 * a.capC);
-    b.Lt0 = dbase;
-    b.Lt1 = dbase + a.capL;
-    b.V = dbase + 2 * a.capL;
+    double* dbase = a.dlists + (size_t)i * (a.capL + 2 * a.capC);
+    b.Lt = dbase;
+    b.V = dbase + a.capL;
     b.Dv = b.V + a.capC;
-    // K-member kernel: the hand-over input stays in L0 (fmm_exact_kernel writes it there), the
-    // member lists go elsewhere (a member rewrites its slice while another may still read input)
-    b.Lin = b.L0;
-    b.Lt = b.Lt0;
-    b.FS = b.L1;
     b.kx = a.kx + i;
     if (K > 1) {
       b.rimc = a.rimc + (size_t)i * K * 2 * capR;
@@ -683,19 +677,9 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
   }
   HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
   if (fs != ctx->stream) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_fill, 0));
-  bool paired = false;
-  ctx->last_k = 0;
-  if (kmode) {
-    HIPCHK(hipMemsetAsync(a.kx, 0, sizeof(af::KX) * n, ctx->stream));
-    HIPCHK(af_launch_band_k(&P, ctx->stream));
-    ctx->last_k = K;
-  } else if (ctx->pair && 16 * ((n + 7) / 8) <= ctx->n_cu) {
-    HIPCHK(hipMemsetAsync(a.px, 0, sizeof(af::PairX) * n, ctx->stream));
-    paired = af_launch_band_pair(&P, ctx->stream) == hipSuccess;
-    if (!paired) (void)hipGetLastError();  // not co-resident / model too large for LDS: single kernel
-  }
-  ctx->last_pair = paired;
-  if (!kmode && !paired) HIPCHK(af_launch_band(&P, ctx->stream));
+  HIPCHK(hipMemsetAsync(a.kx, 0, sizeof(af::KX) * n, ctx->stream));
+  HIPCHK(af_launch_band_k(&P, ctx->stream));
+  ctx->last_k = K;
   HIPCHK(hipEventRecord(ctx->ev[2], ctx->stream));
   if (sg > 1)
     for (int i = 0; i < n; i++) HIPCHK(af_launch_scale(hs[i].T, cells, (double)sg, ctx->stream));
@@ -741,9 +725,8 @@ int alifmm_travel(alifmm_ctx* ctx, int subgrid, int nsrc, const double* scx, con
   HIPCHK(hipEventCreate(&t_begin));
   HIPCHK(hipEventRecord(t_begin, ctx->stream));
   // chunk: two workgroups per source need 2n CUs (pair mode), one per source otherwise
-  // K-member kernel: at least one workgroup per source (sources padded to 8) on the device
-  const int chunk = ctx->kernel == 0 ? std::max(1, std::min(ctx->batch, ctx->n_cu / 8 * 8))
-                    : (ctx->pair && ctx->n_cu >= 16) ? std::min(ctx->batch, ctx->n_cu / 16 * 8) : ctx->batch;
+  // at least one band workgroup per source (sources padded to 8), all co-resident
+  const int chunk = std::max(1, std::min(ctx->batch, ctx->n_cu / 8 * 8));
   for (int s0 = 0; s0 < nsrc; s0 += chunk) {
     int n = std::min(chunk, nsrc - s0);
     int rc;
@@ -756,10 +739,12 @@ int alifmm_travel(alifmm_ctx* ctx, int subgrid, int nsrc, const double* scx, con
       (void)hipEventDestroy(t_begin);
       return rc;
     }
-    if (out) {
-      for (int i = 0; i < n; i++)
-        HIPCHK(hipMemcpyAsync(out + (size_t)(s0 + i) * cells, ctx->fields[first_slot + s0 + i].d, (size_t)cells * 8,
-                              hipMemcpyDeviceToHost, ctx->stream));
+    if (out) {  // pageable host destination: through the pinned staging ring
+      rc = alifmm_copy_fields(ctx, first_slot + s0, n, out + (size_t)s0 * cells, 0, nullptr);
+      if (rc) {
+        (void)hipEventDestroy(t_begin);
+        return rc;
+      }
     }
   }
   hipEvent_t t_end;
@@ -782,6 +767,82 @@ int alifmm_get_field(alifmm_ctx* ctx, int slot, double* out) {
   HIPCHK(hipSetDevice(ctx->device));
   HIPCHK(hipMemcpyAsync(out, ctx->fields[slot].d, ctx->fields[slot].bytes, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
+  return ALIFMM_OK;
+}
+
+// host copy of one staged piece by a team of threads (one slice each)
+static void team_memcpy(char* dst, const char* src, size_t n, int nthreads) {
+  if (nthreads <= 1 || n < (4u << 20)) {
+    memcpy(dst, src, n);
+    return;
+  }
+  std::vector<std::thread> team;
+  const size_t slice = (n + nthreads - 1) / nthreads;
+  for (int t = 0; t < nthreads; t++) {
+    const size_t o = t * slice;
+    if (o >= n) break;
+    team.emplace_back([=] { memcpy(dst + o, src + o, std::min(slice, n - o)); });
+  }
+  for (auto& th : team) th.join();
+}
+
+int alifmm_copy_fields(alifmm_ctx* ctx, int first_slot, int n, double* dst, int dst_kind, double* gbps) {
+  if (!ctx || n < 0 || first_slot < 0 || (n > 0 && !dst) || dst_kind < 0 || dst_kind > 2)
+    return fail(ctx, ALIFMM_E_ARG, "copy_fields: bad args");
+  if (n == 0) return ALIFMM_OK;
+  if (first_slot + n > (int)ctx->fields.size()) return fail(ctx, ALIFMM_E_ARG, "copy_fields: slots out of range");
+  const size_t fb = ctx->fields[first_slot].bytes;
+  for (int i = 0; i < n; i++)
+    if (!ctx->fields[first_slot + i].d || ctx->fields[first_slot + i].bytes != fb)
+      return fail(ctx, ALIFMM_E_ARG, "copy_fields: slot %d empty or of another shape", first_slot + i);
+  HIPCHK(hipSetDevice(ctx->device));
+  const auto t0 = std::chrono::steady_clock::now();
+  char* out = (char*)dst;
+  if (dst_kind != 0) {  // one DMA per field (device -> device, or into host memory the DMA can write)
+    const hipMemcpyKind kind = dst_kind == 2 ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    for (int i = 0; i < n; i++)
+      HIPCHK(hipMemcpyAsync(out + (size_t)i * fb, ctx->fields[first_slot + i].d, fb, kind, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+  } else {
+    // pageable: pieces of kPinBytes through kPinBufs pinned buffers; the DMA of the next pieces
+    // runs while a thread team copies the current one out of its buffer
+    const int nb = alifmm_ctx::kPinBufs;
+    const size_t pb = alifmm_ctx::kPinBytes;
+    for (int b = 0; b < nb; b++) {
+      if (!ctx->pin[b]) HIPCHK(hipHostMalloc(&ctx->pin[b], pb, hipHostMallocDefault));
+      if (!ctx->pin_ev[b]) HIPCHK(hipEventCreateWithFlags(&ctx->pin_ev[b], hipEventDisableTiming));
+    }
+    const size_t per = (fb + pb - 1) / pb;  // pieces per field
+    const long np = (long)per * n;
+    auto piece = [&](long i, const char*& src, char*& d, size_t& len) {
+      const int f = (int)(i / per);
+      const size_t o = (size_t)(i % per) * pb;
+      src = (const char*)ctx->fields[first_slot + f].d + o;
+      d = out + (size_t)f * fb + o;
+      len = std::min(pb, fb - o);
+    };
+    auto issue = [&](long i) -> hipError_t {
+      const char* s;
+      char* d;
+      size_t len;
+      piece(i, s, d, len);
+      hipError_t e = hipMemcpyAsync(ctx->pin[i % nb], s, len, hipMemcpyDeviceToHost, ctx->stream);
+      return e == hipSuccess ? hipEventRecord(ctx->pin_ev[i % nb], ctx->stream) : e;
+    };
+    const int team = (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+    for (long i = 0; i < std::min<long>(nb, np); i++) HIPCHK(issue(i));
+    for (long i = 0; i < np; i++) {
+      HIPCHK(hipEventSynchronize(ctx->pin_ev[i % nb]));
+      const char* s;
+      char* d;
+      size_t len;
+      piece(i, s, d, len);
+      team_memcpy(d, (const char*)ctx->pin[i % nb], len, team);
+      if (i + nb < np) HIPCHK(issue(i + nb));
+    }
+  }
+  const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  if (gbps) *gbps = dt > 0 ? (double)fb * n / dt / 1e9 : 0.0;
   return ALIFMM_OK;
 }
 
@@ -1072,6 +1133,71 @@ int alifmm_local_ops(alifmm_ctx* ctx, int op, int n, int pz, int px, const doubl
   dfree(dd);
   dfree(di);
   if (e != hipSuccess) return fail(ctx, ALIFMM_E_HIP, "local_ops: %s", hipGetErrorString(e));
+  return ALIFMM_OK;
+}
+
+int alifmm_fouds18_band(alifmm_ctx* ctx, int n, int pz, int px, const double* ttn, const int32_t* nsts,
+                        const int32_t* iz, const int32_t* ix, const double* dnx, const double* dnz,
+                        const int32_t* nnz_arg, const int32_t* nnx_arg, const int32_t* mz, const int32_t* mx, int quant,
+                        double* out) {
+  if (!ctx || !ctx->have_model || n < 0 || pz < 1 || px < 1 || (quant != 0 && quant != 1))
+    return fail(ctx, ALIFMM_E_ARG, "fouds18_band: bad args or no model");
+  if (!ctx->d_mid || !ctx->d_mslo)
+    return fail(ctx, ALIFMM_E_ARG, "fouds18_band: the model has no per-material table (too many materials)");
+  for (int k = 0; k < n; k++)
+    if (mz[k] < 0 || mz[k] >= ctx->nz0 || mx[k] < 0 || mx[k] >= ctx->nx0)
+      return fail(ctx, ALIFMM_E_ARG, "fouds18_band: model cell %d (%d, %d) outside the grid", k, mz[k], mx[k]);
+  if (n == 0) return ALIFMM_OK;
+  HIPCHK(hipSetDevice(ctx->device));
+  const size_t pn = (size_t)pz * px;
+  // [ttn | dnx | dnz | out] doubles, [nsts | iz | ix | nnz | nnx | mz | mx] ints
+  double* dd = nullptr;
+  int* di = nullptr;
+  HIPCHK(dalloc(&dd, pn * n + 3 * (size_t)n));
+  if (hipMalloc((void**)&di, (pn * n + 6 * (size_t)n) * 4) != hipSuccess) {
+    dfree(dd);
+    return fail(ctx, ALIFMM_E_HIP, "fouds18_band: out of memory");
+  }
+  af::LocalOpsParams P;
+  memset(&P, 0, sizeof P);
+  P.op = 2;
+  P.n = n;
+  P.pz = pz;
+  P.px = px;
+  P.RM = dev_model(ctx);
+  P.quant = quant;
+  hipError_t e = hipSuccess;
+  double* p = dd;
+  auto putd = [&](const double* h, size_t cnt) {
+    double* q = p;
+    if (e == hipSuccess && cnt) e = hipMemcpy(q, h, cnt * 8, hipMemcpyHostToDevice);
+    p += cnt;
+    return (const double*)q;
+  };
+  int* q = di;
+  auto puti = [&](const int32_t* h, size_t cnt) {
+    int* r = q;
+    if (e == hipSuccess && cnt) e = hipMemcpy(r, h, cnt * 4, hipMemcpyHostToDevice);
+    q += cnt;
+    return (const int*)r;
+  };
+  P.ttn = putd(ttn, pn * n);
+  P.dnx = putd(dnx, n);
+  P.dnz = putd(dnz ? dnz : dnx, n);
+  P.out = p;
+  P.nsts = puti(nsts, pn * n);
+  P.iz = puti(iz, n);
+  P.ix = puti(ix, n);
+  P.nnz_arg = puti(nnz_arg, n);
+  P.nnx_arg = puti(nnx_arg, n);
+  P.mz = puti(mz, n);
+  P.mx = puti(mx, n);
+  if (e == hipSuccess) e = af_launch_local_ops(&P, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e == hipSuccess) e = hipMemcpy(out, P.out, 8 * (size_t)n, hipMemcpyDeviceToHost);
+  dfree(dd);
+  dfree(di);
+  if (e != hipSuccess) return fail(ctx, ALIFMM_E_HIP, "fouds18_band: %s", hipGetErrorString(e));
   return ALIFMM_OK;
 }
 

@@ -1,5 +1,5 @@
-// band_common.h — helpers shared by the band-synchronous FMM kernels (fmm_band.hip: one
-// workgroup per source; fmm_band_pair.hip: two workgroups per source).
+// band_common.h — helpers of the band-synchronous FMM kernel (fmm_band_k.hip: one source over
+// K = 1..16 workgroups) and the exact-order kernel (fmm_exact.hip).
 #pragma once
 #include "kernels.h"
 

@@ -12,7 +12,7 @@
 // (lane 0), the other lanes clear grids and fill the straight-ray footprint.
 //
 // Output for the band kernel: main-grid statuses known 0 / close 1 + list slot / far -1 and the
-// close cells in L0 (count in BandSrc::nl0).
+// close cells in Lin (count in BandSrc::nl0).
 #include "kernels.h"
 #include "local_ops.h"
 #include "fields.h"
@@ -324,7 +324,7 @@ __global__ __launch_bounds__(64) void fmm_exact_kernel(BandParams P) {
       for (int k = 1; k <= h.ntr && k <= P.capL; k++) {
         const int c = lds.cell[k];
         B->S[c] = k;  // close: 1 + close-list slot
-        B->L0[k - 1] = c;
+        B->Lin[k - 1] = c;
       }
       nl = h.ntr;
       if (nl > P.capL) err = 2;

@@ -5,17 +5,6 @@
 
 namespace af {
 
-// per-source exchange block of the two-workgroup band kernel (fmm_band_pair.hip); zeroed by the
-// host before each launch.  Every field is written by one member with sc1 stores.
-struct PairX {
-  int bar;          // pair barrier counter
-  int pad[31];
-  int nax[2][2];    // accepted cells next to the other member's columns, per step
-  // step-start exchange (X1) as flagged words: (step + 1) << 32 | payload, [member][tmin lo, tmin
-  // hi, live, err]; the payload arrives with the flag, so X1 is one store + polls (no counter)
-  unsigned long long x1[2][4];
-};
-
 // per-source exchange block of the K-member band kernel (fmm_band_k.hip); zeroed by the host
 // before each launch.  x1[member][step parity] = (step + 1) << 32 | payload words
 // [Tmin lo, Tmin hi, live close cells, err << 24 | rim-list length], each written by its member
@@ -25,48 +14,43 @@ struct KX {
   unsigned long long x1[kMaxK][2][4];
 };
 
+// one source of a band launch (fmm_exact_kernel / fmm_band_k_kernel); lists are split into K
+// per-member slices (capL / K, capC / K) that spill the LDS lists of the band kernel
 struct BandSrc {
-  double* T;      // field (main grid)
-  int* S;         // status: far -1, known 0, close 1 + close-list slot
-  int* own;       // claim owner ids (main grid)
-  int* L0;        // close list (ping): cells
-  int* L1;        // close list (pong)
-  double* Lt0;    // close list (ping): T of the entry
-  double* Lt1;
-  int* A;         // accepted cells of the step
-  int* C;         // claimed cells of the step
-  int* Cp;        // their close-list slot (-1: far)
-  double* V;      // claimed cells' new values
-  double* Ts[2];  // stage grids (mode 1)
-  int* ax[2];     // pair mode: each member's accepted cells next to the partner's columns
-  PairX* px;      // pair mode: exchange block
-  int* Ss[2];
-  long long steps[4];
-  long long nupd;  // relax evaluations (cell-sweeps) in the main run
-  int err;
-  int nl0;
-  // band profile (BandParams::prof): wall-clock ticks (100 MHz) per phase [tmin, accept, claim,
-  // evaluate, fallback, commit] and list-size sums [close, accepted, evaluated] and max close
-  long long ph[6];
-  long long lsum[3];
-  long long lmax;
-  long long sub[4];  // thread 0 inside phases: claim [neighbour+dedupe, loads, pushes], evaluate loads  // close cells handed to the band kernel in L0 (mode 1: fmm_exact_kernel)
-  // K-member kernel (fmm_band_k.hip): per-member slices (capL / K, capC / K) of the spill arrays
-  // of its LDS lists, the hand-over input list, rim lists and edge buffers
+  double* T;      // field (main grid); the band kernel's edge buffers follow it (E)
+  int* S;         // status: far -1, known 0, close 1 + close-set slot
+  int* own;       // claim stamps (steps with more claim items than the LDS hash holds)
   int* Lin;       // mode 1: close cells handed over by fmm_exact_kernel (nl0 of them)
   int* L;         // close set: cells
   double* Lt;     // close set: T
   int* FS;        // free close-set slots
-  int* D;         // edge commits of the step: cells
-  double* Dv;     //   and values
-  int* Rx;        // claim items from other members' rim cells
+  int* A;         // accepted cells of the step
+  int* C;         // claimed cells of the step
+  int* Cp;        // their close-set slot (-1: far)
+  double* V;      // claimed cells' new values
   int* Bl;        // claimed cells next to other members' columns
   int* Bp;        //   and their close-set slots
+  int* D;         // edge cells accepted in the step (copied forward next step)
+  double* Dv;     //   and their T
+  int* Rx;        // claim items from other members' rim cells
   int* rimc;      // [K][2][capR] published close rim cells (packed cell)
   double* rimt;   //   and their T
-  double* E;      // edge buffers [2][ecells] (column-major edge columns, KGeom::eidx)
+  double* E;      // edge buffers [2][ecells] (4 columns per stripe, column-major: KGeom::eidx)
   KX* kx;
+  double* Ts[2];  // stage grids (mode 1)
+  int* Ss[2];
   int bbox[4];    // mode 1: rows / columns [z0, z1, x0, x1] of the main grid fmm_exact_kernel wrote
+  long long steps[4];
+  long long nupd;  // relax evaluations (cell-sweeps) in the main run
+  int err;
+  int nl0;
+  // band profile (BandParams::prof): wall-clock ticks (100 MHz) of thread 0 of member 0 per phase
+  // [Tmin + X1, accept + rim read, claim, evaluate, fallback, commit], list-size sums [close,
+  // accepted, evaluated], max close, sub-phases [X1 wait, rim read, claim dedupe, drain before X1]
+  long long ph[6];
+  long long lsum[3];
+  long long lmax;
+  long long sub[4];
 };
 
 struct BandParams {
@@ -114,7 +98,7 @@ struct RayParams {
 };
 
 struct LocalOpsParams {
-  int op;  // 0 update(), 1 fouds18_A()
+  int op;  // 0 update(), 1 fouds18_A(), 2 fouds18_A() as the band kernel runs it (resident model)
   long n;
   int pz, px;
   const double* ttn;  // [n][pz][px]
@@ -132,6 +116,12 @@ struct LocalOpsParams {
   const double* tab;    // (361, ncol): phase table for update(), group table for fouds18_A()
   int ncol;
   double* out;
+  // op 2: material of resident-model cell (mz, mx) under MatView::quant, through the per-material
+  // record (band_mat<true>) and the precomputed slownesses DevModel::mslo (fouds18<true>)
+  DevModel RM;
+  const int* mz;
+  const int* mx;
+  int quant;
 };
 
 }  // namespace af
@@ -139,8 +129,6 @@ struct LocalOpsParams {
 extern "C" {
 hipError_t af_launch_init(const af::DevModel* M, af::InitJob* jobs, int njobs, af::HandoverOut* out, hipStream_t stream);
 hipError_t af_launch_exact(const af::BandParams* P, hipStream_t stream);
-hipError_t af_launch_band(const af::BandParams* P, hipStream_t stream);
-hipError_t af_launch_band_pair(const af::BandParams* P, hipStream_t stream);
 hipError_t af_launch_band_k(const af::BandParams* P, hipStream_t stream);
 hipError_t af_launch_scale(double* T, long n, double sg, hipStream_t stream);
 hipError_t af_launch_rays(const af::RayParams* P, hipStream_t stream);

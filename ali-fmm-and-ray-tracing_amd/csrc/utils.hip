@@ -4,6 +4,7 @@
 //   time_between_points() on the resident model (:2835-2989)
 #include "kernels.h"
 #include "local_ops.h"
+#include "band_common.h"
 
 namespace af {
 
@@ -20,6 +21,16 @@ __global__ void local_ops_kernel(LocalOpsParams P) {
   if (k >= P.n) return;
   const long pn = (long)P.pz * P.px;
   PatchField F{P.ttn + k * pn, P.nsts + k * pn, P.pz, P.px};
+  if (P.op == 2) {  // the band kernel's fallback: fouds18<true> on the material record + mslo
+    MatView v;
+    v.s1z = v.s1x = v.s2 = 1;
+    v.side1z = v.side1x = v.side2 = v.lo1z = v.lo1x = v.lo2z = v.lo2x = 0;
+    v.quant = P.quant;
+    const CellMat cm = band_mat<true>(P.RM, P.RM.mtab, P.RM.stab, v, P.mz[k], P.mx[k]);
+    P.out[k] = fouds18<true>(F, P.RM, cm, P.iz[k], P.ix[k], P.dnx[k], P.dnz[k], P.nnx_arg[k], P.nnz_arg[k],
+                             mat_slo(P.RM, v, P.mz[k], P.mx[k]));
+    return;
+  }
   DevModel M;
   M.mslo = nullptr;
   M.nz0 = 1;
@@ -84,5 +95,19 @@ extern "C" hipError_t af_launch_tbp(const af::DevModel* M, int n, const double* 
 extern "C" hipError_t af_launch_mat_slowness(const af::DevModel* M, double* out, hipStream_t stream) {
   if (M->nmat <= 0) return hipSuccess;
   hipLaunchKernelGGL(af::mat_slowness_kernel, dim3((2 * M->nmat + 63) / 64), dim3(64), 0, stream, *M, out);
+  return hipGetLastError();
+}
+
+namespace af {
+// final scaling of travel_finer_grid (:2832 ttn / subgrid_size)
+__global__ void scale_kernel(double* T, long n, double inv) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long stride = (long)gridDim.x * blockDim.x;
+  for (; i < n; i += stride) T[i] = T[i] / inv;
+}
+}  // namespace af
+
+extern "C" hipError_t af_launch_scale(double* T, long n, double sg, hipStream_t stream) {
+  hipLaunchKernelGGL(af::scale_kernel, dim3(2048), dim3(256), 0, stream, T, n, sg);
   return hipGetLastError();
 }

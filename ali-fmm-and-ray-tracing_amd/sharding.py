@@ -27,6 +27,47 @@ def bench_sources(rank, n_sources, n, dnx):
     return scx, scz
 
 
+def gather_fields(ctx, n_local, fnz, fnx, rank, world, device, first_slot=0):
+    """RCCL gather of every rank's resident fields to rank 0 (the result-return leg of bench.py).
+
+    Each rank copies its n_local fields device-to-device into one contiguous buffer
+    (alifmm_copy_fields, kind 2) and joins one dist.gather over an RCCL ("nccl") group onto rank
+    0's device; ranks with fewer fields pad to the largest count.  torch is imported before the
+    library is loaded (bench.py), so both share one HIP runtime and device pointers are valid
+    in both.  Returns the timings (max over ranks) and rates of the two parts."""
+    import time
+
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(device)
+    g = dist.new_group(backend="nccl")
+    counts = torch.tensor([n_local], dtype=torch.int64)
+    cmax = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(cmax, counts)
+    nmax = int(max(int(c) for c in cmax))
+    buf = torch.empty((nmax, fnz, fnx), dtype=torch.float64, device="cuda")
+    recv = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
+    dist.barrier(group=g)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    d2d_gbps = ctx.copy_fields_to_device(first_slot, n_local, buf.data_ptr()) if n_local else 0.0
+    t1 = time.perf_counter()
+    dist.gather(buf, recv, dst=0, group=g)
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    copy_s = max_over_ranks(t1 - t0, dist)
+    gather_s = max_over_ranks(t2 - t1, dist)
+    total = int(sum(int(c) for c in cmax)) * fnz * fnx * 8
+    remote = total - n_local * fnz * fnx * 8 if rank == 0 else 0
+    remote = int(max_over_ranks(remote, dist))
+    del recv, buf
+    dist.destroy_process_group(g)
+    return {"pack_d2d_ms": copy_s * 1e3, "pack_d2d_GBps": d2d_gbps, "rccl_gather_ms": gather_s * 1e3,
+            "rccl_gather_bytes_into_rank0": remote,
+            "rccl_gather_GBps_into_rank0": remote / gather_s / 1e9 if gather_s > 0 else None}
+
+
 def max_over_ranks(value, dist=None):
     """Max of a float over all ranks of the default process group (identity without one)."""
     if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:

@@ -1,16 +1,25 @@
-"""Benchmark: grid-cell updates/s + sources/s on the 4096^2 anisotropic weld-like grid (BASELINE.json).
+"""Benchmark: grid-cell updates/s + sources/s on the 4096^2 anisotropic weld-like grid (BASELINE.json,
+config 4: "4096x4096 weld-like grid, 128 Tx sources sharded across 1/2/4/8 MI355X").
 
-One process per GPU (python -m torch.distributed.run ... bench.py --gpus N).  A "step" is one
-pass of the hot path over one batch: first-arrival travel-time fields for the rank's sources
-(BASELINE C4: 128 sources on the top surface per GPU, subgrid 1), inputs resident in HBM, fields
-left resident in HBM (the ray tracer reads them there).  Sources are independent: each rank
-computes its own shard (weak scaling), no data-path collective; torch.distributed (gloo) only
-provides the barrier and the max-over-ranks of the step time.
+One process per GPU (python -m torch.distributed.run ... bench.py --gpus N).  The 128 C4 sources
+(z = 0, x = 16 + 32 k) are dealt block-cyclically over the N ranks, as the
+reference's update_parallel hands whole sources to its workers (Anis_TTF_rays.py:3938-4051), so
+the total work is fixed and the curve over N is STRONG scaling; --weak gives every rank its own
+128 sources instead.  A "step" is one pass of the hot path over the rank's sources: their
+first-arrival travel-time fields (inputs resident in HBM, fields left resident in HBM, where the
+ray tracer reads them).  Sources are independent: no data-path collective; torch.distributed
+(gloo) only provides the barrier and the max over ranks of the step time.
 
-Reported: value = all ranks' (cells x sources) / max-over-ranks wall time of the timed steps;
-roofline of the dominant kernel (the band kernel: fmm_band_pair_kernel, two workgroups per source,
-when the batch fits the device, else fmm_band_kernel) from in-library HIP events on its stream; cpu_baseline = the
-CPU restatement of the reference (oracle/, one source per thread) on a bounded sample, rank 0, N=1.
+value = 128 x 4096^2 cell-updates x steps / max-over-ranks wall time of the timed steps.
+roofline: the band kernel (fmm_band_k_kernel), SURVEY §8(d)'s 18.1 algorithmic bytes per
+cell-sweep (one evaluation of the local operator, counted by the kernel) over the kernel's
+in-library HIP-event time on its stream; traffic = HBM bytes per launch from rocprofv3 PMC
+passes of the same library build (profiles/*_traffic.json), with traffic / algorithmic.
+result_return: after the timed steps, the fields' way back (not in value): D2H into pageable
+host memory through the library's pinned staging ring; for N > 1 also an RCCL gather of every
+rank's fields to rank 0 over xGMI.
+cpu_baseline: the CPU restatement of the reference (oracle/, one source per thread) on a bounded
+sample, rank 0, N = 1.
 """
 import argparse
 import json
@@ -25,9 +34,12 @@ sys.path.insert(0, os.path.join(REPO, "ali-fmm-and-ray-tracing_amd"))
 sys.path.insert(0, os.path.join(REPO, "tests"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
-# algorithmic bytes per cell-sweep (one local-operator evaluation on the band front), DESIGN.md §5:
-# T f64 read+write 16, status int32 read+write 8, material (veln f64, vel_map f64, velpn i32, stiffness idx i32) 24
-BYTES_PER_SWEEP = 48
+# algorithmic bytes per cell-sweep (T f32 read + write 8, orientation 4,
+# vel_map 4, material id 1, halo 1.06)
+BYTES_PER_SWEEP = 18.1
+# per-core speed of the C restatement over the numba reference on C3 (2048^2, one source), both
+# measured in the build container: 8.69 s (numba) / 3.73 s (oracle/alifmm_oracle.c)
+PORT_VS_REFERENCE_PER_CORE = 8.69 / 3.73
 
 
 def parse():
@@ -36,13 +48,61 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--n", type=int, default=4096, help="grid side (4096 = BASELINE C4)")
-    ap.add_argument("--sources", type=int, default=128, help="sources per GPU (BASELINE C4: 128)")
-    ap.add_argument("--cpu-sample", type=int, default=16, help="sources in the CPU-baseline sample (0: skip)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--cdelta", type=float, default=None)
-    ap.add_argument("--exact-r", type=float, default=None)
+    ap.add_argument("--sources", type=int, default=128, help="total sources (strong) or per GPU (--weak)")
+    ap.add_argument("--weak", action="store_true", help="every rank runs --sources sources of its own")
+    ap.add_argument("--cpu-sample", type=int, default=0, help="sources in the CPU sample (0: one per thread)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: the CPUs this process may run on")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-return", action="store_true", help="skip the result-return measurement")
+    ap.add_argument("--members", type=int, default=None, help="band-kernel workgroups per source (0: auto)")
+    ap.add_argument("--cdelta", type=float, default=None)
     return ap.parse_args()
+
+
+def rank_sources(args, rank, world, dnx):
+    import sharding
+
+    if args.weak:
+        scx, scz = sharding.bench_sources(rank, args.sources, args.n, dnx)
+        return scx, scz, np.arange(args.sources)
+    k = np.array(sharding.deal(range(args.sources), world)[rank], dtype=np.int64)
+    kk = k % (args.n // 32)
+    return dnx * (16 + 32 * kk).astype(np.float64), np.zeros(len(k)), k
+
+
+def cpu_baseline(args, scx, scz, model, vt, dnx, cells):
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O
+
+    veln, velpn, vel_map, stif = model
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count()
+    th = args.cpu_threads or avail
+    ns = args.cpu_sample or th
+    xs, zs = np.resize(scx, ns), np.resize(scz, ns)
+    t1 = time.perf_counter()
+    O.travel_batch(xs[:1], zs[:1], veln, velpn, vel_map, stif, vt, vt, dnx=dnx, n_threads=1)
+    one = time.perf_counter() - t1
+    t1 = time.perf_counter()
+    O.travel_batch(xs, zs, veln, velpn, vel_map, stif, vt, vt, dnx=dnx, n_threads=th)
+    tc = time.perf_counter() - t1
+    model_name = ""
+    try:
+        model_name = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
+    per_core = cells / one  # cell-updates/s of one core
+    return {"value": cells * ns / tc, "unit": "grid-cell updates/s", "cores": th, "kind": "port",
+            "sample": "%d C4 sources (4096^2, z=0) on %d threads (the CPUs this process may use: %d of %d "
+                      "visible), one source per thread, oracle/alifmm_oracle.c (bit-exact restatement of the "
+                      "reference's heap FMM); %.1f s wall; plus 1 source on 1 core: %.2f s"
+                      % (ns, th, avail, os.cpu_count(), tc, one),
+            "host_cpu": model_name, "host_cpus_visible": os.cpu_count(), "host_cpus_usable": avail,
+            "seconds_per_source_1core": one,
+            "value_all_visible_cores_extrapolated": per_core * os.cpu_count(),
+            "port_vs_numba_reference_per_core": PORT_VS_REFERENCE_PER_CORE}
 
 
 def main():
@@ -52,6 +112,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
+        import torch  # noqa: F401  (before the library: one HIP runtime for both, see sharding.gather_fields)
         import torch.distributed as dist
 
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -61,7 +122,7 @@ def main():
     import workloads as W
 
     n = args.n
-    veln, velpn, vel_map, stif = W.weldlike_model(n)
+    model = W.weldlike_model(n)
     dnx = W.weldlike_dnx()
     vt = W.default_table()
     # one GPU per rank (LOCAL_RANK); ALIFMM_BENCH_DEVICE pins every rank to one device, only to
@@ -70,10 +131,11 @@ def main():
     ctx = _alifmm.Context(dev)
     if args.cdelta is not None:
         ctx.set_option("cdelta", args.cdelta)
-    if args.exact_r is not None:
-        ctx.set_option("exact_r", args.exact_r)
-    ctx.set_model(veln, velpn, vel_map, stif, vt, vt, dnx)
-    scx, scz = sharding.bench_sources(rank, args.sources, n, dnx)
+    if args.members is not None:
+        ctx.set_option("members", args.members)
+    ctx.set_model(*model, vt, vt, dnx)
+    scx, scz, _ = rank_sources(args, rank, world, dnx)
+    ns = len(scx)
 
     def barrier():
         if dist is not None:
@@ -85,27 +147,27 @@ def main():
     t0 = time.perf_counter()
     band_ms = init_ms = 0.0
     for _ in range(args.steps):
-        ctx.travel(scx, scz, subgrid=1, first_slot=0, copy_out=False)
+        ctx.travel(scx, scz, subgrid=1, first_slot=0, copy_out=False)  # synchronous: returns when done
         ti, tb, _ = ctx.last_timing()
         init_ms += ti
         band_ms += tb
     barrier()
-    dt = time.perf_counter() - t0
-    sweeps = sum(ctx.source_stats(i)[1] for i in range(args.sources))
-    band_kernel = "fmm_band_pair_kernel" if int(ctx.get_option("last_pair")) else "fmm_band_kernel"
-    steps_main = [int(ctx.source_stats(i)[0][3]) for i in range(args.sources)]
-    dt = sharding.max_over_ranks(dt, dist)
+    dt = sharding.max_over_ranks(time.perf_counter() - t0, dist)
+    sweeps = sum(ctx.source_stats(i)[1] for i in range(ns))
+    steps_main = [int(ctx.source_stats(i)[0][3]) for i in range(ns)]
+    members = int(ctx.get_option("last_k"))
     cells = float(n) * n
-    total_src = args.sources * world
+    total_src = args.sources * (world if args.weak else 1)
     value = cells * total_src * args.steps / dt
     band_avg_s = band_ms / args.steps / 1e3
     achieved = BYTES_PER_SWEEP * sweeps / band_avg_s / 1e9 if band_avg_s > 0 else None
 
-    config = {"workload": "C4: %dx%d weld-like, %d top-surface Tx sources per GPU, subgrid 1" % (n, n, args.sources),
-              "sources_per_gpu": args.sources, "total_sources": args.sources * world, "grid": [n, n], "subgrid": 1,
-              "cdelta": args.cdelta, "exact_r": args.exact_r}
-    # HBM-side bytes per launch: PMC passes of tools/profile.sh on this library AND this workload
-    traffic = traffic_bytes = None
+    config = {"workload": "C4: %dx%d weld-like grid, %d top-surface Tx sources %s, subgrid 1"
+                          % (n, n, total_src, "per GPU (weak)" if args.weak else "dealt over the GPUs (strong)"),
+              "total_sources": total_src, "sources_per_gpu": ns, "grid": [n, n], "subgrid": 1,
+              "band_workgroups_per_source": members, "cdelta": args.cdelta}
+    # HBM-side bytes per launch: rocprofv3 PMC passes (tools/profile.sh) on this library and workload
+    traffic_bytes = None
     try:
         import glob
         import hashlib
@@ -114,31 +176,26 @@ def main():
         for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json"))):
             t = json.load(open(f))
             if (t.get("libalifmm_sha256") == lib_sha and t.get("traffic_bytes_per_launch")
-                    and t.get("bench_config") == {k: v for k, v in config.items() if k != "total_sources"}):
+                    and t.get("sources_per_gpu") == ns and t.get("grid") == [n, n]):
                 traffic_bytes = t["traffic_bytes_per_launch"]
-                traffic = traffic_bytes / band_avg_s / 1e9  # GB/s over the same launch time as achieved
     except OSError:
         pass
 
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu and args.cpu_sample > 0:
-        sys.path.insert(0, os.path.join(REPO, "oracle"))
-        import oracle as O
-
-        ns = args.cpu_sample
-        th = min(args.cpu_threads, ns)
+    # result-return leg (not in value): D2H of this rank's fields; RCCL gather to rank 0 (N > 1)
+    ret = None
+    if not args.no_return:
+        ret = {}
+        barrier()
         t1 = time.perf_counter()
-        O.travel_batch(scx[:ns], scz[:ns], veln, velpn, vel_map, stif, vt, vt, dnx=dnx, n_threads=th)
-        tc = time.perf_counter() - t1
-        model = ""
-        try:
-            model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
-        except (OSError, StopIteration):
-            pass
-        cpu = {"value": cells * ns / tc, "unit": "grid-cell updates/s", "cores": th, "kind": "port",
-               "host_cpu": model, "host_cpus_visible": os.cpu_count(), "seconds_per_source_per_core": tc * th / ns,
-               "sample": "%d C4 sources (4096^2, z=0) on %d threads, one source per thread, oracle/alifmm_oracle.c "
-                         "(bit-exact restatement of the reference's heap FMM); %.1f s wall" % (ns, th, tc)}
+        _, gbps = ctx.copy_fields(0, ns, 1)
+        d2h = sharding.max_over_ranks(time.perf_counter() - t1, dist)
+        ret.update({"d2h_ms": d2h * 1e3, "d2h_GBps_per_gpu": gbps, "bytes_per_gpu": int(cells * 8 * ns),
+                    "d2h": "pageable host memory through the library's pinned staging ring, every GPU at once"})
+        if world > 1:
+            ret.update(sharding.gather_fields(ctx, ns, n, n, rank, world, dev))
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(args, scx, scz, model, vt, dnx, cells)
     if rank == 0:
         out = {
             "metric": "grid-cell updates/sec + sources/sec on 4096^2 anisotropic grid",
@@ -149,26 +206,30 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": dt / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if args.weak else "strong",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic: weld-like model built from the reference's weld_*.npy (edge-padded, 8x nearest), "
                     "stiffness row of the notebook",
             "config": config,
             "sources_per_s": total_src * args.steps / dt,
-            "kernel_ms_per_step": {"fmm_init_kernel": init_ms / args.steps, band_kernel: band_ms / args.steps},
+            "kernel_ms_per_step": {"fmm_init_kernel": init_ms / args.steps, "fmm_band_k_kernel": band_ms / args.steps},
             "band_steps_main_mean": float(np.mean(steps_main)),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
-                         "kernel": band_kernel, "bytes_per_cell_sweep": BYTES_PER_SWEEP,
+                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+                         "traffic": traffic_bytes,
+                         "kernel": "fmm_band_k_kernel", "bytes_per_cell_sweep": BYTES_PER_SWEEP,
                          "cell_sweeps_per_launch": int(sweeps),
                          "algorithmic_bytes_per_launch": BYTES_PER_SWEEP * int(sweeps),
-                         "traffic_bytes_per_launch": traffic_bytes},
+                         "traffic_over_algorithmic": (traffic_bytes / (BYTES_PER_SWEEP * sweeps))
+                         if traffic_bytes else None},
+            "result_return": ret,
             "cpu_baseline": cpu,
         }
         if cpu:
             out["speedup_vs_cpu_baseline"] = value / cpu["value"]
-        print(json.dumps(out))
+            out["speedup_vs_cpu_all_visible_cores_extrapolated"] = value / cpu["value_all_visible_cores_extrapolated"]
+        print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
     ctx.close()

@@ -46,14 +46,17 @@ int alifmm_set_model(alifmm_ctx* ctx, int nnz, int nnx, const double* veln, cons
                      const double* vel_map, const int64_t* stif_den, const double* group_tab,
                      const double* phase_tab, int ncol, double dnx, double dnz, double gox, double goz);
 
-/* Tuning: "pair" (1, default: two workgroups per source when the chunk fits the device, results
- * identical to the one-workgroup kernel), "prof" (1: record the band profile, alifmm_band_profile;
- * either kernel), "cdelta" (band width in units of dnx/vmax, default 0.5), "r0" (near-source band
- * schedule radius in cells, default 40), "exact_r" (radius in cells of the exact heap-ordered
- * main-loop prefix, 0..48, default 20), "batch" (sources per launch, default 256). */
+/* Tuning: "members" (workgroups per source of the band kernel: 0 = as many as the device holds
+ * for the batch, else 1, 2, 4, 8 or 16; results are bit-identical for every value), "stripe_log"
+ * (column-stripe width log2 of the band kernel's ownership, 0 = automatic), "prof" (1: record the
+ * band profile, alifmm_band_profile), "cdelta" (band width in units of dnx/vmax, default 0.5),
+ * "r0" (near-source band schedule radius in cells, default 40), "exact_r" (radius in cells of the
+ * exact heap-ordered main-loop prefix, 0..48, default 20), "batch" (sources per launch, default
+ * 256). */
 int alifmm_set_option(alifmm_ctx* ctx, const char* name, double value);
-/* Read an option, or "last_pair" (1 if the last alifmm_travel ran the two-workgroup kernel) and
- * "n_cu" (compute units of the device). */
+/* Read an option, or "last_k" (workgroups per source of the last band launch), "n_cu"
+ * (compute units of the device) and "vmax" (the model's fastest speed [m/s]: the exact prefix
+ * covers T <= exact_r * dnx / vmax). */
 int alifmm_get_option(alifmm_ctx* ctx, const char* name, double* value);
 
 /* Shape of a travel-time field for subgrid size sg: (sg*(nnz-1)+1, sg*(nnx-1)+1). */
@@ -70,6 +73,14 @@ int alifmm_travel(alifmm_ctx* ctx, int subgrid, int nsrc, const double* scx, con
 /* Copy a resident field to the host; release all resident fields. */
 int alifmm_get_field(alifmm_ctx* ctx, int slot, double* out);
 int alifmm_release_fields(alifmm_ctx* ctx);
+
+/* Copy the resident fields of slots first_slot .. first_slot+n-1 (one shape) into dst, slot after
+ * slot (the (nsrc, fnz, fnx) result stack of ALI_FMM.update() :3870-3936, which the reference's
+ * workers return over queue2 :3610, :3659).  dst_kind 0: pageable host memory, copied through a
+ * ring of pinned staging buffers (the DMA of one piece overlaps the host copy of the previous);
+ * 1: host memory the DMA engine can write directly (pinned or registered); 2: device memory of
+ * this context's GPU (e.g. a communication buffer).  *gbps (nullable) = bytes / wall time. */
+int alifmm_copy_fields(alifmm_ctx* ctx, int first_slot, int n, double* dst, int dst_kind, double* gbps);
 
 /* Trace npairs rays (replaces find_ray() :3104-3465 incl. ray_time() :2992-3022).
  *   field_slot[k]        resident field of the RECEIVER of ray k (its subgrid is used)
@@ -123,6 +134,15 @@ int alifmm_local_ops(alifmm_ctx* ctx, int op, int n, int pz, int px, const doubl
                      const int32_t* nnz_arg, const int32_t* nnx_arg, const double* cell_veln,
                      const int64_t* cell_velpn, const double* cell_vm, const int64_t* cell_stif,
                      const double* tab, int ncol, double* out);
+
+/* fouds18_A() (:240-901) exactly as the band kernel evaluates it: the material of resident-model
+ * cell (mz, mx) through the model's per-material record and its precomputed stencil slownesses
+ * (quant 1: the subgrid > 1 view, orientation truncated to int32 and vel_map to float32, as
+ * finer_grid_n does at :26-56).  Same patches and arguments as alifmm_local_ops op 1. */
+int alifmm_fouds18_band(alifmm_ctx* ctx, int n, int pz, int px, const double* ttn, const int32_t* nsts,
+                        const int32_t* iz, const int32_t* ix, const double* dnx, const double* dnz,
+                        const int32_t* nnz_arg, const int32_t* nnx_arg, const int32_t* mz, const int32_t* mx,
+                        int quant, double* out);
 
 #ifdef __cplusplus
 }

@@ -27,3 +27,17 @@ def golden():
         return cache[name]
 
     return load
+
+
+@pytest.fixture(scope="session")
+def envelope():
+    """Measured parity errors of this run (name -> value), written to gpurun_out/parity_envelope.json
+    at the end of the session: the evidence the thresholds in test_gpu_parity.py are set against."""
+    import json
+
+    rec = {}
+    yield rec
+    if rec:
+        os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+        with open(os.path.join(REPO, "gpurun_out", "parity_envelope.json"), "w") as f:
+            json.dump(rec, f, indent=1, sort_keys=True)

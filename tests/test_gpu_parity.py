@@ -1,12 +1,17 @@
 """GPU parity: the MI355X path (libalifmm.so through the drop-in module) against the oracle and the
 reference's own golden vectors.  Run on the GPU box: pytest -m gpu.
 
-Tolerances (justified by SURVEY.md §7 hard part 2 and Appendix C):
+Tolerances (justified by SURVEY.md §7 hard part 2 and Appendix C; every measured
+error is also written to gpurun_out/parity_envelope.json, profiles/r2_parity_envelope.json keeps
+the run the thresholds are set against, about 2x above it):
   * local operators, time_between_points, rays on a given field: bit-exact except where ocml's
     f64 atan/tan/sin/cos differ from glibc by an ulp -> rel <= 1e-12 per value, >= 99 % exact;
+  * the exact prefix (every cell with T <= exact_r * dnx / vmax, heap order of the reference,
+    :94-237 and :1512-1993): rel <= 1e-12;
   * travel-time fields (band-synchronous reformulation of the heap FMM), cells > 5 nodes from
-    the source: rel L-inf <= 1e-2, rel mean <= 1e-3;
-  * ray travel times end-to-end (GPU fields + GPU rays): rel <= 5e-3.
+    the source: rel L-inf <= 3e-3, rel mean <= 5e-5 on the C3, C4 and weld grids (FIELD_*), and
+    SMALL_* on the 41..201-node cases, whose errors are larger relative to their small T;
+  * ray travel times end-to-end (GPU fields + GPU rays): rel <= 5e-4 (RAY_END2END).
 """
 import numpy as np
 import pytest
@@ -16,7 +21,11 @@ import workloads as W
 
 pytestmark = pytest.mark.gpu
 
-FIELD_MAX, FIELD_MEAN, RAY_END2END = 1e-2, 1e-3, 5e-3
+FIELD_MAX, FIELD_MEAN = 3e-3, 5e-5
+SMALL_MAX, SMALL_MEAN = 1e-2, 1e-3
+RAY_END2END = 5e-4
+KAT_END2END = 5e-3  # K1-K3: the notebook prints 9 significant digits of its numba run
+EXACT = 1e-12
 
 
 @pytest.fixture(scope="module")
@@ -39,7 +48,30 @@ def _field_err(T, Tref, src, excl=5):
     zz, xx = np.mgrid[0:T.shape[0], 0:T.shape[1]]
     m = np.hypot(zz - src[1], xx - src[0]) > excl
     r = np.abs(T[m] - Tref[m]) / Tref[m]
-    return r.max(), r.mean()
+    return float(r.max()), float(r.mean())
+
+
+def _check_field(envelope, name, T, Tref, src, excl=5, tol=(FIELD_MAX, FIELD_MEAN)):
+    mx, mean = _field_err(T, Tref, src, excl)
+    envelope[name] = {"rel_max": mx, "rel_mean": mean}
+    assert mx <= tol[0] and mean <= tol[1], (name, mx, mean)
+
+
+def _exact_pin(envelope, name, T, Tref, tstop, min_cells):
+    """Every cell the exact heap walk finalises (T <= tstop, the walk's stop) equals the reference's
+    value to 1e-12 relative (device transcendental ulps), the source cell exactly."""
+    m = Tref <= 0.999 * tstop
+    n = int(m.sum())
+    rel = np.abs(T[m] - Tref[m]) / np.maximum(Tref[m], 1e-300)
+    envelope[name] = {"cells": n, "rel_max": float(rel.max()) if n else None, "exact_frac": float(np.mean(T[m] == Tref[m]))}
+    assert n >= min_cells, (name, n)
+    assert rel.max() <= EXACT, (name, float(rel.max()))
+
+
+def _ray_err(envelope, name, t, ref, tol=RAY_END2END):
+    r = abs(t - ref) / ref
+    envelope.setdefault(name, []).append(float(r))
+    assert r <= tol, (name, t, ref)
 
 
 def test_library_is_the_hip_build():
@@ -84,9 +116,8 @@ def test_time_between_points_vs_reference_vectors(golden, ctx):
         assert np.mean(out == r[:, 5]) >= 0.9 and rel.max() <= 1e-12, (sg, np.mean(out == r[:, 5]), rel.max())
 
 
-def test_fmm_small_fields(golden, A):
+def test_fmm_small_fields(golden, A, envelope):
     g = golden("fmm_small")
-    worst = []
     for k in range(int(g["ncases"])):
         p = "c%d_" % k
         dnx, x, z, sg = g[p + "meta"]
@@ -102,47 +133,51 @@ def test_fmm_small_fields(golden, A):
             src = (sg * x, sg * z)
         ref = g[p + "out"]
         assert T.shape == ref.shape
-        mx, mean = _field_err(T, ref, src, excl=5 * int(sg))
-        worst.append((k, mx, mean))
-    bad = [w for w in worst if w[1] > FIELD_MAX or w[2] > FIELD_MEAN]
-    assert not bad, bad
+        _check_field(envelope, "fmm_small_%d_sg%d" % (k, int(sg)), T, ref, src, excl=5 * int(sg),
+                     tol=(SMALL_MAX, SMALL_MEAN))
 
 
-def test_c1_fields_and_analytic(golden, A):
+def test_c1_fields_analytic_and_exact_prefix(golden, A, envelope):
     g = golden("c1_fields")
     veln, velpn, vm, _ = W.c1_model()
     M = A.ALI_FMM(veln, velpn, vm, 1e-3 * g["src"][:, 0].astype(float), 1e-3 * g["src"][:, 1].astype(float))
     T = M.update(veln, velpn, vm)
+    c = M._ctx(0)
+    tstop = c.get_option("exact_r") * 1e-3 / c.get_option("vmax")
     zz, xx = np.mgrid[0:201, 0:201]
     for k, (x, z) in enumerate(g["src"]):
-        mx, mean = _field_err(T[k], g["out"][k], (x, z))
-        assert mx <= FIELD_MAX and mean <= FIELD_MEAN, (k, mx, mean)
+        _check_field(envelope, "c1_%d" % k, T[k], g["out"][k], (x, z), tol=(SMALL_MAX, SMALL_MEAN))
+        _exact_pin(envelope, "exact_c1_%d" % k, T[k], g["out"][k], tstop, 200)
         r = np.hypot(zz - z, xx - x)
         m = r > 20
         rel = np.abs(T[k][m] - 1e-3 * r[m] / 5790.0) / (1e-3 * r[m] / 5790.0)
         assert rel.max() < 2.0e-2 and rel.mean() < 9e-3
 
 
-def test_weld_sg1_field_and_rays(golden, A, ctx):
+def test_weld_sg1_field_rays_and_exact_prefix(golden, A, ctx, envelope):
     g = golden("weld_sg1")
     veln, velpn, vm, sd = W.weld_model()
     vt = W.default_table()
     scx, scz = W.weld_transducers()
     T = A.travel(scx[46], scz[46], None, None, 0, np.zeros(veln.shape), veln, velpn, vm, sd, vt, vt, 0, 0, 2e-4, 2e-4,
                  500, 424)
-    mx, mean = _field_err(T, g["field"], (250, 423))
-    assert mx <= FIELD_MAX and mean <= FIELD_MEAN, (mx, mean)
+    _check_field(envelope, "weld_sg1", T, g["field"], (250, 423))
+    ctx.set_model(veln, velpn, vm, sd, vt, vt, 2e-4)
+    T2 = ctx.travel([scx[46]], [scz[46]])[0]
+    assert np.array_equal(T2, T)
+    _exact_pin(envelope, "exact_weld_sg1", T, g["field"], ctx.get_option("exact_r") * 2e-4 / ctx.get_option("vmax"),
+               100)
     # ray tracer in isolation: the reference's own field in, the reference's rays out
     isx, isz = np.round(scx / 2e-4), np.round(scz / 2e-4)
     for i in (0, 15, 30):
         rx, ry, t = A.find_ray(2e-4, vt, [isx[i], isz[i]], [isx[46], isz[46]], g["field"], veln, velpn, vm, sd, 1)
         ref_t = float(g["time_%d" % i])
-        assert abs(t - ref_t) / ref_t <= 1e-12, (i, t, ref_t)
+        assert abs(t - ref_t) / ref_t <= EXACT, (i, t, ref_t)
         assert len(rx) == len(g["ray_x_%d" % i])
         assert np.max(np.abs(rx - g["ray_x_%d" % i])) <= 1e-9 and np.max(np.abs(ry - g["ray_y_%d" % i])) <= 1e-9
 
 
-def test_weld_sg9_field_and_rays(golden, A):
+def test_weld_sg9_field_and_rays(golden, A, envelope):
     """travel_finer_grid, subgrid 9 (the reference's weld example): 3808 x 4492 fine field, then
     rays 0/15/30 -> 46 on the GPU field vs the reference's rays on its own field."""
     g = golden("weld_sg9")
@@ -151,21 +186,19 @@ def test_weld_sg9_field_and_rays(golden, A):
     scx, scz = W.weld_transducers()
     T = A.travel_finer_grid(scx[46], scz[46], veln, velpn, vm, sd, 9, vt, vt, 0, 0, 2e-4, 2e-4)
     assert T.shape == tuple(g["fine_shape"])
-    dec = T[::9, ::9]
-    mx, mean = _field_err(dec, g["field_dec"], (250, 423))
-    assert mx <= FIELD_MAX and mean <= FIELD_MEAN, (mx, mean)
-    for line, ref in ((T[T.shape[0] // 2], g["row_mid"]), (T[:, T.shape[1] // 2], g["col_mid"])):
+    _check_field(envelope, "weld_sg9_dec9", T[::9, ::9], g["field_dec"], (250, 423))
+    for nm, line, ref in (("row", T[T.shape[0] // 2], g["row_mid"]), ("col", T[:, T.shape[1] // 2], g["col_mid"])):
         r = np.abs(line - ref) / np.maximum(ref, 1e-300)
+        envelope["weld_sg9_" + nm] = float(r.max())
         assert r.max() <= FIELD_MAX, r.max()
     isx, isz = np.round(scx / 2e-4), np.round(scz / 2e-4)
     for i in (0, 15, 30):
         rx, ry, t = A.find_ray(2e-4, vt, [9 * isx[i], 9 * isz[i]], [9 * isx[46], 9 * isz[46]], T, veln, velpn, vm,
                                sd, 9)
-        ref_t = float(g["time_%d" % i])
-        assert abs(t - ref_t) / ref_t <= RAY_END2END, (i, t, ref_t)
+        _ray_err(envelope, "ray_weld_sg9", t, float(g["time_%d" % i]))
 
 
-def test_notebook_kats_end_to_end(golden, A):
+def test_notebook_kats_end_to_end(golden, A, envelope):
     """K1-K3 through the unchanged ALI_FMM surface (GPU fields + GPU rays) vs the published outputs."""
     g = golden("kat_notebook")
     dnx = 1e-3
@@ -176,7 +209,7 @@ def test_notebook_kats_end_to_end(golden, A):
         vm[:, j] = 3000 + 21 * j
     M = A.ALI_FMM(veln, velpn, vm, dnx * np.array([1, 199]), dnx * np.array([30, 180]), dnx=1e-3)
     t = M.find_all_TTF_rays(veln, velpn, vm)
-    assert abs(t[0, 1] - 5.08845096e-05) / 5.08845096e-05 <= RAY_END2END
+    _ray_err(envelope, "kat_k1", t[0, 1], 5.08845096e-05, KAT_END2END)
     c22, c23, c33, c44, sigma = 249.0e9, 133.0e9, 205.0e9, 125.0e9, 7850
     vm1 = np.ones((201, 201))
     M1 = A.ALI_FMM(veln, velpn, vm1, dnx * np.array([1, 199]), dnx * np.array([100, 140]), dnx=1e-3)
@@ -188,7 +221,7 @@ def test_notebook_kats_end_to_end(golden, A):
     trans[0, 1] = 1
     t = M1.find_all_TTF_rays(veln, velpn, vm1, trans_pairs=trans)
     for (i, j), tp in {(0, 1): 3.54124066e-05, (1, 0): 3.54107926e-05}.items():
-        assert abs(t[i, j] - tp) / tp <= RAY_END2END
+        _ray_err(envelope, "kat_k2", t[i, j], tp, KAT_END2END)
     sd = W.stif_field(201, 201)
     veln3 = 20 * np.ones((201, 201))
     velpn3 = 0 * np.ones((201, 201), dtype=int)
@@ -196,42 +229,45 @@ def test_notebook_kats_end_to_end(golden, A):
                    dnx=1e-3)
     t = M2.find_all_TTF_rays(veln3, velpn3, vm1, stif_den=sd)
     for (i, j), tp in {(0, 1): 3.56081540e-05, (0, 2): 2.53646805e-05, (1, 2): 2.76255662e-05}.items():
-        assert abs(t[i, j] - tp) / tp <= RAY_END2END
+        _ray_err(envelope, "kat_k3", t[i, j], tp, KAT_END2END)
 
 
-def test_c3_2048_field(golden, ctx):
+def test_c3_2048_field_and_exact_prefix(golden, ctx, envelope):
     """BASELINE C3: 2048^2 Voronoi grains, stiffness everywhere, source (1024, 682), vs the reference
-    field (every 8th node + the source row)."""
+    field (every 8th node + the source row); the source row's exact-prefix cells to 1e-12."""
     g = golden("c3_2048")
     vt = W.default_table()
     ctx.set_model(*W.c3_model(), vt, vt, 1e-3)
     x, z = W.c3_source()
     T = ctx.travel([x], [z])[0]
-    mx, mean = _field_err(T[::8, ::8], g["field_dec8"], (1024 / 8, 682 / 8), excl=1)
-    assert mx <= FIELD_MAX and mean <= FIELD_MEAN, (mx, mean)
+    _check_field(envelope, "c3_dec8", T[::8, ::8], g["field_dec8"], (1024 / 8, 682 / 8), excl=1)
     r = np.abs(T[682] - g["row_src"]) / np.maximum(g["row_src"], 1e-300)
     r[1019:1030] = 0  # within 5 nodes of the source
+    envelope["c3_row_src"] = float(r.max())
     assert r.max() <= FIELD_MAX, r.max()
+    tstop = ctx.get_option("exact_r") * 1e-3 / ctx.get_option("vmax")
+    _exact_pin(envelope, "exact_c3_row", T[682], g["row_src"], tstop, 10)
 
 
-def test_c4_4096_fields_rays_and_batch_consistency(golden, ctx):
+def test_c4_4096_fields_rays_and_batch_consistency(golden, ctx, envelope):
     """BASELINE C4/C5 grid (4096^2 weld-like): a top-surface source field and a bottom receiver
-    field vs the reference (every 8th node), the 5 reference rays through the REFERENCE's receiver
-    field (ray kernel in isolation, bit-level), and per-source fields that do not depend on the
-    batch they were computed in (a 4-source batch vs single-source calls: bit-identical)."""
+    field vs the reference (every 8th node, exact prefix included), the 5 reference rays end to
+    end, and per-source fields that do not depend on the batch they were computed in (a 4-source
+    batch vs single-source calls: bit-identical)."""
     g = golden("c4_weldlike")
     vt = W.default_table()
     dnx = W.weldlike_dnx()
     veln, velpn, vm, sd = W.weldlike_model()
     ctx.set_model(veln, velpn, vm, sd, vt, vt, dnx)
+    tstop = ctx.get_option("exact_r") * dnx / ctx.get_option("vmax")
     sx, sz = W.c4_sources(128)
     k = int(g["src_index"])
     T = ctx.travel([sx[k]], [sz[k]])[0]
-    mx, mean = _field_err(T[::8, ::8], g["field_dec8"], ((16 + 32 * k) / 8, 0), excl=1)
-    assert mx <= FIELD_MAX and mean <= FIELD_MEAN, (mx, mean)
+    _check_field(envelope, "c4_src%d_dec8" % k, T[::8, ::8], g["field_dec8"], ((16 + 32 * k) / 8, 0), excl=1)
+    _exact_pin(envelope, "exact_c4_src", T[::8, ::8], g["field_dec8"], tstop, 3)
     TR = ctx.travel([dnx * 2056], [dnx * 4095])[0]
-    mx, mean = _field_err(TR[::8, ::8], g["rec_field_dec8"], (2056 / 8, 4095 / 8), excl=1)
-    assert mx <= FIELD_MAX and mean <= FIELD_MEAN, (mx, mean)
+    _check_field(envelope, "c4_rec_dec8", TR[::8, ::8], g["rec_field_dec8"], (2056 / 8, 4095 / 8), excl=1)
+    _exact_pin(envelope, "exact_c4_rec", TR[::8, ::8], g["rec_field_dec8"], tstop, 3)
     # batch independence: sources 0..3 together == each alone (sources never share state)
     B = ctx.travel(sx[:4], sz[:4])
     for i in (0, 3):
@@ -244,16 +280,112 @@ def test_c4_4096_fields_rays_and_batch_consistency(golden, ctx):
     ctx.put_field(0, 1, TR)
     t, lens, flags, rays = ctx.find_rays([0] * 5, [[x, 0.0] for x in xs], [[2056.0, 4095.0]] * 5)
     for i, x in enumerate(xs):
-        ref_t = float(g["time_%d" % x])
-        assert abs(t[i] - ref_t) / ref_t <= RAY_END2END, (x, t[i], ref_t)
+        _ray_err(envelope, "ray_c4", t[i], float(g["time_%d" % x]))
         rx = g["ray_x_%d" % x]
         assert abs(len(rays[i][0]) - len(rx)) <= 0.02 * len(rx), (x, len(rays[i][0]), len(rx))
 
 
-def test_weld_example_end_to_end(golden, A):
+def test_c4_full_128_source_batch(golden, ctx, envelope):
+    """The benchmarked configuration itself: all 128 C4 sources in one call (auto members per
+    source), fields left resident; the golden source's field vs the reference, and a few slots
+    bit-identical to single-source calls (which run with 16 members per source)."""
+    g = golden("c4_weldlike")
+    vt = W.default_table()
+    dnx = W.weldlike_dnx()
+    ctx.set_model(*W.weldlike_model(), vt, vt, dnx)
+    sx, sz = W.c4_sources(128)
+    k = int(g["src_index"])
+    ctx.travel(sx, sz, copy_out=False)
+    kb = int(ctx.get_option("last_k"))
+    Tk = ctx.get_field(k, 1)
+    _check_field(envelope, "c4_batch128_src%d_dec8" % k, Tk[::8, ::8], g["field_dec8"], ((16 + 32 * k) / 8, 0),
+                 excl=1)
+    others = {i: ctx.get_field(i, 1) for i in (0, 127)}
+    steps = [int(ctx.source_stats(i)[0][3]) for i in range(128)]
+    envelope["c4_batch128"] = {"members": kb, "steps_mean": float(np.mean(steps))}
+    assert all(s > 0 for s in steps)
+    # the resident fields come back through copy_fields exactly as get_field returns them
+    C, gbps = ctx.copy_fields(0, 2, 1)
+    assert np.array_equal(C[0], others[0]) and gbps > 0
+    for i, Ti in list(others.items()) + [(k, Tk)]:
+        S = ctx.travel([sx[i]], [sz[i]])[0]
+        assert int(ctx.get_option("last_k")) != kb or kb == 16
+        assert np.array_equal(S, Ti), i
+    ctx.release_fields()
+
+
+def test_members_bit_identical(ctx, envelope):
+    """One source over K = 2, 4, 16 workgroups (column stripes, one exchange per band step) gives
+    the same bits as K = 1: C4 sources on stripe boundaries, the grid corners and the interior;
+    the weld model at subgrid 3 (stage grids + fine-grid main loop)."""
+    vt = W.default_table()
+    dnx = W.weldlike_dnx()
+    ctx.set_model(*W.weldlike_model(), vt, vt, dnx)
+    xs = dnx * np.array([0.0, 63.0, 64.0, 2047.0, 4095.0, 1000.0])
+    zs = dnx * np.array([0.0, 0.0, 100.0, 4095.0, 4095.0, 2000.0])
+    try:
+        ctx.set_option("members", 1)
+        ref = ctx.travel(xs, zs)
+        assert ctx.get_option("last_k") == 1.0
+        for K in (2, 4, 16):
+            ctx.set_option("members", K)
+            F = ctx.travel(xs, zs)
+            assert ctx.get_option("last_k") == K
+            assert np.array_equal(F, ref), (K, [float(np.nanmax(np.abs(F[i] - ref[i]))) for i in range(len(xs))])
+        del ref, F
+        veln, velpn, vm, sd = W.weld_model()
+        ctx.set_model(veln, velpn, vm, sd, vt, vt, 2e-4)
+        scx, scz = W.weld_transducers()
+        ctx.set_option("members", 1)
+        ref = ctx.travel(scx[[0, 46]], scz[[0, 46]], subgrid=3)
+        for K in (2, 8):
+            ctx.set_option("members", K)
+            assert np.array_equal(ctx.travel(scx[[0, 46]], scz[[0, 46]], subgrid=3), ref), K
+    finally:
+        ctx.set_option("members", 0)
+    ctx.release_fields()
+
+
+def test_band_fouds18_path_vs_oracle(golden, ctx, envelope):
+    """fouds18_A() as the band kernel runs it (the material record + the per-material slownesses
+    precomputed by mat_slowness_kernel, fouds18<true>) against the oracle's fouds18_A with the
+    same cell's material, on the reference's own neighbourhoods, for both material views (subgrid
+    1 as is; subgrid > 1 with finer_grid_n's int32 orientation / float32 vel_map)."""
+    g = golden("local_ops")
+    vt = W.default_table()
+    n = len(g["f_out"])
+    f = g["f_args"]
+    iz, ix, dnx = f[:, 0].astype(np.int32), f[:, 1].astype(np.int32), f[:, 2]
+    nsts = g["f_nsts"].astype(np.int32)
+    rng = np.random.default_rng(7)
+    # weld: orientation columns; C3: per-cell stiffness (velpn 0) in every grain
+    for name, (veln, velpn, vm, sd), dx in (("weld", W.weld_model(), 2e-4), ("c3", W.c3_model(512), 1e-3)):
+        ctx.set_model(veln, velpn, vm, sd, vt, vt, dx)
+        mz = rng.integers(0, veln.shape[0], n)
+        mx = rng.integers(0, veln.shape[1], n)
+        for quant in (0, 1):
+            out = ctx.fouds18_band(g["f_ttn"], nsts, iz, ix, dnx, dnx, np.full(n, 7), np.full(n, 7), mz, mx, quant)
+            ref = np.empty(n)
+            for c in range(n):
+                a, b = veln[mz[c], mx[c]], vm[mz[c], mx[c]]
+                if quant:
+                    a, b = float(int(a)), float(np.float32(b))
+                st = None if sd is None else np.ascontiguousarray(np.broadcast_to(sd[mz[c], mx[c]], (7, 7, 5)))
+                ref[c] = O.fouds18_A(int(iz[c]), int(ix[c]), nsts[c], g["f_ttn"][c], dnx[c], dnx[c], 7, 7,
+                                     np.full((7, 7), a), np.full((7, 7), int(velpn[mz[c], mx[c]]), dtype=np.int64),
+                                     np.full((7, 7), b), vt, st)
+            rel = np.abs(out - ref) / np.maximum(np.abs(ref), 1e-300)
+            envelope["fouds18_band_%s_q%d" % (name, quant)] = {"exact_frac": float(np.mean(out == ref)),
+                                                               "rel_max": float(rel.max())}
+            assert np.mean(out == ref) >= 0.99 and rel.max() <= EXACT, (name, quant, np.mean(out == ref), rel.max())
+
+
+def test_weld_example_end_to_end(golden, A, envelope, tmp_path):
     """Weld_rays.py (the reference's example) through the unchanged ALI_FMM surface, minus plots:
     31 bottom receiver fields at subgrid 9 + 961 top->bottom rays (find_all_TTF_rays_parallel),
     the trimmed ray arrays the script saves, and rays 0/15/30 -> 46 vs the reference's times."""
+    import raystore
+
     veln, velpn, vel_map, stif = W.weld_model()
     velpn = velpn.astype(int)
     sx, sy = W.weld_transducers()
@@ -264,8 +396,7 @@ def test_weld_example_end_to_end(golden, A):
     t = M.find_all_TTF_rays_parallel(veln, velpn, vel_map, stif_den=stif, n_threads=8, trans_pairs=pairs)
     g = golden("weld_sg9")
     for i in (0, 15, 30):
-        ref = float(g["time_%d" % i])
-        assert abs(t[i, 46] - ref) / ref <= RAY_END2END, (i, t[i, 46], ref)
+        _ray_err(envelope, "ray_weld_example", t[i, 46], float(g["time_%d" % i]))
     assert np.all(t[:n, n:] > 0) and np.all(t[n:, :] == 0) and np.all(t[:n, :n] == 0)
     max_len = int(np.max(M.ray_len))
     assert 2 < max_len <= M.ray_paths_x.shape[2]
@@ -290,34 +421,43 @@ def test_weld_example_end_to_end(golden, A):
     rx2, ry2 = M2.ray_path(15, 46)
     np.testing.assert_array_equal(rx2, rx)
     np.testing.assert_array_equal(ry2, ry)
+    # save_ray_store round trip: the .npz reads back (np.load, no pickles) to the same rays
+    path = str(tmp_path / "rays.npz")
+    M2.save_ray_store(path)
+    S = raystore.RayStore.load(path)
+    np.testing.assert_array_equal(S.ray_len, M.ray_len)
+    for i, j in ((0, 46), (15, 46), (30, 61)):
+        x, z = S.path(i, j)
+        np.testing.assert_array_equal(x, M.ray_paths_x[i, j, 0:M.ray_len[i, j]])
+        np.testing.assert_array_equal(z, M.ray_paths_y[i, j, 0:M.ray_len[i, j]])
 
 
-def test_pair_kernel_identical_to_single_workgroup(ctx):
-    """Two workgroups per source (fmm_band_pair.hip) vs one (fmm_band.hip): bit-identical fields,
-    subgrid 1 on the C4 grid (sources across stripe boundaries and the grid corner) and subgrid 3
-    on the weld model."""
-    vt = W.default_table()
-    dnx = W.weldlike_dnx()
-    ctx.set_model(*W.weldlike_model(), vt, vt, dnx)
-    xs = dnx * np.array([0.0, 63.0, 64.0, 2047.0, 4095.0, 1000.0])
-    zs = dnx * np.array([0.0, 0.0, 100.0, 4095.0, 4095.0, 2000.0])
-    ctx.set_option("pair", 1)
-    A = ctx.travel(xs, zs)
-    assert ctx.get_option("last_pair") == 1.0
-    ctx.set_option("pair", 0)
-    Bf = ctx.travel(xs, zs)
-    assert ctx.get_option("last_pair") == 0.0
-    ctx.set_option("pair", 1)
-    assert np.array_equal(A, Bf), [float(np.max(np.abs(A[i] - Bf[i]))) for i in range(len(xs))]
-    del A, Bf
+def test_update_parallel_low_mem_and_update_i(golden, A, envelope, tmp_path, monkeypatch):
+    """update_parallel(low_mem=True) writes temp_TTF_<i>.npy per selected source into the working
+    directory and returns None (:3938-4051, spill :3614/:3668), the files bit-equal to update();
+    update_i (:4053-4088) at subgrid 1 and 9 equals the batch call's field, and at subgrid 9 the
+    reference's weld field."""
     veln, velpn, vm, sd = W.weld_model()
-    ctx.set_model(veln, velpn, vm, sd, vt, vt, 2e-4)
-    scx, scz = W.weld_transducers()
-    A = ctx.travel(scx[[0, 46]], scz[[0, 46]], subgrid=3)
-    ctx.set_option("pair", 0)
-    Bf = ctx.travel(scx[[0, 46]], scz[[0, 46]], subgrid=3)
-    ctx.set_option("pair", 1)
-    assert np.array_equal(A, Bf)
+    velpn = velpn.astype(int)
+    sx, sy = W.weld_transducers()
+    M = A.ALI_FMM(veln, velpn, vm, sx, sy, stif_den=sd, dnx=0.0002)
+    sel = np.zeros(len(sx), dtype=int)
+    sel[[3, 46, 60]] = 1
+    F = M.update(veln, velpn, vm, stif_den=sd, subgrid_size=1, sources=sel)
+    monkeypatch.chdir(tmp_path)
+    assert M.update_parallel(veln, velpn, vm, stif_den=sd, subgrid_size=1, sources=sel, n_threads=2,
+                             low_mem=True) is None
+    assert sorted(p.name for p in tmp_path.iterdir()) == ["temp_TTF_3.npy", "temp_TTF_46.npy", "temp_TTF_60.npy"]
+    for i in (3, 46, 60):
+        np.testing.assert_array_equal(np.load(tmp_path / ("temp_TTF_%d.npy" % i)), F[i])
+    np.testing.assert_array_equal(M.update_i(46, veln, velpn, vm, stif_den=sd, subgrid_size=1), F[46])
+    T9 = M.update_i(46, veln, velpn, vm, stif_den=sd, subgrid_size=9)
+    g = golden("weld_sg9")
+    assert T9.shape == tuple(g["fine_shape"])
+    _check_field(envelope, "update_i_sg9_dec9", T9[::9, ::9], g["field_dec"], (250, 423))
+    sel9 = np.zeros(len(sx), dtype=int)
+    sel9[46] = 1
+    np.testing.assert_array_equal(M.update(veln, velpn, vm, stif_den=sd, subgrid_size=9, sources=sel9)[46], T9)
 
 
 def test_sharded_contexts_bit_identical(A, monkeypatch):
@@ -351,7 +491,7 @@ def test_sharded_contexts_bit_identical(A, monkeypatch):
                 np.testing.assert_array_equal(a, b)
 
 
-def test_empty_and_degenerate_requests(A, ctx):
+def test_empty_and_degenerate_requests(A, ctx, envelope):
     """Edge cases of the drop-in surface: no selected sources, no ray pairs, a 1-column grid, a
     source outside the grid (reference: IndexError-like failure -> the C-ABI's argument error)."""
     import _alifmm
@@ -375,8 +515,7 @@ def test_empty_and_degenerate_requests(A, ctx):
     v2, p2, m2 = np.zeros((n, 2)), np.ones((n, 2), dtype=np.int64), np.full((n, 2), 5790.0)
     T = A.travel(0.0, 0.0, None, None, 0, np.zeros((n, 2)), v2, p2, m2, None, vt, vt, 0, 0, 1e-3, 1e-3, 2, n)
     R = O.travel(0.0, 0.0, v2, p2, m2, None, vt, vt, dnx=1e-3)
-    mx, mean = _field_err(T, R, (0, 0))
-    assert mx <= FIELD_MAX and mean <= FIELD_MEAN, (mx, mean)
+    _check_field(envelope, "two_column", T, R, (0, 0), tol=(SMALL_MAX, SMALL_MEAN))
     # a source outside the grid is an argument error, not a fault
     with pytest.raises(_alifmm.AlifmmError):
         ctx.travel(np.array([1.0]), np.array([0.0]))

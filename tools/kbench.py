@@ -22,7 +22,7 @@ def main():
     name = sys.argv[1]
     sizes = [int(a) for a in sys.argv[2:]] or [128, 16]
     ctx = _alifmm.Context(0)
-    for opt in ("kernel", "members", "stripe_log", "cdelta"):  # ALIFMM_OPT_<NAME>=value
+    for opt in ("members", "stripe_log", "cdelta"):  # ALIFMM_OPT_<NAME>=value
         v = os.environ.get("ALIFMM_OPT_" + opt.upper())
         if v is not None:
             ctx.set_option(opt, float(v))

@@ -1,4 +1,4 @@
-"""K-member band kernel (fmm_band_k.hip) vs the round-1 kernels: bit-identity and timing.
+"""K-member band kernel (fmm_band_k.hip): bit-identity of K = 2..16 against K = 1, timing, phase profile.
 
 python tools/kcheck.py [quick]   (GPU box)
 """
@@ -16,8 +16,7 @@ import _alifmm  # noqa: E402
 import workloads as W  # noqa: E402
 
 
-def run(ctx, xs, zs, sg=1, kernel=0, members=0):
-    ctx.set_option("kernel", kernel)
+def run(ctx, xs, zs, sg=1, members=0):
     ctx.set_option("members", members)
     t = time.perf_counter()
     F = ctx.travel(xs, zs, subgrid=sg)
@@ -34,10 +33,10 @@ def main():
     ctx.set_model(*W.weldlike_model(), vt, vt, dnx)
     xs = dnx * np.array([0.0, 63.0, 64.0, 2047.0, 4095.0, 1000.0])
     zs = dnx * np.array([0.0, 0.0, 100.0, 4095.0, 4095.0, 2000.0])
-    ref, dt, _, tm = run(ctx, xs, zs, kernel=1)
+    ref, dt, _, tm = run(ctx, xs, zs, members=1)
     out["c4_ref_s"] = dt
-    for K in ([2, 16] if quick else [1, 2, 4, 8, 16]):
-        F, dt, k, tm = run(ctx, xs, zs, kernel=0, members=K)
+    for K in ([2, 16] if quick else [2, 4, 8, 16]):
+        F, dt, k, tm = run(ctx, xs, zs, members=K)
         same = [bool(np.array_equal(F[i], ref[i])) for i in range(len(xs))]
         diff = [float(np.nanmax(np.abs(F[i] - ref[i]))) for i in range(len(xs))]
         out["c4_K%d" % K] = {"k": k, "same": same, "maxdiff": diff, "s": dt, "band_ms": tm[1]}
@@ -48,31 +47,30 @@ def main():
     ctx.set_model(veln, velpn, vm, sd, vt, vt, 2e-4)
     scx, scz = W.weld_transducers()
     for sg in (1, 3):
-        ref, _, _, _ = run(ctx, scx[[0, 46]], scz[[0, 46]], sg=sg, kernel=1)
+        ref, _, _, _ = run(ctx, scx[[0, 46]], scz[[0, 46]], sg=sg, members=1)
         for K in (2, 8):
-            F, dt, k, tm = run(ctx, scx[[0, 46]], scz[[0, 46]], sg=sg, kernel=0, members=K)
+            F, dt, k, tm = run(ctx, scx[[0, 46]], scz[[0, 46]], sg=sg, members=K)
             same = [bool(np.array_equal(F[i], ref[i])) for i in range(2)]
             out["weld_sg%d_K%d" % (sg, K)] = {"k": k, "same": same, "s": dt}
             print(json.dumps({"weld_sg%d_K%d" % (sg, K): out["weld_sg%d_K%d" % (sg, K)]}), flush=True)
-    # timing: C4 128 sources (auto K) and 16 sources (auto K), old vs new
+    # timing: C4 128 and 16 sources, K = 1 vs auto K
     ctx.set_model(*W.weldlike_model(), vt, vt, dnx)
     sx, sz = W.c4_sources(128)
     for ns in (128, 16):
-        for kern in (1, 0):
-            ctx.set_option("kernel", kern)
-            ctx.set_option("members", 0)
+        for kern in (1, 0):  # members: 1, auto
+            ctx.set_option("members", kern)
             ctx.travel(sx[:ns], sz[:ns], copy_out=False)  # warm
             t = time.perf_counter()
             ctx.travel(sx[:ns], sz[:ns], copy_out=False)
             dt = time.perf_counter() - t
             ti, tb, tt = ctx.last_timing()
-            r = {"kernel": kern, "k": ctx.get_option("last_k"), "wall_s": dt, "init_ms": ti, "band_ms": tb,
+            r = {"members_opt": kern, "k": ctx.get_option("last_k"), "wall_s": dt, "init_ms": ti, "band_ms": tb,
                  "steps": int(ctx.source_stats(0)[0][3]), "sweeps": int(sum(ctx.source_stats(i)[1] for i in range(ns)))}
             out["c4_time_%d_k%d" % (ns, kern)] = r
-            print(json.dumps({"c4_time_%d_kernel%d" % (ns, kern): r}), flush=True)
+            print(json.dumps({"c4_time_%d_members%d" % (ns, kern): r}), flush=True)
     # phase profile (in-kernel wall clock, 100 MHz ticks -> us per step) of the K kernel
     for ns in (128, 16):
-        ctx.set_option("kernel", 0)
+        ctx.set_option("members", 0)
         ctx.set_option("prof", 1)
         ctx.travel(sx[:ns], sz[:ns], copy_out=False)
         ctx.set_option("prof", 0)

@@ -1,5 +1,5 @@
 """Summarise a tools/profile.sh run: kernel-trace stats -> profiles/TAG_kernel_stats.csv, and the
-per-launch HBM-side traffic of the band kernel (fmm_band_pair_kernel, or fmm_band_kernel) from the FETCH_SIZE / WRITE_SIZE passes ->
+per-launch HBM-side traffic of the band kernel (fmm_band_k_kernel) from the FETCH_SIZE / WRITE_SIZE passes ->
 profiles/TAG_traffic.json (bench.py reports it as roofline.traffic when the library matches).
 
 Correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE counts 128-B requests at 64 B on gfx950,
@@ -26,7 +26,7 @@ def per_launch(d, counter):
     vals = {}
     for f in glob.glob(os.path.join(out, d, "*counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            if "fmm_band" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            if "fmm_band_k_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter:
                 vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
     return sum(vals.values()) / len(vals) if vals else None
 
@@ -43,14 +43,13 @@ for f in ("pmc_fetch.log", "pmc_write.log"):
         cfg = json.loads(line)["config"]
         cfg.pop("total_sources", None)  # per-GPU workload: the same launch at any world size
         cfg.setdefault("cdelta", None)  # bench lines before these keys ran the defaults
-        cfg.setdefault("exact_r", None)
         if bench_config is not None and cfg != bench_config:
             sys.exit("FETCH and WRITE passes profiled different workloads: %s vs %s" % (bench_config, cfg))
         bench_config = cfg
     except (OSError, IndexError):
         pass
 res = {
-    "kernel": "fmm_band_pair_kernel / fmm_band_kernel (the band kernel of the run)",
+    "kernel": "fmm_band_k_kernel",
     "fetch_size_kb_per_launch": fetch_kb,
     "write_size_kb_per_launch": write_kb,
     "traffic_bytes_per_launch": (2 * fetch_kb + write_kb) * 1024 if fetch_kb and write_kb else None,
@@ -58,6 +57,9 @@ res = {
                   "L2 memory-side requests (Infinity-Cache hits included)",
     "libalifmm_sha256": hashlib.sha256(open(lib, "rb").read()).hexdigest(),
     "bench_config": bench_config,
+    # the workload keys bench.py matches before it reports the figure as roofline.traffic
+    "sources_per_gpu": (bench_config or {}).get("sources_per_gpu"),
+    "grid": (bench_config or {}).get("grid"),
 }
 json.dump(res, open(os.path.join(repo, "profiles", tag + "_traffic.json"), "w"), indent=1)
 print(json.dumps(res))
