@@ -3,10 +3,31 @@
 // The local operators below are the reference's arithmetic (Anis_TTF_rays.py, cited per
 // function) in double precision, operation order preserved and compiled with
 // -ffp-contract=off, so that a cell evaluated on the same neighbourhood matches the CPU
-// oracle to the last bit except where ocml's atan/tan/sin/cos differ from glibc by an ulp.
+// oracle to the last bit except where the trigonometric functions differ from glibc's.
+// AF_CRMATH (default 1): atan / sin / cos / tan are cr_math.h's correctly rounded ones (glibc's
+// results on all but ~0.1 % of arguments, where glibc itself is off by just over half an ulp);
+// 0: ocml's (~1 % of results an ulp away).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#ifndef AF_CRMATH
+#define AF_CRMATH 1
+#endif
+#if AF_CRMATH
+#include "cr_math.h"
+#define AF_ATAN crm::atan
+#define AF_SIN crm::sin
+#define AF_COS crm::cos
+#define AF_TAN crm::tan
+#define AF_SINCOS crm::sincos
+#else
+#define AF_ATAN atan
+#define AF_SIN sin
+#define AF_COS cos
+#define AF_TAN tan
+#define AF_SINCOS sincos
+#endif
 
 #define AF_DEV __device__ __forceinline__
 
@@ -148,24 +169,24 @@ AF_DEV double christoffel_group(const double* s, double eff, double vm) {
     return 1000 * vm * sqrt(lam / sigma);
   }
   double c22 = s[0], c23 = s[1], c33 = s[2], c44 = s[3];
-  double tan_ang = tan(eff * kDeg2Rad);
+  double tan_ang = AF_TAN(eff * kDeg2Rad);
   double A = c22 + c33 - 2 * c44;
   double B = (c23 + c44) * (tan_ang - 1 / tan_ang);
   double C = c22 - c33;
   double disc = B * B + A * A - C * C;
   double pa;
   if (eff < 90)
-    pa = pymod(atan((-B - sqrt(disc)) / (C - A)), M_PI);
+    pa = pymod(AF_ATAN((-B - sqrt(disc)) / (C - A)), M_PI);
   else
-    pa = pymod(atan((-B + sqrt(disc)) / (C - A)), M_PI);
-  double lam = 0.5 * (cos(2 * pa) * (c22 - c44) + sin(2 * pa) * (c23 + c44) * tan_ang + c22 + c44);
-  return 1000 * vm * sqrt(lam / sigma) / cos(eff * kDeg2Rad - pa);
+    pa = pymod(AF_ATAN((-B + sqrt(disc)) / (C - A)), M_PI);
+  double lam = 0.5 * (AF_COS(2 * pa) * (c22 - c44) + AF_SIN(2 * pa) * (c23 + c44) * tan_ang + c22 + c44);
+  return 1000 * vm * sqrt(lam / sigma) / AF_COS(eff * kDeg2Rad - pa);
 }
 
 // Christoffel PHASE velocity (update() :1400-1406).
 AF_DEV double christoffel_phase(const double* s, double eff, double vm) {
-  double ca = cos(eff * kDeg2Rad);
-  double sa = sin(eff * kDeg2Rad);
+  double sa, ca;
+  AF_SINCOS(eff * kDeg2Rad, &sa, &ca);
   double A = ca * ca * s[0] + sa * sa * s[3];
   double B = ca * sa * (s[1] + s[3]);
   double C = ca * ca * s[3] + sa * sa * s[2];
@@ -197,7 +218,7 @@ AF_DEV void wad(I ix, I iz, I x1, I x2, I x3, I z1, I z2, I z3, double y1, doubl
   if (dx == 0)
     angle = 0.0;
   else
-    angle = pymod(atan(dz / dx) * kRad2Deg + 90, 180);
+    angle = pymod(AF_ATAN(dz / dx) * kRad2Deg + 90, 180);
   dist = fabs(dz * (double)(x2 - ix) - dx * (double)(z2 - iz)) / sqrt(dx * dx + dz * dz);
 }
 
@@ -209,7 +230,7 @@ AF_DEV double tbp(const DevModel& M, double x1, double x2, double y1, double y2,
   y2 = y2 / (double)sg;
   double section_time = 0.0;
   double start_x = x1, end_x = x2, start_y = y1, end_y = y2, prev_x = x1, prev_y = y1;
-  double angle = (x1 == x2) ? 0.0 : atan((y2 - y1) / (x2 - x1)) * kRad2Deg;
+  double angle = (x1 == x2) ? 0.0 : AF_ATAN((y2 - y1) / (x2 - x1)) * kRad2Deg;
   double mm = 0, cc = 0;
   if (end_x != start_x) {
     mm = (end_y - start_y) / (end_x - start_x);

@@ -26,13 +26,19 @@ struct XLds {
   int cell[kXHeap];
 };
 
-// addtree / updtree / downtree (:94-237) over a global nsts array, heap slots in LDS
+// addtree / updtree / downtree (:94-237) over a global nsts array, heap slots in LDS.  Keys are
+// copies of ttn; a node with two heap entries (the stage-1 window corners, added by two of the
+// edge loops :2277-2288) has every entry's key refreshed when its ttn changes (dup / sync), as
+// the reference's comparisons read the live ttn.
+constexpr int kXDup = 8;
 struct XHeap {
   XLds* H;
   int* S;
   const double* T;
   int ntr;
   int err;
+  int ndup = 0;
+  int dup[kXDup];
   AF_DEV static int parent(int t) { return (int)rint((double)t / 2.0); }  // half-even (:123)
   AF_DEV void swap(int a, int b) {
     int c = H->cell[a];
@@ -65,6 +71,13 @@ struct XHeap {
       ntr = kXHeap - 1;
       return;
     }
+    if (S[c] > 0) {  // already in the heap: a second entry
+      if (ndup == kXDup) {
+        err = 3;
+        return;
+      }
+      dup[ndup++] = c;
+    }
     S[c] = ntr;
     H->cell[ntr] = c;
     H->key[ntr] = key;
@@ -75,6 +88,14 @@ struct XHeap {
   AF_DEV void upd(int c, int tpc, double key) {
     H->key[tpc] = key;
     sift_up(c, tpc);
+  }
+  // node c's ttn is now key: every heap entry of a node with two entries takes it
+  AF_DEV void sync(int c, double key) {
+    bool d = false;
+    for (int k = 0; k < ndup; k++) d |= dup[k] == c;
+    if (!d) return;
+    for (int k = 1; k <= ntr; k++)
+      if (H->cell[k] == c) H->key[k] = key;
   }
   AF_DEV void down() {
     if (ntr == 1) {
@@ -176,12 +197,14 @@ AF_DEV long long xloop(XHeap& h, const DevModel& M, const XGrid& g, bool stage, 
           const double v = xrelax(M, g, nbz[k], nbx[k]);
           g.T[r] = v;
           h.add(r, v);
+          if (h.ndup) h.sync(r, v);
         } else if (st[k] > 0) {
           // the heap index read up front is still the node's: only earlier neighbours' sift-ups
           // move heap entries in between, and they may move this node — re-read it from S then
           const double v = xrelax(M, g, nbz[k], nbx[k]);
           g.T[r] = v;
           h.upd(r, g.S[r], v);
+          if (h.ndup) h.sync(r, v);
         }
       } else if (stage && (k < 2 ? abs(isx_s - nbx[k]) : abs(isz_s - nbz[k])) == max_dist + 1) {
         finished = true;
@@ -267,7 +290,7 @@ __global__ __launch_bounds__(64) void fmm_exact_kernel(BandParams P) {
       for (int k = lane; k < w * w; k += blockDim.x) {
         const int i = k / w - side1, j = k % w - side1;
         if (0 <= isz_s + i && isz_s + i <= g.nz - 1 && 0 <= isx_s + j && isx_s + j <= g.nx - 1) {
-          double angle = (j == 0) ? 90.0 : atan((double)i / (double)j) * kRad2Deg;
+          double angle = (j == 0) ? 90.0 : AF_ATAN((double)i / (double)j) * kRad2Deg;
           double eff = pymod(cs.veln + angle, 180);
           double velocity = (cs.velpn != 0 || cs.stif == nullptr) ? table_vel(M.gtab, M.ncol, eff, cs.velpn, cs.vm)
                                                                   : christoffel_group(cs.stif, eff, cs.vm);

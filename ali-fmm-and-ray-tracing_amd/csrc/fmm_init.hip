@@ -46,12 +46,18 @@ struct LdsField {
 
 // addtree / updtree / downtree (:94-237).  Keys are stored in the heap next to the node (a copy
 // of its ttn, refreshed by every add/upd), so a sift level is one LDS read instead of two
-// dependent ones; comparisons are exactly the reference's.
+// dependent ones; comparisons are exactly the reference's.  The reference compares live ttn, so
+// a node with two heap entries (the stage-1 window corners, added by two of the edge loops
+// :1601-1612) has both entries' keys change when its ttn does: such nodes are recorded (dup) and
+// every key of theirs is refreshed with their ttn (sync).
+constexpr int kInitDup = 8;
 struct Heap {
   InitLds* L;
   int nz, nx;
   int ntr;
   int err;
+  int ndup = 0;
+  unsigned short dup[kInitDup];
   AF_DEV int bz(int k) const { return L->hcell[k] >> 8; }
   AF_DEV int bx(int k) const { return L->hcell[k] & 255; }
   AF_DEV double tb(int k) const { return L->hkey[k]; }
@@ -80,9 +86,15 @@ struct Heap {
     }
   }
   // addtree :94-138
-  AF_DEV void add(int iz, int ix) {
+  // fresh: the node is known to be far (a relaxation job; its status already reads 1, set by
+  // the relax role), else its status tells whether it already has an entry
+  AF_DEV void add(int iz, int ix, bool fresh = false) {
     ntr += 1;
     if (ntr >= kInitHeap) { err = 1; ntr = kInitHeap - 1; return; }
+    if (!fresh && L->S[iz * nx + ix] > 0) {  // already in the heap: a second entry
+      if (ndup == kInitDup) { err = 1; return; }
+      dup[ndup++] = (unsigned short)((iz << 8) | ix);
+    }
     L->S[iz * nx + ix] = (short)ntr;
     L->hcell[ntr] = (unsigned short)((iz << 8) | ix);
     L->hkey[ntr] = L->T[iz * nx + ix];
@@ -93,6 +105,16 @@ struct Heap {
     const int tpc = L->S[iz * nx + ix];
     L->hkey[tpc] = L->T[iz * nx + ix];
     sift_up(iz, ix, tpc);
+  }
+  // a node's ttn changed: every heap entry of a node with two entries takes the new value
+  AF_DEV void sync(int iz, int ix) {
+    const unsigned short c = (unsigned short)((iz << 8) | ix);
+    bool d = false;
+    for (int k = 0; k < ndup; k++) d |= dup[k] == c;
+    if (!d) return;
+    const double t = L->T[iz * nx + ix];
+    for (int k = 1; k <= ntr; k++)
+      if (L->hcell[k] == c) L->hkey[k] = t;
   }
   // downtree :178-237
   AF_DEV void down() {
@@ -192,8 +214,9 @@ AF_DEV bool pop_two_role(Heap& h, int& seq, int n) {
   h.down();
   if (!await_value(&L->done, seq)) return false;
   for (int k = 0; k < n; k++) {
-    if (L->jkind[k] & kJobAdd) h.add(L->jz[k], L->jx[k]);
+    if (L->jkind[k] & kJobAdd) h.add(L->jz[k], L->jx[k], true);
     else h.upd(L->jz[k], L->jx[k]);
+    if (h.ndup) h.sync(L->jz[k], L->jx[k]);
   }
   return true;
 }
@@ -410,7 +433,7 @@ __global__ __launch_bounds__(128) void fmm_init_kernel(DevModel M, InitJob* jobs
       for (int k = lane; k < w * w; k += nl) {
         int i = k / w - side1, j = k % w - side1;
         if (0 <= isz_s + i && isz_s + i <= nz - 1 && 0 <= isx_s + j && isx_s + j <= nx - 1) {
-          double angle = (j == 0) ? 90.0 : atan((double)i / (double)j) * kRad2Deg;
+          double angle = (j == 0) ? 90.0 : AF_ATAN((double)i / (double)j) * kRad2Deg;
           double eff = pymod(cs.veln - angle, 180);
           double velocity = (cs.velpn != 0 || cs.stif == nullptr)
                                 ? table_vel(M.gtab, M.ncol, eff, cs.velpn, cs.vm)

@@ -51,7 +51,7 @@ def parse():
     ap.add_argument("--sources", type=int, default=128, help="total sources (strong) or per GPU (--weak)")
     ap.add_argument("--weak", action="store_true", help="every rank runs --sources sources of its own")
     ap.add_argument("--cpu-sample", type=int, default=0, help="sources in the CPU sample (0: one per thread)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0: the CPUs this process may run on")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: the CPUs this job is granted (affinity, cgroup quota)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-return", action="store_true", help="skip the result-return measurement")
     ap.add_argument("--members", type=int, default=None, help="band-kernel workgroups per source (0: auto)")
@@ -70,16 +70,53 @@ def rank_sources(args, rank, world, dnx):
     return dnx * (16 + 32 * kk).astype(np.float64), np.zeros(len(k)), k
 
 
+def _host_cpus():
+    """(usable, quota, physical, logical): CPUs this process may run on (affinity), the job's CPU
+    share in whole CPUs (cgroup quota / OMP_NUM_THREADS; None: unlimited), physical cores and
+    logical CPUs of the host."""
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count()
+    quota = None
+    try:  # cgroup v2, else v1
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            if q > 0:
+                quota = max(1, q // int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read()))
+        except (OSError, ValueError):
+            pass
+    # the GPU boxes state a job's CPU share in OMP_NUM_THREADS (16 per GPU)
+    share = os.environ.get("OMP_NUM_THREADS", "")
+    if share.isdigit() and int(share) > 0:
+        quota = min(quota or int(share), int(share))
+    cores, phys, core = set(), None, None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("physical id"):
+                phys = line.split(":")[1].strip()
+            elif line.startswith("core id"):
+                core = line.split(":")[1].strip()
+                cores.add((phys, core))
+    except OSError:
+        pass
+    return usable, quota, len(cores) or os.cpu_count(), os.cpu_count()
+
+
 def cpu_baseline(args, scx, scz, model, vt, dnx, cells):
+    """the C restatement of the reference's solver, one source per thread on the
+    CPUs this job is granted (affinity and cgroup quota), plus one source on one core; the
+    all-core figure of the host is the 1-core rate times its physical cores (stated as such)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
 
     veln, velpn, vel_map, stif = model
-    try:
-        avail = len(os.sched_getaffinity(0))
-    except AttributeError:
-        avail = os.cpu_count()
-    th = args.cpu_threads or avail
+    usable, quota, phys, logical = _host_cpus()
+    th = args.cpu_threads or min(usable, quota or usable)
     ns = args.cpu_sample or th
     xs, zs = np.resize(scx, ns), np.resize(scz, ns)
     t1 = time.perf_counter()
@@ -95,13 +132,14 @@ def cpu_baseline(args, scx, scz, model, vt, dnx, cells):
         pass
     per_core = cells / one  # cell-updates/s of one core
     return {"value": cells * ns / tc, "unit": "grid-cell updates/s", "cores": th, "kind": "port",
-            "sample": "%d C4 sources (4096^2, z=0) on %d threads (the CPUs this process may use: %d of %d "
-                      "visible), one source per thread, oracle/alifmm_oracle.c (bit-exact restatement of the "
-                      "reference's heap FMM); %.1f s wall; plus 1 source on 1 core: %.2f s"
-                      % (ns, th, avail, os.cpu_count(), tc, one),
-            "host_cpu": model_name, "host_cpus_visible": os.cpu_count(), "host_cpus_usable": avail,
+            "sample": "%d C4 sources (4096^2, z=0) on %d threads (this job's CPUs: affinity %d, share %s), "
+                      "one source per thread, oracle/alifmm_oracle.c (bit-exact restatement of the reference's "
+                      "heap FMM); %.1f s wall; plus 1 source on 1 core: %.2f s"
+                      % (ns, th, usable, quota, tc, one),
+            "host_cpu": model_name, "host_physical_cores": phys, "host_logical_cpus": logical,
             "seconds_per_source_1core": one,
-            "value_all_visible_cores_extrapolated": per_core * os.cpu_count(),
+            "value_1core": per_core,
+            "value_all_physical_cores_extrapolated": per_core * phys,
             "port_vs_numba_reference_per_core": PORT_VS_REFERENCE_PER_CORE}
 
 
@@ -228,7 +266,7 @@ def main():
         }
         if cpu:
             out["speedup_vs_cpu_baseline"] = value / cpu["value"]
-            out["speedup_vs_cpu_all_visible_cores_extrapolated"] = value / cpu["value_all_visible_cores_extrapolated"]
+            out["speedup_vs_cpu_all_physical_cores_extrapolated"] = value / cpu["value_all_physical_cores_extrapolated"]
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -12,7 +12,8 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "lib", "liboracle.so")
+# ALIFMM_ORACLE_LIB: another build of the same restatement (lib/liboracle_cr.so, the CR-trig one)
+_LIB_PATH = os.environ.get("ALIFMM_ORACLE_LIB") or os.path.join(_HERE, "lib", "liboracle.so")
 _lib = None
 
 _d = ctypes.c_double

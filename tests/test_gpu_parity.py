@@ -11,7 +11,8 @@ the run the thresholds are set against, about 2x above it):
   * travel-time fields (band-synchronous reformulation of the heap FMM), cells > 5 nodes from
     the source: rel L-inf <= 3e-3, rel mean <= 5e-5 on the C3, C4 and weld grids (FIELD_*), and
     SMALL_* on the 41..201-node cases, whose errors are larger relative to their small T;
-  * ray travel times end-to-end (GPU fields + GPU rays): rel <= 5e-4 (RAY_END2END).
+  * ray travel times end-to-end (GPU fields + GPU rays): rel <= 5e-4 (RAY_END2END; C4's 4096-node
+    rays 2.5e-3, K1-K3 against the notebook's 9 printed digits 1e-4).
 """
 import numpy as np
 import pytest
@@ -21,10 +22,14 @@ import workloads as W
 
 pytestmark = pytest.mark.gpu
 
+# measured (profiles/r2_parity_envelope.json): C3 5.8e-4 / 1.9e-5, C4 9.0e-4 / 2.1e-5, weld sg1
+# 1.3e-3 / 2.1e-5, weld sg9 6.0e-4 / 1.6e-5; small cases 2.9e-3 / 8.1e-5; rays: weld 6.2e-5, C4
+# 1.2e-3 (through the GPU receiver field, whose own error is 3.5e-4), K1-K3 4.6e-5
 FIELD_MAX, FIELD_MEAN = 3e-3, 5e-5
-SMALL_MAX, SMALL_MEAN = 1e-2, 1e-3
+SMALL_MAX, SMALL_MEAN = 6e-3, 2e-4
 RAY_END2END = 5e-4
-KAT_END2END = 5e-3  # K1-K3: the notebook prints 9 significant digits of its numba run
+RAY_C4 = 2.5e-3
+KAT_END2END = 1e-4  # K1-K3: the notebook prints 9 significant digits of its numba run
 EXACT = 1e-12
 
 
@@ -81,7 +86,7 @@ def test_library_is_the_hip_build():
     assert b"gfx950" in _alifmm.lib().alifmm_version()
 
 
-def test_local_ops_vs_reference_vectors(golden, ctx):
+def test_local_ops_vs_reference_vectors(golden, ctx, envelope):
     g = golden("local_ops")
     n = len(g["u_out"])
     a = g["u_args"]
@@ -91,6 +96,7 @@ def test_local_ops_vs_reference_vectors(golden, ctx):
     ref = g["u_out"]
     exact = np.sum(out == ref)
     rel = np.abs(out - ref) / np.maximum(np.abs(ref), 1e-300)
+    envelope["local_ops_update"] = {"exact_frac": float(exact / n), "rel_max": float(rel.max())}
     assert exact >= 0.99 * n and rel.max() <= 1e-12, (exact, n, rel.max())
     f = g["f_args"]
     m = len(g["f_out"])
@@ -100,10 +106,11 @@ def test_local_ops_vs_reference_vectors(golden, ctx):
     reff = g["f_out"]
     exact = np.sum(outf == reff)
     rel = np.abs(outf - reff) / np.maximum(np.abs(reff), 1e-300)
+    envelope["local_ops_fouds18"] = {"exact_frac": float(exact / m), "rel_max": float(rel.max())}
     assert exact >= 0.99 * m and rel.max() <= 1e-12, (exact, m, rel.max())
 
 
-def test_time_between_points_vs_reference_vectors(golden, ctx):
+def test_time_between_points_vs_reference_vectors(golden, ctx, envelope):
     rows = golden("tbp_weld")["rows"]
     veln, velpn, vm, sd = W.weld_model()
     vt = W.default_table()
@@ -112,6 +119,7 @@ def test_time_between_points_vs_reference_vectors(golden, ctx):
         r = rows[rows[:, 4] == sg]
         out = ctx.time_between_points(r[:, 0], r[:, 1], r[:, 2], r[:, 3], sg)
         rel = np.abs(out - r[:, 5]) / np.maximum(r[:, 5], 1e-300)
+        envelope["tbp_sg%d" % sg] = {"exact_frac": float(np.mean(out == r[:, 5])), "rel_max": float(rel.max())}
         # every piece of the DDA evaluates atan/tan/cos (ocml vs glibc ulps): most values bit-exact
         assert np.mean(out == r[:, 5]) >= 0.9 and rel.max() <= 1e-12, (sg, np.mean(out == r[:, 5]), rel.max())
 
@@ -280,7 +288,7 @@ def test_c4_4096_fields_rays_and_batch_consistency(golden, ctx, envelope):
     ctx.put_field(0, 1, TR)
     t, lens, flags, rays = ctx.find_rays([0] * 5, [[x, 0.0] for x in xs], [[2056.0, 4095.0]] * 5)
     for i, x in enumerate(xs):
-        _ray_err(envelope, "ray_c4", t[i], float(g["time_%d" % x]))
+        _ray_err(envelope, "ray_c4", t[i], float(g["time_%d" % x]), RAY_C4)
         rx = g["ray_x_%d" % x]
         assert abs(len(rays[i][0]) - len(rx)) <= 0.02 * len(rx), (x, len(rays[i][0]), len(rx))
 
