@@ -61,7 +61,24 @@ CR_HD dd div_n(dd a, double n) {
   const double h = a.h / n;
   return fast_two_sum(h, (fma(-h, n, a.h) + a.l) / n);
 }
-CR_HD dd tab(const double (*t)[2], int i) { return {t[i][0], t[i][1]}; }
+// Table reads.  A translation unit that defines CR_LDS_TABLES keeps the tables in LDS on the
+// device (a table entry is then an LDS read instead of a dependent global load, which the
+// latency-bound solver kernels would wait on): each of its kernels calls crm::lds_init() with
+// all threads and synchronises before the first use.
+constexpr int kTabWords = 2 * (129 + 65);
+#if defined(__HIP_DEVICE_COMPILE__) && defined(CR_LDS_TABLES)
+__shared__ double crm_lds_tab[kTabWords];
+__device__ inline void lds_init() {
+  for (int k = threadIdx.x; k < kTabWords; k += blockDim.x)
+    crm_lds_tab[k] = k < 258 ? (&kAtanTab[0][0])[k] : (&kSinTab[0][0])[k - 258];
+}
+CR_HD dd tab_atan(int i) { return {crm_lds_tab[2 * i], crm_lds_tab[2 * i + 1]}; }
+CR_HD dd tab_sin(int i) { return {crm_lds_tab[258 + 2 * i], crm_lds_tab[259 + 2 * i]}; }
+#else
+CR_HD void lds_init() {}
+CR_HD dd tab_atan(int i) { return {kAtanTab[i][0], kAtanTab[i][1]}; }
+CR_HD dd tab_sin(int i) { return {kSinTab[i][0], kSinTab[i][1]}; }
+#endif
 
 // atan(t) for a double-double |t| <= 2^-8 + 2^-20: t + t P(t^2), P = -q/3 + q^2 (1/5 - q/7 + ...)
 CR_HD dd atan_small(dd t) {
@@ -74,10 +91,8 @@ CR_HD dd atan_small(dd t) {
   return add(t, mul(t, P));
 }
 
-CR_HD double atan(double x) {
+CR_HD double atan_accurate(double x) {
   const double a = fabs(x);
-  if (!(a <= 0x1p60)) return a != a ? x + x : copysign(kPio2H, x);  // NaN; pi/2 - 1/a rounds to pi/2
-  if (a < 0x1p-27) return x;  // |atan x - x| < |x|^3 / 3: below half an ulp
   const bool inv = a > 1.0;
   dd u{a, 0.0};
   if (inv) {
@@ -91,7 +106,7 @@ CR_HD double atan(double x) {
   p.l += u.l * c;
   dd d = two_sum(1.0, p.h);
   d = fast_two_sum(d.h, d.l + p.l);
-  dd r = add(tab(kAtanTab, k), atan_small(div(n, d)));
+  dd r = add(tab_atan(k), atan_small(div(n, d)));
   if (inv) r = add({kPio2H, kPio2L}, {-r.h, -r.l});
   return copysign(r.h + r.l, x);
 }
@@ -117,7 +132,7 @@ CR_HD void sincos_dd(double x, dd& s, dd& c) {
   const dd C = add(add({-0.5 * q.h, -0.5 * q.l}, q2_24), {yc, 0.0});  // cos r = 1 + C
   // sin / cos of (j mod 256) pi/128 = qd pi/2 + a from the quarter-period table
   const int m = j & 255, qd = m >> 6, i = m & 63;
-  const dd sa = tab(kSinTab, i), ca = tab(kSinTab, 64 - i);
+  const dd sa = tab_sin(i), ca = tab_sin(64 - i);
   const dd nsa{-sa.h, -sa.l}, nca{-ca.h, -ca.l};
   const dd sj = qd == 0 ? sa : qd == 1 ? ca : qd == 2 ? nsa : nca;
   const dd cj = qd == 0 ? ca : qd == 1 ? nsa : qd == 2 ? nca : sa;
@@ -128,18 +143,97 @@ CR_HD void sincos_dd(double x, dd& s, dd& c) {
   c = add(cj, add(mul(cj, C), {-ssr.h, -ssr.l}));
 }
 
+// Fast paths: the same reductions with the series tails in double (error below 2^-63 of the
+// result), then a rounding test: when the approximation's error interval straddles a rounding
+// boundary (about 1 argument in 2^9), the double-double evaluation above decides.
+CR_HD bool rounds_same(double h, double l, double e) { return h + (l + e) == h + (l - e); }
+
+CR_HD double atan(double x) {
+  const double a = fabs(x);
+  if (!(a <= 0x1p60)) return a != a ? x + x : copysign(kPio2H, x);  // NaN; pi/2 - 1/a rounds to pi/2
+  if (a < 0x1p-27) return x;  // |atan x - x| < |x|^3 / 3: below half an ulp
+  const bool inv = a > 1.0;
+  double uh = a, ul = 0.0;
+  if (inv) {
+    uh = 1.0 / a;
+    ul = fma(-uh, a, 1.0) * uh;
+  }
+  const int k = (int)(uh * 128.0 + 0.5);
+  const double c = k * (1.0 / 128);
+  const double nh = uh - c;  // exact (Sterbenz)
+  const double ph = uh * c, pl = fma(uh, c, -ph) + ul * c;
+  const double dh = 1.0 + ph, dl = ((1.0 - dh) + ph) + pl;  // 1 >= |ph|
+  const double th = nh / dh;
+  const double tl = ((fma(-th, dh, nh) + ul) - th * dl) / dh;
+  const double q = th * th;
+  const double tP = th * q * ((((1.0 / 13 * q - 1.0 / 11) * q + 1.0 / 9) * q - 1.0 / 7) * q * q + (1.0 / 5 * q - 1.0 / 3));
+  // atan u = A_k + t + t P
+  const dd A = tab_atan(k);
+  dd r = two_sum(A.h, th);
+  r.l += (A.l + tl) + tP;
+  if (inv) {
+    dd v = two_sum(kPio2H, -r.h);
+    v.l += kPio2L - r.l;
+    r = v;
+  }
+  const double h = r.h + r.l, l = r.l - (h - r.h);
+  if (rounds_same(h, l, fabs(h) * 0x1p-63)) return copysign(h, x);
+  return copysign(atan_accurate(a), x);
+}
+
+CR_HD void sincos(double x, double* sp, double* cp) {
+  if (!(fabs(x) < 0x1p14)) {
+    *sp = ::sin(x);
+    *cp = ::cos(x);
+    return;
+  }
+  const double jd = nearbyint(x * k128OverPi);
+  const int j = (int)jd;
+  const double r1 = x - jd * kP1;
+  const double p2h = jd * kP2, p2l = fma(jd, kP2, -p2h);
+  const double rh0 = r1 - p2h;
+  const double rl0 = ((r1 - rh0) - p2h) - p2l - jd * kP3;  // r1 - rh0 - p2h exact (|r1| >= |p2h|)
+  const double rh = rh0 + rl0, rl = rl0 - (rh - rh0);
+  const double q = rh * rh;
+  const double S = q * ((((-1.0 / 39916800 * q + 1.0 / 362880) * q - 1.0 / 5040) * q + 1.0 / 120) * q - 1.0 / 6);
+  const double C = q * ((((1.0 / 3628800 * -q + 1.0 / 40320) * q - 1.0 / 720) * q + 1.0 / 24) * q - 0.5);
+  const int m = j & 255, qd = m >> 6, i = m & 63;
+  const dd sa = tab_sin(i), ca = tab_sin(64 - i);
+  const dd nsa{-sa.h, -sa.l}, nca{-ca.h, -ca.l};
+  const dd sj = qd == 0 ? sa : qd == 1 ? ca : qd == 2 ? nsa : nca;
+  const dd cj = qd == 0 ? ca : qd == 1 ? nsa : qd == 2 ? nca : sa;
+  // sin r = r + r S with r = rh + rl: rh + (rl + rh S)
+  const double sr_l = rl + rh * S;
+  // sin x = sj + cj rh + [sj C + cj (rl + rh S) + cj_l rh + sj_l]
+  const dd ps = two_prod(cj.h, rh);
+  const dd s0 = two_sum(sj.h, ps.h);
+  const double sl = s0.l + (ps.l + sj.l + sj.h * C + cj.h * sr_l + cj.l * rh);
+  // cos x = cj - sj rh + [cj C - sj (rl + rh S) - sj_l rh + cj_l]
+  const dd pc = two_prod(-sj.h, rh);
+  const dd c0 = two_sum(cj.h, pc.h);
+  const double cl = c0.l + (pc.l + cj.l + cj.h * C - sj.h * sr_l - sj.l * rh);
+  const double s = s0.h + sl, c = c0.h + cl;
+  const double ls = sl - (s - s0.h), lc = cl - (c - c0.h);
+  if (rounds_same(s, ls, fabs(s) * 0x1p-62) && rounds_same(c, lc, fabs(c) * 0x1p-62)) {
+    *sp = fabs(x) < 0x1p-26 ? x : s;
+    *cp = c;
+    return;
+  }
+  dd sd, cd;
+  sincos_dd(x, sd, cd);
+  *sp = fabs(x) < 0x1p-26 ? x : sd.h + sd.l;
+  *cp = cd.h + cd.l;
+}
+
 CR_HD double sin(double x) {
-  if (!(fabs(x) < 0x1p14)) return ::sin(x);
-  if (fabs(x) < 0x1p-26) return x;  // |sin x - x| < |x|^3 / 6: below half an ulp
-  dd s, c;
-  sincos_dd(x, s, c);
-  return s.h + s.l;
+  double s, c;
+  sincos(x, &s, &c);
+  return s;
 }
 CR_HD double cos(double x) {
-  if (!(fabs(x) < 0x1p14)) return ::cos(x);
-  dd s, c;
-  sincos_dd(x, s, c);
-  return c.h + c.l;
+  double s, c;
+  sincos(x, &s, &c);
+  return c;
 }
 CR_HD double tan(double x) {
   if (!(fabs(x) < 0x1p14)) return ::tan(x);
@@ -148,17 +242,6 @@ CR_HD double tan(double x) {
   sincos_dd(x, s, c);
   const dd t = div(s, c);
   return t.h + t.l;
-}
-CR_HD void sincos(double x, double* sp, double* cp) {
-  if (!(fabs(x) < 0x1p14)) {
-    *sp = ::sin(x);
-    *cp = ::cos(x);
-    return;
-  }
-  dd s, c;
-  sincos_dd(x, s, c);
-  *sp = fabs(x) < 0x1p-26 ? x : s.h + s.l;
-  *cp = c.h + c.l;
 }
 
 }  // namespace crm

@@ -14,8 +14,8 @@
 #ifndef AF_CRMATH
 #define AF_CRMATH 1
 #endif
-#if AF_CRMATH
 #include "cr_math.h"
+#if AF_CRMATH
 #define AF_ATAN crm::atan
 #define AF_SIN crm::sin
 #define AF_COS crm::cos

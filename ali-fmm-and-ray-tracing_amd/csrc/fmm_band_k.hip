@@ -37,6 +37,7 @@
 // Cross-CU data (flags, rim lists, edge buffers) is stored with sc1 stores, drained (vmcnt 0) by
 // every wave before the flag, and read with sc1 loads after the flag (MI355X_MICROARCH.md
 // "inter-workgroup visibility", Valid forms).  Flags and rim lists are double-buffered by parity.
+#define CR_LDS_TABLES  // cr_math.h tables in LDS (crm::lds_init at kernel start)
 #include <type_traits>
 #include "kernels.h"
 #include "local_ops.h"
@@ -203,6 +204,7 @@ __global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
   int* S = B->S;
   int* own = B->own;
   DevModel M = P.M;
+  crm::lds_init();
   if (LDSMAT) {
     for (int k = tid; k < 5 * M.nstab; k += kThreads) sh->stab[k] = M.stab[k];
     for (int k = tid; k < 361 * M.ncol; k += kThreads) sh->ptab[k] = M.ptab[k];

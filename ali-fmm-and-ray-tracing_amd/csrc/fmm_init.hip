@@ -10,6 +10,7 @@
 // clear LDS, fill the straight-ray footprint and decimate between stages.  Output: the decimated
 // stage-3 nodes that the band kernel hands over to the main grid (:2006-2040), as (cell, ttn,
 // class) triples.
+#define CR_LDS_TABLES  // cr_math.h tables in LDS (crm::lds_init at kernel start)
 #include "device_common.h"
 #include "local_ops.h"
 #include "kernels.h"
@@ -396,6 +397,7 @@ __global__ __launch_bounds__(128) void fmm_init_kernel(DevModel M, InitJob* jobs
   __shared__ InitLds lds;
   InitLds* L = &lds;
   const int src = blockIdx.x;
+  crm::lds_init();
   if (LDSMAT)
     for (int k = threadIdx.x; k < M.nmat; k += blockDim.x) L->mat[k] = M.mtab[k];
   if (src >= njobs) return;
