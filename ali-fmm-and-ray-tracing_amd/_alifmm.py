@@ -70,6 +70,7 @@ def _load():
             "alifmm_source_stats": (_i, [_p, _i, _p, _p]),
             "alifmm_last_timing": (_i, [_p, _p, _p, _p]),
             "alifmm_band_profile": (_i, [_p, _i, _p]),
+            "alifmm_init_profile": (_i, [_p, _i, _p]),
             "alifmm_put_field": (_i, [_p, _i, _i, _p]),
             "alifmm_time_between_points": (_i, [_p, _i, _p, _p, _p, _p, _i, _p]),
             "alifmm_local_ops": (_i, [_p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i,
@@ -285,6 +286,14 @@ class Context:
     def band_profile(self, slot):
         out = np.zeros(14, dtype=np.int64)
         self._chk(lib().alifmm_band_profile(self._h, int(slot), _ptr(out)), "band_profile")
+        return out
+
+    def init_profile(self, i):
+        """Source-init profile of source i of the last chunk: ticks (100 MHz) of stage 1/2/3 and the
+        exact prefix, their pops, relax-role busy ticks, relaxations | fallbacks << 32
+        (alifmm_init_profile)."""
+        out = np.zeros(16, dtype=np.int64)
+        self._chk(lib().alifmm_init_profile(self._h, int(i), _ptr(out)), "init_profile")
         return out
 
     def last_timing(self):

@@ -860,6 +860,14 @@ int alifmm_band_profile(alifmm_ctx* ctx, int slot, int64_t* out14) {
   return ALIFMM_OK;
 }
 
+int alifmm_init_profile(alifmm_ctx* ctx, int i, int64_t* out16) {
+  if (!ctx || !out16 || i < 0 || i >= ctx->arena.nsrc || !ctx->arena.ho)
+    return fail(ctx, ALIFMM_E_ARG, "init_profile: bad index");
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(hipMemcpy(out16, &ctx->arena.ho[i].prof[0], 16 * sizeof(long long), hipMemcpyDeviceToHost));
+  return ALIFMM_OK;
+}
+
 int alifmm_last_timing(alifmm_ctx* ctx, double* init_ms, double* band_ms, double* total_ms) {
   if (!ctx) return ALIFMM_E_ARG;
   if (init_ms) *init_ms = ctx->t_init;

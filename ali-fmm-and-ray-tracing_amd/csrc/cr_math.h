@@ -18,8 +18,12 @@
 
 #if defined(__HIPCC__)
 #define CR_HD __host__ __device__ inline
+// the double-double paths (~1 argument in 2^9); inlined: an out-of-line call costs the callers
+// spills across it (measured slower in the band and init kernels)
+#define CR_COLD __host__ __device__ inline
 #else
 #define CR_HD inline
+#define CR_COLD inline
 #endif
 #define CR_TABLE static constexpr
 #define CR_CONST static constexpr
@@ -91,7 +95,7 @@ CR_HD dd atan_small(dd t) {
   return add(t, mul(t, P));
 }
 
-CR_HD double atan_accurate(double x) {
+CR_COLD double atan_accurate(double x) {
   const double a = fabs(x);
   const bool inv = a > 1.0;
   dd u{a, 0.0};
@@ -112,7 +116,7 @@ CR_HD double atan_accurate(double x) {
 }
 
 // sin and cos of x as double-doubles (|x| < 2^14)
-CR_HD void sincos_dd(double x, dd& s, dd& c) {
+CR_COLD void sincos_dd(double x, dd& s, dd& c) {
   const double jd = nearbyint(x * k128OverPi);
   const int j = (int)jd;
   // r = x - j pi/128: j kP1 exact (33-bit kP1, |j| < 2^20), x - j kP1 exact (Sterbenz)

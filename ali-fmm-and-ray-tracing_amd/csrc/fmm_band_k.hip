@@ -140,6 +140,23 @@ struct Win5 {
   AF_DEV double tt(long z, long x) const { return t[(z - iz + 2) * 5 + (x - ix + 2)]; }
 };
 
+// fouds18_A() on a staged window, out of line: the fallback runs for a few per cent of the cells,
+// and one shared copy keeps its ~30 KB of code out of the step loop's instruction-cache working set
+#ifndef AF_F18_OUTLINE
+#define AF_F18_OUTLINE 0
+#endif
+#if AF_F18_OUTLINE
+#define AF_F18_ATTR __attribute__((noinline))
+#else
+#define AF_F18_ATTR __forceinline__
+#endif
+template <bool PRE_ONLY>
+__device__ AF_F18_ATTR double fouds18_w5(const Win5& F, const DevModel& M, const CellMat& cm, int z,
+                                                      int x, double dnx, double dnz, int nx, int nz,
+                                                      const double* pre) {
+  return fouds18<PRE_ONLY>(F, M, cm, z, x, dnx, dnz, nx, nz, pre);
+}
+
 // X1 read side (wave 0): lane l polls word l & 3 of member l >> 2 (K <= kMaxK = 16 members, one
 // word per lane) until every member's words carry this step's tag, then the wave reduces them:
 // global Tmin, live close cells (sum), error (or), and the neighbour members' rim-list lengths.
@@ -714,8 +731,7 @@ __global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
             const CellMat cm = band_mat<LDSMAT>(M, sh->mat, sh->stab, R.mv, z, x);
             const double dnx_f = launder_u(R.dnx), dnz_f = launder_u(R.dnz);
             double v;
-            if constexpr (LDSMAT) v = fouds18<true>(F, M, cm, z, x, dnx_f, dnz_f, nx, nz, mat_slo(M, R.mv, z, x));
-            else v = fouds18<false>(F, M, cm, z, x, dnx_f, dnz_f, nx, nz, mat_slo(M, R.mv, z, x));
+            v = fouds18_w5<LDSMAT>(F, M, cm, z, x, dnx_f, dnz_f, nx, nz, mat_slo(M, R.mv, z, x));
             VL.put(e, v);
           }
         }

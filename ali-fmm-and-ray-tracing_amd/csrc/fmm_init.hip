@@ -19,9 +19,12 @@
 namespace af {
 
 constexpr int kInitMaxN = 109 * 109;  // largest stage grid (stage 1 / 2)
-constexpr int kInitHeap = 2048;       // heap slots (the stage fronts stay below ~500 nodes)
+constexpr int kInitHeap = 1024;       // heap slots (the stage fronts stay below ~500 nodes)
 constexpr int kInitMat = 256;         // material records staged in LDS (DevModel::mtab)
 constexpr int kInitDec = 37 * 37;     // decimated stage-1/2 grid
+constexpr int kInitWin = 53 * 53;     // coarse cells under a stage grid / the prefix window
+constexpr int kInitStab = 64;         // stiffness rows staged in LDS
+constexpr int kInitPtab = 361 * 2;    // phase table staged in LDS (ncol <= 2)
 
 struct InitLds {
   double T[kInitMaxN];
@@ -29,12 +32,17 @@ struct InitLds {
   short S[kInitMaxN];
   double hkey[kInitHeap];          // heap keys: ttn of the node (kept equal to it by add/upd)
   MatRec mat[kInitMat];
+  double stab[5 * kInitStab];       // DevModel::stab (nstab <= kInitStab)
+  double ptab[kInitPtab];           // DevModel::ptab (ncol <= 2)
   unsigned short hcell[kInitHeap];  // heap nodes (z << 8) | x
+  unsigned char smid[kInitWin];     // material ids of the coarse cells under the current grid
   signed char decC[kInitDec];       // 0 far, 1 known inner, 2 known outer, 3 close
   // heap role -> relax role hand-off of one pop's neighbours (two-wavefront heap walk)
   int cmd, done;                    // sequence numbers (cmd -1: stop)
   int njob;
   int jz[4], jx[4], jkind[4];       // kind: 1 add (far), 2 upd (close), +4: stage-1 quirk nnz
+  long long rbusy;                  // profile: relax-role ticks of the current walk
+  long long rjobs;                  // profile: relaxations | fouds18_A() fallbacks << 32
 };
 
 struct LdsField {
@@ -58,6 +66,7 @@ struct Heap {
   int ntr;
   int err;
   int ndup = 0;
+  int pops = 0;
   unsigned short dup[kInitDup];
   AF_DEV int bz(int k) const { return L->hcell[k] >> 8; }
   AF_DEV int bx(int k) const { return L->hcell[k] & 255; }
@@ -147,16 +156,42 @@ struct Heap {
   }
 };
 
-// material of a node: one id load + the LDS record (LDSMAT), else the model arrays
+// coarse cells under the current grid: rows cz0.., columns cx0.. (w per row); their material
+// ids are in InitLds::smid (LDSMAT)
+struct MidWin {
+  int cz0, cx0, w, h;
+};
+
+// all lanes: the material ids of window W into LDS
+AF_DEV void load_smid(const DevModel& M, InitLds* L, const MidWin& W, int lane, int nl) {
+  for (int k = lane; k < W.w * W.h; k += nl) {
+    const long c = (long)(W.cz0 + k / W.w) * M.nx0 + W.cx0 + k % W.w;
+    L->smid[k] = M.mid8 ? gld(M.mid8 + c) : (unsigned char)gld(M.mid + c);
+  }
+}
+
+// material of a node: the LDS id + the LDS record (LDSMAT), else the model arrays; *pre: the
+// material's fouds18_A() slownesses (DevModel::mslo) or null
 template <bool LDSMAT>
-AF_DEV CellMat init_mat(const DevModel& M, const InitLds* L, const MatView& v, int z, int x) {
-  if (!LDSMAT) return cell_mat(M, v, z, x);
-  const MatRec m = L->mat[gld(M.mid + mv_cell(M, v, z, x))];
+AF_DEV CellMat init_mat(const DevModel& M, const InitLds* L, const MatView& v, const MidWin& W, int z, int x,
+                        const double** pre) {
+  if (!LDSMAT) {
+    *pre = nullptr;
+    return cell_mat(M, v, z, x);
+  }
+  const int fz = v.lo1z + (z + v.side1z) / v.s1z, fx = v.lo1x + (x + v.side1x) / v.s1x;
+  const int cz = v.lo2z + (fz + v.side2) / v.s2, cx = v.lo2x + (fx + v.side2) / v.s2;
+  // W.w == 0: the window is larger than InitLds::smid (exact_r > 20), ids from the model
+  const long gc = (long)cz * M.nx0 + cx;
+  const int id = W.w ? (int)L->smid[(cz - W.cz0) * W.w + (cx - W.cx0)]
+                     : (M.mid8 ? (int)gld(M.mid8 + gc) : gld(M.mid + gc));
+  const MatRec m = L->mat[id];
   CellMat r;
   r.velpn = m.velpn;
   r.veln = v.quant ? (double)(int)m.veln : m.veln;
   r.vm = v.quant ? (double)(float)m.vm : m.vm;
   r.stif = m.sidx >= 0 ? M.stab + 5 * m.sidx : nullptr;
+  *pre = M.mslo ? M.mslo + 8 * id + 4 * (v.quant ? 1 : 0) : nullptr;
   return r;
 }
 
@@ -164,19 +199,50 @@ struct StageCfg {
   double dnx;
   int isx, isz, max_dist, quirk;
   MatView mv;
+  MidWin mw;
 };
+
+// field accessor of the exact main-loop prefix: main-grid coordinates, LDS window storage;
+// nodes outside the window have never been touched (far: nsts -1, ttn 0)
+struct WinField {
+  const double* T;
+  const short* S;
+  int wz0, wx0, wz1, wx1, ww;
+  AF_DEV int st(long z, long x) const {
+    return (z < wz0 || z > wz1 || x < wx0 || x > wx1) ? -1 : (int)S[(z - wz0) * ww + (x - wx0)];
+  }
+  AF_DEV double tt(long z, long x) const {
+    return (z < wz0 || z > wz1 || x < wx0 || x > wx1) ? 0.0 : T[(z - wz0) * ww + (x - wx0)];
+  }
+};
+
+// update() then fouds18_A() (:1635-1638) on an LDS neighbourhood, for the stage walks and the prefix
+AF_DEV double fouds18_win(const WinField& F, const DevModel& M, const CellMat& cm, int iz, int ix, double dnx,
+                          double dnz, int nnx, int nnz, const double* pre) {
+  return fouds18(F, M, cm, iz, ix, dnx, dnz, nnx, nnz, pre);
+}
+
+AF_DEV double eval_node(const double* T, const short* S, int z0, int x0, int z1, int x1, int w, const DevModel& M,
+                        const CellMat& cm, int iz, int ix, double dnx, double dnz, int nnz_upd, int nnz, int nnx,
+                        const double* pre, long long* nf18) {
+  NbFieldT nb;
+  nb.load_lds(T, S, z0, x0, z1, x1, w, iz, ix);
+  double v = update(nb, M, cm, iz, ix, dnx, nnz_upd, nnx);
+  if (v == -1.0) {
+    const WinField F{T, S, z0, x0, z1, x1, w};
+    v = fouds18_win(F, M, cm, iz, ix, dnx, dnz, nnx, nnz, pre);
+    *nf18 += 1;
+  }
+  return v;
+}
 
 // relax one neighbour: update() then fouds18_A() (:1635-1638)
 AF_DEV void relax(InitLds* L, const DevModel& M, const StageCfg& c, int nz, int nx, int iz, int ix, int quirk,
-                  const CellMat& cm) {
-  LdsField F{L->T, L->S, nz, nx};
-  // register copy of the neighbourhood; rows past nz read as nsts -1 (the padded reads of the
-  // stage-1 quirk nnz = nnx1, :1645); update() bounds-checks every other position itself
-  NbFieldT nb;
-  nb.load_lds(L->T, L->S, 0, 0, nz - 1, nx - 1, nx, iz, ix);
-  double v = update(nb, M, cm, iz, ix, c.dnx, quirk ? nx : nz, nx);
-  if (v == -1.0) v = fouds18(F, M, cm, iz, ix, c.dnx, c.dnx, nx, nz);
-  L->T[iz * nx + ix] = v;
+                  const CellMat& cm, const double* pre, long long* nf18) {
+  // rows past nz read as nsts -1 (the padded reads of the stage-1 quirk nnz = nnx1, :1645);
+  // update() bounds-checks every other position itself
+  L->T[iz * nx + ix] =
+      eval_node(L->T, L->S, 0, 0, nz - 1, nx - 1, nx, M, cm, iz, ix, c.dnx, c.dnx, quirk ? nx : nz, nz, nx, pre, nf18);
 }
 
 // Two-wavefront heap walk.  The reference relaxes a popped node's neighbours after downtree, and
@@ -189,15 +255,23 @@ AF_DEV void relax(InitLds* L, const DevModel& M, const StageCfg& c, int nz, int 
 // Same results as the one-lane walk, with downtree off the critical path.
 constexpr int kJobAdd = 1, kJobUpd = 2, kJobQuirk = 4;
 AF_DEV void post(int* w, int v) { __hip_atomic_store(w, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP); }
+// the waiting role backs off between polls (s_sleep) so that it does not take issue slots and
+// LDS cycles from the working one
+#ifndef AF_INIT_SLEEP
+#define AF_INIT_SLEEP 1
+#endif
 AF_DEV bool await_value(int* w, int v) {  // false: timeout (the other role is gone)
-  for (long spins = 0; __hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != v; spins++)
+  for (long spins = 0; __hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != v; spins++) {
+    if (AF_INIT_SLEEP) __builtin_amdgcn_s_sleep(AF_INIT_SLEEP);
     if (spins > (1L << 28)) return false;
+  }
   return true;
 }
 AF_DEV int await_change(int* w, int last) {  // the next value != last, or -2 on timeout
   for (long spins = 0;; spins++) {
     const int v = __hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (v != last) return v;
+    if (AF_INIT_SLEEP) __builtin_amdgcn_s_sleep(AF_INIT_SLEEP);
     if (spins > (1L << 28)) return -2;
   }
 }
@@ -206,6 +280,7 @@ AF_DEV int await_change(int* w, int last) {  // the next value != last, or -2 on
 // neighbours' addtree / updtree in order.  false: the relax role timed out
 AF_DEV bool pop_two_role(Heap& h, int& seq, int n) {
   InitLds* L = h.L;
+  h.pops++;
   if (n == 0) {  // nothing to relax
     h.down();
     return true;
@@ -267,17 +342,25 @@ AF_DEV void stage_loop(Heap& h, const DevModel& M, const StageCfg& c, int tid) {
     post(&L->cmd, -1);
   } else if (tid == 64) {
     int last = 0;
+    long long busy = 0, njobs = 0, nf18 = 0;
     while (true) {
       const int cmd = await_change(&L->cmd, last);
       if (cmd < 0) break;  // stop (or timeout: the heap role is gone)
       last = cmd;
+      const long long t0 = wall_clock64();
       for (int k = 0; k < L->njob; k++) {
         const int z = L->jz[k], x = L->jx[k], kind = L->jkind[k];
-        relax(L, M, c, nz, nx, z, x, (kind & kJobQuirk) ? 1 : 0, init_mat<LDSMAT>(M, L, c.mv, z, x));
+        const double* pre;
+        const CellMat cm = init_mat<LDSMAT>(M, L, c.mv, c.mw, z, x, &pre);
+        relax(L, M, c, nz, nx, z, x, (kind & kJobQuirk) ? 1 : 0, cm, pre, &nf18);
+        njobs++;
         if (kind & kJobAdd) L->S[z * nx + x] = 1;  // valid for the next relaxations (addtree sets the index)
       }
+      busy += wall_clock64() - t0;
       post(&L->done, cmd);
     }
+    L->rbusy = busy;
+    L->rjobs = njobs | (nf18 << 32);
   }
 }
 
@@ -311,23 +394,11 @@ AF_DEV void clear_grid(InitLds* L, int n, int lane, int nl) {
   }
 }
 
-// field accessor of the exact main-loop prefix: main-grid coordinates, LDS window storage;
-// nodes outside the window have never been touched (far: nsts -1, ttn 0)
-struct WinField {
-  const double* T;
-  const short* S;
-  int wz0, wx0, wz1, wx1, ww;
-  AF_DEV int st(long z, long x) const {
-    return (z < wz0 || z > wz1 || x < wx0 || x > wx1) ? -1 : (int)S[(z - wz0) * ww + (x - wx0)];
-  }
-  AF_DEV double tt(long z, long x) const {
-    return (z < wz0 || z > wz1 || x < wx0 || x > wx1) ? 0.0 : T[(z - wz0) * ww + (x - wx0)];
-  }
-};
 
 // main loop :2055-2102 on the LDS window (heap in window-local coordinates), two roles as above
 template <bool LDSMAT>
-AF_DEV void main_prefix(Heap& h, const DevModel& M, const InitJob& J, int wz0, int wx0, int wz1, int wx1, int tid) {
+AF_DEV void main_prefix(Heap& h, const DevModel& M, const InitJob& J, int wz0, int wx0, int wz1, int wx1,
+                        const MidWin& pw, int tid) {
   InitLds* L = h.L;
   const int ww = h.nx;
   const int nnz = M.nz0, nnx = M.nx0;
@@ -371,35 +442,51 @@ AF_DEV void main_prefix(Heap& h, const DevModel& M, const InitJob& J, int wz0, i
     }
     post(&L->cmd, -1);
   } else if (tid == 64) {
-    const WinField F{L->T, L->S, wz0, wx0, wz1, wx1, ww};
     int last = 0;
+    long long busy = 0, njobs = 0, nf18 = 0;
     while (true) {
       const int cmd = await_change(&L->cmd, last);
       if (cmd < 0) break;
       last = cmd;
+      const long long t0 = wall_clock64();
       for (int k = 0; k < L->njob; k++) {
         const int lz = L->jz[k], lx = L->jx[k], iz = lz + wz0, ix = lx + wx0;
-        const CellMat cm = init_mat<LDSMAT>(M, L, ident, iz, ix);
-        NbFieldT nb;
-        nb.load_lds(L->T, L->S, wz0, wx0, wz1, wx1, ww, iz, ix);
-        double v = update(nb, M, cm, iz, ix, J.dnx, nnz, nnx);
-        if (v == -1.0) v = fouds18(F, M, cm, iz, ix, J.dnx, J.dnz, nnx, nnz);
+        const double* pre;
+        const CellMat cm = init_mat<LDSMAT>(M, L, ident, pw, iz, ix, &pre);
+        const double v =
+            eval_node(L->T, L->S, wz0, wx0, wz1, wx1, ww, M, cm, iz, ix, J.dnx, J.dnz, nnz, nnz, nnx, pre, &nf18);
+        njobs++;
         L->T[lz * ww + lx] = v;
         if (L->jkind[k] & kJobAdd) L->S[lz * ww + lx] = 1;
       }
+      busy += wall_clock64() - t0;
       post(&L->done, cmd);
     }
+    L->rbusy = busy;
+    L->rjobs = njobs | (nf18 << 32);
   }
 }
 
 template <bool LDSMAT>
-__global__ __launch_bounds__(128) void fmm_init_kernel(DevModel M, InitJob* jobs, int njobs, HandoverOut* out) {
+__global__ __launch_bounds__(128) void fmm_init_kernel(DevModel M0, InitJob* jobs, int njobs, HandoverOut* out) {
   __shared__ InitLds lds;
   InitLds* L = &lds;
   const int src = blockIdx.x;
   crm::lds_init();
-  if (LDSMAT)
+  if (src < njobs && threadIdx.x < 16) out[src].prof[threadIdx.x] = 0;
+  DevModel M = M0;
+  if (LDSMAT) {
     for (int k = threadIdx.x; k < M.nmat; k += blockDim.x) L->mat[k] = M.mtab[k];
+    // the small tables the relaxations read: LDS instead of dependent global loads
+    if (M.stab && M.nstab <= kInitStab) {
+      for (int k = threadIdx.x; k < 5 * M.nstab; k += blockDim.x) L->stab[k] = M.stab[k];
+      M.stab = L->stab;
+    }
+    if (361 * M.ncol <= kInitPtab) {
+      for (int k = threadIdx.x; k < 361 * M.ncol; k += blockDim.x) L->ptab[k] = M.ptab[k];
+      M.ptab = L->ptab;
+    }
+  }
   if (src >= njobs) return;
   const int lane = threadIdx.x, nl = blockDim.x;
   InitJob J = jobs[src];
@@ -423,7 +510,9 @@ __global__ __launch_bounds__(128) void fmm_init_kernel(DevModel M, InitJob* jobs
     c.max_dist = sg * size;
     c.quirk = stg == 0;
     c.mv = MatView{sg, (sg - 1) / 2, bottom, sg, (sg - 1) / 2, left, 1, 0, 0, 0, 1};
+    c.mw = MidWin{bottom, left, right - left + 1, top - bottom + 1};
     clear_grid(L, nz * nx, lane, nl);
+    if (LDSMAT) load_smid(M, L, c.mw, lane, nl);
     __syncthreads();
     Heap h{L, nz, nx, 0, 0};
     if (stg == 0) {
@@ -475,9 +564,18 @@ __global__ __launch_bounds__(128) void fmm_init_kernel(DevModel M, InitJob* jobs
       L->done = 0;
     }
     __syncthreads();
+    const long long ts = wall_clock64();
     stage_loop<LDSMAT>(h, M, c, lane);
-    if (lane == 0) err |= h.err;
+    if (lane == 0) {
+      err |= h.err;
+      O->prof[stg] = wall_clock64() - ts;
+      O->prof[4 + stg] = h.pops;
+    }
     __syncthreads();
+    if (lane == 0) {
+      O->prof[8 + stg] = L->rbusy;
+      O->prof[12 + stg] = L->rjobs;
+    }
     decimate(L, nz, nx, lane, nl);
     __syncthreads();
     pisz = isz_s;
@@ -499,6 +597,8 @@ __global__ __launch_bounds__(128) void fmm_init_kernel(DevModel M, InitJob* jobs
       err = 1;
     } else {
       clear_grid(L, wh * ww, lane, nl);
+      const MidWin pw = wh * ww <= kInitWin ? MidWin{wz0, wx0, ww, wh} : MidWin{0, 0, 0, 0};
+      if (LDSMAT && pw.w) load_smid(M, L, pw, lane, nl);
       __syncthreads();
       Heap h{L, wh, ww, 0, 0};
       if (lane == 0) {
@@ -515,9 +615,18 @@ __global__ __launch_bounds__(128) void fmm_init_kernel(DevModel M, InitJob* jobs
         L->done = 0;
       }
       __syncthreads();
-      main_prefix<LDSMAT>(h, M, J, wz0, wx0, wz1, wx1, lane);
-      if (lane == 0) err |= h.err;
+      const long long ts = wall_clock64();
+      main_prefix<LDSMAT>(h, M, J, wz0, wx0, wz1, wx1, pw, lane);
+      if (lane == 0) {
+        err |= h.err;
+        O->prof[3] = wall_clock64() - ts;
+        O->prof[7] = h.pops;
+      }
       __syncthreads();
+      if (lane == 0) {
+        O->prof[11] = L->rbusy;
+        O->prof[15] = L->rjobs;
+      }
       // emit every touched window node: known (1) / close (3)
       if (lane == 0) {
         int n = 0;

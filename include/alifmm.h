@@ -115,6 +115,10 @@ int alifmm_last_timing(alifmm_ctx* ctx, double* init_ms, double* band_ms, double
  * evaluated list sizes; out14[9] the largest close set; out14[10..13] thread 0's ticks inside
  * phases: claim [neighbour + dedupe, nsts loads, list pushes], evaluate [neighbourhood loads]. */
 int alifmm_band_profile(alifmm_ctx* ctx, int slot, int64_t* out14);
+/* Source-init profile of source i of the last travel chunk (subgrid 1): wall-clock ticks
+ * (100 MHz) of stage 1, 2, 3 and the exact main-loop prefix, their heap pops, the ticks the
+ * relaxation role was busy in each, and their relaxations | fouds18_A() fallbacks << 32. */
+int alifmm_init_profile(alifmm_ctx* ctx, int i, int64_t* out16);
 
 /* Upload a host travel-time field (fine grid of `subgrid`) into a slot, e.g. for find_ray() on a
  * field computed elsewhere (find_ray's rec_TTF argument, :3105). */
