@@ -16,8 +16,8 @@ cell-sweep (one evaluation of the local operator, counted by the kernel) over th
 in-library HIP-event time on its stream; traffic = HBM bytes per launch from rocprofv3 PMC
 passes of the same library build (profiles/*_traffic.json), with traffic / algorithmic.
 result_return: after the timed steps, the fields' way back (not in value): D2H into pageable
-host memory through the library's pinned staging ring; for N > 1 also an RCCL gather of every
-rank's fields to rank 0 over xGMI.
+host memory through the library's pinned staging ring, every rank at once; with --gather (N > 1)
+also an RCCL gather of every rank's fields to rank 0 over xGMI.
 cpu_baseline: the CPU restatement of the reference (oracle/, one source per thread) on a bounded
 sample, rank 0, N = 1.
 """
@@ -54,6 +54,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: the CPUs this job is granted (affinity, cgroup quota)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-return", action="store_true", help="skip the result-return measurement")
+    ap.add_argument("--gather", action="store_true", help="N > 1: also time an RCCL gather of all fields to rank 0")
     ap.add_argument("--members", type=int, default=None, help="band-kernel workgroups per source (0: auto)")
     ap.add_argument("--cdelta", type=float, default=None)
     return ap.parse_args()
@@ -229,7 +230,9 @@ def main():
         d2h = sharding.max_over_ranks(time.perf_counter() - t1, dist)
         ret.update({"d2h_ms": d2h * 1e3, "d2h_GBps_per_gpu": gbps, "bytes_per_gpu": int(cells * 8 * ns),
                     "d2h": "pageable host memory through the library's pinned staging ring, every GPU at once"})
-        if world > 1:
+        if world > 1 and "ALIFMM_BENCH_DEVICE" in os.environ:
+            ret["rccl_gather"] = "skipped: every rank on one device (RCCL needs one GPU per rank)"
+        elif world > 1 and args.gather:
             ret.update(sharding.gather_fields(ctx, ns, n, n, rank, world, dev))
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
