@@ -267,6 +267,13 @@ AF_DEV bool await_value(int* w, int v) {  // false: timeout (the other role is g
   }
   return true;
 }
+AF_DEV bool await_at_least(int* w, int v) {  // false: timeout
+  for (long spins = 0; __hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < v; spins++) {
+    if (AF_INIT_SLEEP) __builtin_amdgcn_s_sleep(AF_INIT_SLEEP);
+    if (spins > (1L << 28)) return false;
+  }
+  return true;
+}
 AF_DEV int await_change(int* w, int last) {  // the next value != last, or -2 on timeout
   for (long spins = 0;; spins++) {
     const int v = __hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -276,9 +283,11 @@ AF_DEV int await_change(int* w, int last) {  // the next value != last, or -2 on
   }
 }
 
-// heap role, one pop: hand the classified neighbours to the relax role, downtree, wait, then the
-// neighbours' addtree / updtree in order.  false: the relax role timed out
-AF_DEV bool pop_two_role(Heap& h, int& seq, int n) {
+// heap role, one pop: hand the classified neighbours to the relax role, downtree, then each
+// neighbour's addtree / updtree as soon as its relaxation is done (L->done counts relaxations), so
+// the sift-ups run beside the later neighbours' relaxations (they only move heap indices: the
+// validity the relaxations read stays).  false: the relax role timed out
+AF_DEV bool pop_two_role(Heap& h, int& seq, int& jobs, int n) {
   InitLds* L = h.L;
   h.pops++;
   if (n == 0) {  // nothing to relax
@@ -288,12 +297,13 @@ AF_DEV bool pop_two_role(Heap& h, int& seq, int n) {
   L->njob = n;
   post(&L->cmd, ++seq);
   h.down();
-  if (!await_value(&L->done, seq)) return false;
   for (int k = 0; k < n; k++) {
+    if (!await_at_least(&L->done, jobs + k + 1)) return false;
     if (L->jkind[k] & kJobAdd) h.add(L->jz[k], L->jx[k], true);
     else h.upd(L->jz[k], L->jx[k]);
     if (h.ndup) h.sync(L->jz[k], L->jx[k]);
   }
+  jobs += n;
   return true;
 }
 
@@ -303,7 +313,7 @@ AF_DEV void stage_loop(Heap& h, const DevModel& M, const StageCfg& c, int tid) {
   InitLds* L = h.L;
   const int nz = h.nz, nx = h.nx;
   if (tid == 0) {
-    int seq = 0;
+    int seq = 0, jobs = 0;
     bool finished = false;
     while (h.ntr > 0 && !finished && !h.err) {
       const int ix = h.bx(1), iz = h.bz(1);
@@ -337,7 +347,7 @@ AF_DEV void stage_loop(Heap& h, const DevModel& M, const StageCfg& c, int tid) {
           finished = true;
         }
       }
-      if (!pop_two_role(h, seq, n)) h.err = 1;
+      if (!pop_two_role(h, seq, jobs, n)) h.err = 1;
     }
     post(&L->cmd, -1);
   } else if (tid == 64) {
@@ -348,16 +358,17 @@ AF_DEV void stage_loop(Heap& h, const DevModel& M, const StageCfg& c, int tid) {
       if (cmd < 0) break;  // stop (or timeout: the heap role is gone)
       last = cmd;
       const long long t0 = wall_clock64();
-      for (int k = 0; k < L->njob; k++) {
+      const int nj = L->njob;  // read once: the heap role refills the jobs after the last one is done
+      for (int k = 0; k < nj; k++) {
         const int z = L->jz[k], x = L->jx[k], kind = L->jkind[k];
         const double* pre;
         const CellMat cm = init_mat<LDSMAT>(M, L, c.mv, c.mw, z, x, &pre);
         relax(L, M, c, nz, nx, z, x, (kind & kJobQuirk) ? 1 : 0, cm, pre, &nf18);
         njobs++;
         if (kind & kJobAdd) L->S[z * nx + x] = 1;  // valid for the next relaxations (addtree sets the index)
+        post(&L->done, (int)njobs);
       }
       busy += wall_clock64() - t0;
-      post(&L->done, cmd);
     }
     L->rbusy = busy;
     L->rjobs = njobs | (nf18 << 32);
@@ -404,7 +415,7 @@ AF_DEV void main_prefix(Heap& h, const DevModel& M, const InitJob& J, int wz0, i
   const int nnz = M.nz0, nnx = M.nx0;
   const MatView ident{1, 0, 0, 1, 0, 0, 1, 0, 0, 0, 0};
   if (tid == 0) {
-    int seq = 0;
+    int seq = 0, jobs = 0;
     while (h.ntr > 0 && !h.err) {
       const int lx = h.bx(1), lz = h.bz(1);
       if (L->T[lz * ww + lx] >= J.tstop) break;
@@ -438,7 +449,7 @@ AF_DEV void main_prefix(Heap& h, const DevModel& M, const InitJob& J, int wz0, i
           }
         }
       }
-      if (!pop_two_role(h, seq, n)) h.err = 1;
+      if (!pop_two_role(h, seq, jobs, n)) h.err = 1;
     }
     post(&L->cmd, -1);
   } else if (tid == 64) {
@@ -449,7 +460,8 @@ AF_DEV void main_prefix(Heap& h, const DevModel& M, const InitJob& J, int wz0, i
       if (cmd < 0) break;
       last = cmd;
       const long long t0 = wall_clock64();
-      for (int k = 0; k < L->njob; k++) {
+      const int nj = L->njob;  // read once: the heap role refills the jobs after the last one is done
+      for (int k = 0; k < nj; k++) {
         const int lz = L->jz[k], lx = L->jx[k], iz = lz + wz0, ix = lx + wx0;
         const double* pre;
         const CellMat cm = init_mat<LDSMAT>(M, L, ident, pw, iz, ix, &pre);
@@ -458,9 +470,9 @@ AF_DEV void main_prefix(Heap& h, const DevModel& M, const InitJob& J, int wz0, i
         njobs++;
         L->T[lz * ww + lx] = v;
         if (L->jkind[k] & kJobAdd) L->S[lz * ww + lx] = 1;
+        post(&L->done, (int)njobs);
       }
       busy += wall_clock64() - t0;
-      post(&L->done, cmd);
     }
     L->rbusy = busy;
     L->rjobs = njobs | (nf18 << 32);
