@@ -11,6 +11,15 @@
 // stage-3 nodes that the band kernel hands over to the main grid (:2006-2040), as (cell, ttn,
 // class) triples.
 #define CR_LDS_TABLES  // cr_math.h tables in LDS (crm::lds_init at kernel start)
+#ifdef AF_INIT_UPD_PROF  // diagnostic builds: wall clock between update()'s stencil stage and its finish
+__device__ long long af_upd_mark;
+__device__ long long af_prof_acc[3];  // load, stencil stage, finish (all sources, one lane each)
+#define AF_UPD_HOOK(dep)                                               \
+  do {                                                                 \
+    asm volatile("" ::"v"(dep));                                       \
+    af_upd_mark = wall_clock64();                                      \
+  } while (0)
+#endif
 #include "device_common.h"
 #include "local_ops.h"
 #include "kernels.h"
@@ -225,9 +234,23 @@ AF_DEV double fouds18_win(const WinField& F, const DevModel& M, const CellMat& c
 AF_DEV double eval_node(const double* T, const short* S, int z0, int x0, int z1, int x1, int w, const DevModel& M,
                         const CellMat& cm, int iz, int ix, double dnx, double dnz, int nnz_upd, int nnz, int nnx,
                         const double* pre, long long* nf18) {
+#ifdef AF_INIT_UPD_PROF
+  const long long ta = wall_clock64();
+#endif
   NbFieldT nb;
   nb.load_lds(T, S, z0, x0, z1, x1, w, iz, ix);
+#ifdef AF_INIT_UPD_PROF
+  asm volatile("" ::"v"(nb.t0), "v"(nb.t11), "v"(nb.vm));
+  const long long tb = wall_clock64();
+#endif
   double v = update(nb, M, cm, iz, ix, dnx, nnz_upd, nnx);
+#ifdef AF_INIT_UPD_PROF
+  asm volatile("" ::"v"(v));
+  const long long tc = wall_clock64();
+  af_prof_acc[0] += tb - ta;
+  af_prof_acc[1] += af_upd_mark - tb;
+  af_prof_acc[2] += tc - af_upd_mark;
+#endif
   if (v == -1.0) {
     const WinField F{T, S, z0, x0, z1, x1, w};
     v = fouds18_win(F, M, cm, iz, ix, dnx, dnz, nnx, nnz, pre);
@@ -638,6 +661,13 @@ __global__ __launch_bounds__(128) void fmm_init_kernel(DevModel M0, InitJob* job
       if (lane == 0) {
         O->prof[11] = L->rbusy;
         O->prof[15] = L->rjobs;
+#ifdef AF_INIT_UPD_PROF
+        if (src == 0) {  // diagnostic builds: the accumulators (whole launch so far) replace [8..10]
+          O->prof[8] = af_prof_acc[0];
+          O->prof[9] = af_prof_acc[1];
+          O->prof[10] = af_prof_acc[2];
+        }
+#endif
       }
       // emit every touched window node: known (1) / close (3)
       if (lane == 0) {

@@ -733,6 +733,9 @@ AF_DEV double update_nb(const F& f, const DevModel& M, const CellMat& cm, AF_UPD
     }
     if (sno == -1 || ix == 0 || ix == nnx - 1 || iz == 0 || iz == nnz - 1)
         upd_tri(f, iz, ix, nnz, nnx, sno, min_diff, diff, w, wt, angle, dist);
+#ifdef AF_UPD_HOOK
+    AF_UPD_HOOK(wt + angle + dist);  // profiling builds: the stencil stage is done
+#endif
     return upd_finish(M, cm, ix, iz, w, wt, angle, dist, dnx);
 }
 
