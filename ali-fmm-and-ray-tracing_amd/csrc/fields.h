@@ -45,6 +45,16 @@ struct NbField {
     return k == 0 ? t0 : k == 1 ? t1 : k == 2 ? t2 : k == 3 ? t3 : k == 4 ? t4 : k == 5 ? t5 : k == 6 ? t6
          : k == 7 ? t7 : k == 8 ? t8 : k == 9 ? t9 : k == 10 ? t10 : t11;
   }
+  // the cell at offset (dz, dx) now holds the valid value v (no-op outside the 12 positions)
+  AF_DEV void patch(int dz, int dx, double v) {
+    const int ad = abs(dz) + abs(dx);
+    if (ad == 0 || ad > 2 || (dz != 0 && dx != 0 && (abs(dz) != 1 || abs(dx) != 1))) return;
+    const int k = slot(dz, dx);
+    vm |= 1u << k;
+    t0 = k == 0 ? v : t0; t1 = k == 1 ? v : t1; t2 = k == 2 ? v : t2; t3 = k == 3 ? v : t3;
+    t4 = k == 4 ? v : t4; t5 = k == 5 ? v : t5; t6 = k == 6 ? v : t6; t7 = k == 7 ? v : t7;
+    t8 = k == 8 ? v : t8; t9 = k == 9 ? v : t9; t10 = k == 10 ? v : t10; t11 = k == 11 ? v : t11;
+  }
   AF_DEV void load(const double* T, const int* S, int nz, int nx, int z, int x) {
     iz = z;
     ix = x;
@@ -117,6 +127,16 @@ struct NbFieldT {
     t6 = t[6]; t7 = t[7]; t8 = t[8]; t9 = t[9]; t10 = t[10]; t11 = t[11];
   }
   AF_DEV void load(const double* T, int nz, int nx, int z, int x) { load_t<false>(T, nz, nx, z, x); }
+  // the cell at offset (dz, dx) now holds the valid value v (no-op outside the 12 positions)
+  AF_DEV void patch(int dz, int dx, double v) {
+    const int ad = abs(dz) + abs(dx);
+    if (ad == 0 || ad > 2 || (dz != 0 && dx != 0 && (abs(dz) != 1 || abs(dx) != 1))) return;
+    const int k = NbField::slot(dz, dx);
+    vm |= 1u << k;
+    t0 = k == 0 ? v : t0; t1 = k == 1 ? v : t1; t2 = k == 2 ? v : t2; t3 = k == 3 ? v : t3;
+    t4 = k == 4 ? v : t4; t5 = k == 5 ? v : t5; t6 = k == 6 ? v : t6; t7 = k == 7 ? v : t7;
+    t8 = k == 8 ? v : t8; t9 = k == 9 ? v : t9; t10 = k == 10 ? v : t10; t11 = k == 11 ? v : t11;
+  }
   // As load(), with sc1 loads (cells another workgroup of the launch writes)
   AF_DEV void load_sc1(const double* T, int nz, int nx, int z, int x) { load_t<true>(T, nz, nx, z, x); }
   // From a status-coded grid in LDS (the init kernel's stage grids / prefix window): validity =

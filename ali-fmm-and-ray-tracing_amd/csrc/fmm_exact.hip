@@ -13,6 +13,7 @@
 //
 // Output for the band kernel: main-grid statuses known 0 / close 1 + list slot / far -1 and the
 // close cells in Lin (count in BandSrc::nl0).
+#define CR_LDS_TABLES  // cr_math.h tables in LDS (crm::lds_init at kernel start)
 #include "kernels.h"
 #include "local_ops.h"
 #include "fields.h"
@@ -24,6 +25,8 @@ constexpr int kXHeap = 8192;
 struct XLds {
   double key[kXHeap];
   int cell[kXHeap];
+  UpdSel psel[4];  // parallel relaxation: each neighbour's stencil stage on the pop's state ...
+  double pval[4];  // ... and its value
 };
 
 // addtree / updtree / downtree (:94-237) over a global nsts array, heap slots in LDS.  Keys are
@@ -39,6 +42,7 @@ struct XHeap {
   int err;
   int ndup = 0;
   int dup[kXDup];
+  AF_DEV void setS(int c, int v) { S[c] = v; }
   AF_DEV static int parent(int t) { return (int)rint((double)t / 2.0); }  // half-even (:123)
   AF_DEV void swap(int a, int b) {
     int c = H->cell[a];
@@ -53,8 +57,8 @@ struct XHeap {
     const double tv = H->key[tpc];
     while (tpp > 0) {
       if (tv < H->key[tpp]) {
-        S[c] = tpp;
-        S[H->cell[tpp]] = tpc;
+        setS(c, tpp);
+        setS(H->cell[tpp], tpc);
         swap(tpc, tpp);
         tpc = tpp;
         tpp = parent(tpc);
@@ -63,22 +67,23 @@ struct XHeap {
       }
     }
   }
-  // key = the node's ttn; the relaxation passes the value it has just stored (no reload of T[c])
-  AF_DEV void add(int c, double key) {
+  // key = the node's ttn; the relaxation passes the value it has just stored (no reload of T[c]);
+  // fresh: the node is known to be far (a relaxation of a far neighbour)
+  AF_DEV void add(int c, double key, bool fresh = false) {
     ntr += 1;
     if (ntr >= kXHeap) {
       err = 3;
       ntr = kXHeap - 1;
       return;
     }
-    if (S[c] > 0) {  // already in the heap: a second entry
+    if (!fresh && S[c] > 0) {  // already in the heap: a second entry
       if (ndup == kXDup) {
         err = 3;
         return;
       }
       dup[ndup++] = c;
     }
-    S[c] = ntr;
+    setS(c, ntr);
     H->cell[ntr] = c;
     H->key[ntr] = key;
     sift_up(c, ntr);
@@ -102,7 +107,7 @@ struct XHeap {
       ntr -= 1;
       return;
     }
-    S[H->cell[ntr]] = 1;
+    setS(H->cell[ntr], 1);
     H->cell[1] = H->cell[ntr];
     H->key[1] = H->key[ntr];
     ntr -= 1;
@@ -110,8 +115,8 @@ struct XHeap {
     while (tpc < ntr) {
       if (H->key[tpc] > H->key[tpc + 1]) tpc = tpc + 1;
       if (H->key[tpc] < H->key[tpp]) {
-        S[H->cell[tpp]] = tpc;
-        S[H->cell[tpc]] = tpp;
+        setS(H->cell[tpp], tpc);
+        setS(H->cell[tpc], tpp);
         swap(tpc, tpp);
         tpp = tpc;
         tpc = 2 * tpp;
@@ -121,8 +126,8 @@ struct XHeap {
     }
     if (tpc == ntr) {
       if (H->key[tpc] < H->key[tpp]) {
-        S[H->cell[tpp]] = tpc;
-        S[H->cell[tpc]] = tpp;
+        setS(H->cell[tpp], tpc);
+        setS(H->cell[tpc], tpp);
         swap(tpc, tpp);
       }
     }
@@ -214,6 +219,96 @@ AF_DEV long long xloop(XHeap& h, const DevModel& M, const XGrid& g, bool stage, 
   return pops;
 }
 
+// xloop run by the whole wavefront: lane 0 keeps the heap; the popped node's neighbours are
+// evaluated on lanes 0..3 at once against the pop's state (pass 1), lane k > 0 re-runs its
+// stencil stage with the earlier neighbours' pass-1 values applied (pass 2), and lane 0 commits
+// them in the reference's order, finishing a neighbour itself only when its stencil stage differs
+// (update()'s value is a function of its stencil stage: results are the sequential ones bit for
+// bit).  Returns the pops (lane 0's count).
+AF_DEV long long xloop_par(XHeap& h, const DevModel& M, const XGrid& g, bool stage, int isx_s, int isz_s,
+                           int max_dist, double tstop, XBox* box, int lane) {
+  long long pops = 0;
+  bool finished = false;
+  const int nz = g.nz, nx = g.nx;
+  while (true) {
+    int go = 0, c = 0;
+    if (lane == 0) {
+      go = h.ntr > 0 && !finished && !h.err && !(tstop > 0 && h.H->key[1] >= tstop);
+      c = h.H->cell[1];
+    }
+    go = __shfl(go, 0);
+    if (!go) break;
+    c = __shfl(c, 0);
+    const int iz = c / nx, ix = c - iz * nx;
+    // lane k < 4: neighbour k (x-1, x+1, z-1, z+1), status read before downtree (see xloop)
+    const int kz = lane == 2 ? iz - 1 : lane == 3 ? iz + 1 : iz;
+    const int kx = lane == 0 ? ix - 1 : lane == 1 ? ix + 1 : ix;
+    const bool inb = lane < 4 && (lane < 2 ? (0 <= kx && kx <= nx - 1) : (0 <= kz && kz <= nz - 1));
+    const int st = inb ? g.S[kz * nx + kx] : 0;
+    const bool edge = lane < 4 && !inb && stage && (lane < 2 ? abs(isx_s - kx) : abs(isz_s - kz)) == max_dist + 1;
+    const unsigned long long jm = __ballot(inb && st != 0);
+    if (__ballot(edge) != 0ull) finished = true;
+    int stk[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) stk[k] = __shfl(st, k);
+    const bool job = (jm >> lane) & 1ull;
+    if (lane == 0) {
+      g.S[c] = 0;
+      h.down();
+      pops++;
+    }
+    // pass 1
+    NbField nb;
+    if (job) {
+      const CellMat cm = cell_mat(M, g.mv, kz, kx);
+      nb.load(g.T, g.S, nz, nx, kz, kx);
+      const UpdSel sel = update_nb_select(nb, kz, kx, nz, nx);
+      h.H->psel[lane] = sel;
+      h.H->pval[lane] = update_nb_finish(M, cm, kz, kx, g.dnx, sel);
+    }
+    // pass 2 (on pass 1's neighbourhood, patched)
+    bool ok = true;
+    if (job && (jm & ((1ull << lane) - 1ull))) {
+      for (int j = 0; j < lane; j++) {
+        if ((jm >> j) & 1ull) {
+          const int jz = j == 2 ? iz - 1 : j == 3 ? iz + 1 : iz, jx = j == 0 ? ix - 1 : j == 1 ? ix + 1 : ix;
+          nb.patch(jz - kz, jx - kx, h.H->pval[j]);
+        }
+      }
+      ok = update_nb_select(nb, kz, kx, nz, nx).same(h.H->psel[lane]);
+    }
+    const unsigned long long okm = __ballot(ok);
+    // commit in order (lane 0)
+    if (lane == 0) {
+      bool chain = true;
+      for (int k = 0; k < 4; k++) {
+        if (!((jm >> k) & 1ull)) continue;
+        const int rz = k == 2 ? iz - 1 : k == 3 ? iz + 1 : iz, rx = k == 0 ? ix - 1 : k == 1 ? ix + 1 : ix;
+        const int r = rz * nx + rx;
+        double v = h.H->pval[k];
+        if (!(chain && ((okm >> k) & 1ull))) {
+          NbField nq;
+          nq.load(g.T, g.S, nz, nx, rz, rx);
+          const UpdSel sel = update_nb_select(nq, rz, rx, nz, nx);
+          if (!sel.same(h.H->psel[k])) v = update_nb_finish(M, cell_mat(M, g.mv, rz, rx), rz, rx, g.dnx, sel);
+        }
+        if (v == -1.0) {
+          GField F{g.T, g.S, nz, nx};
+          v = fouds18(F, M, cell_mat(M, g.mv, rz, rx), rz, rx, g.dnx, g.dnz, nx, nz, mat_slo(M, g.mv, rz, rx));
+        }
+        chain = chain && __double_as_longlong(v) == __double_as_longlong(h.H->pval[k]);
+        if (box) box->add(rz, rx);
+        g.T[r] = v;
+        if (stk[k] == -1) h.add(r, v, true);
+        else h.upd(r, g.S[r], v);  // its heap index now (earlier sift-ups may have moved it)
+        if (h.ndup) h.sync(r, v);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the commits before the next pop's loads
+    }
+  }
+  return pops;
+}
+
 // hand-over of every 3rd node of a stage grid into the next grid, in row-major order (:2391-2425,
 // :2725-2759): ttn copied, known nodes stay known, "outer" known nodes and close nodes -> heap
 AF_DEV void xhandover(XHeap& h, const XGrid& s, int isz_s, int isx_s, const XGrid& d, int isz_d, int isx_d,
@@ -249,6 +344,7 @@ AF_DEV void xclear(double* T, int* S, int n) {
 __global__ __launch_bounds__(64) void fmm_exact_kernel(BandParams P) {
   __shared__ XLds lds;
   const int src = blockIdx.x;
+  crm::lds_init();
   if (src >= P.nsrc) return;
   BandSrc* B = P.src + src;
   const int lane = threadIdx.x;
@@ -315,9 +411,13 @@ __global__ __launch_bounds__(64) void fmm_exact_kernel(BandParams P) {
     } else if (lane == 0) {
       xhandover(h, prev, pisz, pisx, g, isz_s, isx_s);
     }
-    if (lane == 0) {
-      B->steps[stg] = xloop(h, M, g, true, isx_s, isz_s, scale * size, 0.0);
-      err = h.err;
+    if (lane == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // grid stores before the walk's loads
+    {
+      const long long pops = xloop_par(h, M, g, true, isx_s, isz_s, scale * size, 0.0, nullptr, lane);
+      if (lane == 0) {
+        B->steps[stg] = pops;
+        err = h.err;
+      }
     }
     err = __shfl(err, 0);
     __syncthreads();
@@ -326,34 +426,42 @@ __global__ __launch_bounds__(64) void fmm_exact_kernel(BandParams P) {
     pisx = isx_s;
   }
   // fine main grid (memset by the host: T 0, S -1): hand-over, then the exact prefix
-  if (lane == 0) {
-    int nl = 0;
-    if (!err) {
-      XGrid g;
-      g.T = B->T;
-      g.S = B->S;
-      g.nz = nnz;
-      g.nx = nnx;
-      g.mv = MatView{sg, sgside, 0, sg, sgside, 0, 1, 0, 0, 0, 1};
-      g.dnx = P.dnx;  // the coarse spacing on the fine grid (:2790; field divided by sg at the end)
-      g.dnz = P.dnz;
-      XHeap h{&lds, g.S, g.T, 0, 0};
-      XBox box;  // what the K-member band kernel copies into its edge buffers
+  {
+    XGrid g;
+    g.T = B->T;
+    g.S = B->S;
+    g.nz = nnz;
+    g.nx = nnx;
+    g.mv = MatView{sg, sgside, 0, sg, sgside, 0, 1, 0, 0, 0, 1};
+    g.dnx = P.dnx;  // the coarse spacing on the fine grid (:2790; field divided by sg at the end)
+    g.dnz = P.dnz;
+    XHeap h{&lds, g.S, g.T, 0, 0};
+    XBox box;  // what the K-member band kernel copies into its edge buffers
+    if (!err && lane == 0) {
       xhandover(h, prev, pisz, pisx, g, (int)isz, (int)isx, &box);
-      B->steps[2] = xloop(h, M, g, false, 0, 0, 0, P.tstop, &box);
-      for (int q = 0; q < 4; q++) B->bbox[q] = box.b[q];
-      err = h.err;
-      // heap -> band close list (statuses: heap index > 0 -> close 1)
-      for (int k = 1; k <= h.ntr && k <= P.capL; k++) {
-        const int c = lds.cell[k];
-        B->S[c] = k;  // close: 1 + close-list slot
-        B->Lin[k - 1] = c;
-      }
-      nl = h.ntr;
-      if (nl > P.capL) err = 2;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    B->nl0 = nl;
-    B->err = err;
+    if (!err) {
+      const long long pops = xloop_par(h, M, g, false, 0, 0, 0, P.tstop, &box, lane);
+      if (lane == 0) B->steps[2] = pops;
+    }
+    if (lane == 0) {
+      int nl = 0;
+      if (!err) {
+        for (int q = 0; q < 4; q++) B->bbox[q] = box.b[q];
+        err = h.err;
+        // heap -> band close list (statuses: heap index > 0 -> close 1)
+        for (int k = 1; k <= h.ntr && k <= P.capL; k++) {
+          const int c = lds.cell[k];
+          B->S[c] = k;  // close: 1 + close-list slot
+          B->Lin[k - 1] = c;
+        }
+        nl = h.ntr;
+        if (nl > P.capL) err = 2;
+      }
+      B->nl0 = nl;
+      B->err = err;
+    }
   }
 }
 

@@ -50,6 +50,8 @@ struct InitLds {
   int cmd, done;                    // sequence numbers (cmd -1: stop)
   int njob;
   int jz[4], jx[4], jkind[4];       // kind: 1 add (far), 2 upd (close), +4: stage-1 quirk nnz
+  UpdSel psel[4];                   // parallel relaxation: each job's stencil stage on the pop's state ...
+  double pval[4];                   // ... and its value
   long long rbusy;                  // profile: relax-role ticks of the current walk
   long long rjobs;                  // profile: relaxations | fouds18_A() fallbacks << 32
 };
@@ -330,7 +332,108 @@ AF_DEV bool pop_two_role(Heap& h, int& seq, int& jobs, int n) {
   return true;
 }
 
-// stage FMM loop (:1620-1674) over the two roles (tid 0: heap, tid 64: relax)
+// The relax role (wavefront 1).  A pop's neighbours are relaxed in order, each seeing the earlier
+// ones' new values (the reference's sequence).  Lane k first evaluates job k against the pop's
+// state (all jobs at once, one SIMD pass); then lane 0 walks the jobs in order: job 0's value
+// stands, and job k > 0 re-runs only update()'s cheap stencil stage on the current state — if it
+// equals lane k's (same stencil, same input values) the value is lane k's, else lane 0 finishes it
+// itself.  update()'s value is a function of its stencil stage's outputs, so the result is the
+// sequential one bit for bit; the expensive finish (wavefront angle, phase velocity) of most
+// later jobs runs beside job 0's.  fouds18_A() (no usable stencil) always runs in sequence.
+struct RelaxWin {
+  int z0, x0, z1, x1, w;  // LDS window: rows z0..z1, columns x0..x1 (stage grids: the whole grid)
+  int oz, ox;             // job coordinates (LDS-local) + (oz, ox) = operator coordinates
+  int nnz, nnx;           // operator bounds
+  double dnx, dnz;
+  int quirk_nnz;          // update()'s nnz for quirk jobs (stage 1: nnx1, :1645)
+};
+
+template <bool LDSMAT>
+AF_DEV void relax_role(InitLds* L, const DevModel& M, const MatView& mv, const MidWin& mw, const RelaxWin& R,
+                       int lane) {
+  int last = 0;
+  long long busy = 0, njobs = 0, nf18 = 0, nref = 0;
+  while (true) {
+    int cmd = 0;
+    if (lane == 0) cmd = await_change(&L->cmd, last);
+    cmd = __shfl(cmd, 0);
+    if (cmd < 0) break;  // stop (or timeout: the heap role is gone)
+    last = cmd;
+    const long long t0 = wall_clock64();
+    const int nj = L->njob;  // read once: the heap role refills the jobs after the last one is done
+    if (lane < nj) {
+      const int lz = L->jz[lane], lx = L->jx[lane], kind = L->jkind[lane];
+      const int iz = lz + R.oz, ix = lx + R.ox;
+      const double* pre;
+      const CellMat cm = init_mat<LDSMAT>(M, L, mv, mw, iz, ix, &pre);
+      NbFieldT nb;
+      nb.load_lds(L->T, L->S, R.z0, R.x0, R.z1, R.x1, R.w, iz, ix);
+      const UpdSel sel = update_nb_select(nb, iz, ix, (kind & kJobQuirk) ? R.quirk_nnz : R.nnz, R.nnx);
+      L->psel[lane] = sel;
+      L->pval[lane] = update_nb_finish(M, cm, iz, ix, R.dnx, sel);
+    }
+#ifdef AF_INIT_UPD_PROF
+    const double pv0 = L->pval[0];
+    asm volatile("" ::"v"(pv0));
+    const long long t1 = wall_clock64();
+    if (lane == 0) af_prof_acc[0] += t1 - t0;
+#endif
+    // pass 2: lane k > 0 re-runs job k's stencil stage on the pop's state with jobs 0..k-1 applied
+    // (their pass-1 values; they become valid) — equal to its pass-1 stencil stage: pass-1 value
+    // stands, provided every earlier job's does (checked in order by lane 0 below)
+    bool ok = true;
+    if (lane > 0 && lane < nj) {
+      const int lz = L->jz[lane], lx = L->jx[lane], kind = L->jkind[lane];
+      const int iz = lz + R.oz, ix = lx + R.ox;
+      NbFieldT nb;
+      nb.load_lds(L->T, L->S, R.z0, R.x0, R.z1, R.x1, R.w, iz, ix);
+      for (int j = 0; j < lane; j++) nb.patch(L->jz[j] - lz, L->jx[j] - lx, L->pval[j]);
+      const UpdSel sel = update_nb_select(nb, iz, ix, (kind & kJobQuirk) ? R.quirk_nnz : R.nnz, R.nnx);
+      ok = sel.same(L->psel[lane]);
+    }
+    const unsigned long long okm = __ballot(ok);
+    if (lane == 0) {
+      bool chain = true;  // every earlier job kept its pass-1 value
+      for (int k = 0; k < nj; k++) {
+        const int lz = L->jz[k], lx = L->jx[k], kind = L->jkind[k];
+        const int iz = lz + R.oz, ix = lx + R.ox;
+        const double* pre;
+        const CellMat cm = init_mat<LDSMAT>(M, L, mv, mw, iz, ix, &pre);
+        double v = L->pval[k];
+        if (k > 0 && !(chain && ((okm >> k) & 1ull))) {
+          NbFieldT nb;
+          nb.load_lds(L->T, L->S, R.z0, R.x0, R.z1, R.x1, R.w, iz, ix);
+          const UpdSel sel = update_nb_select(nb, iz, ix, (kind & kJobQuirk) ? R.quirk_nnz : R.nnz, R.nnx);
+          if (!sel.same(L->psel[k])) {
+            v = update_nb_finish(M, cm, iz, ix, R.dnx, sel);
+            nref++;
+          }
+        }
+        if (v == -1.0) {
+          const WinField F{L->T, L->S, R.z0, R.x0, R.z1, R.x1, R.w};
+          v = fouds18_win(F, M, cm, iz, ix, R.dnx, R.dnz, R.nnx, R.nnz, pre);
+          nf18++;
+        }
+        chain = chain && __double_as_longlong(v) == __double_as_longlong(L->pval[k]);
+        L->T[lz * R.w + lx] = v;
+        njobs++;
+        if (kind & kJobAdd) L->S[lz * R.w + lx] = 1;  // valid for the next relaxations (addtree sets the index)
+        post(&L->done, (int)njobs);
+      }
+#ifdef AF_INIT_UPD_PROF
+      af_prof_acc[1] += wall_clock64() - t1;
+      af_prof_acc[2] += nj;
+#endif
+    }
+    busy += wall_clock64() - t0;
+  }
+  if (lane == 0) {
+    L->rbusy = busy;
+    L->rjobs = njobs | (nref << 24) | (nf18 << 44);
+  }
+}
+
+// stage FMM loop (:1620-1674) over the two roles (tid 0: heap, wavefront 1: relax)
 template <bool LDSMAT>
 AF_DEV void stage_loop(Heap& h, const DevModel& M, const StageCfg& c, int tid) {
   InitLds* L = h.L;
@@ -373,28 +476,8 @@ AF_DEV void stage_loop(Heap& h, const DevModel& M, const StageCfg& c, int tid) {
       if (!pop_two_role(h, seq, jobs, n)) h.err = 1;
     }
     post(&L->cmd, -1);
-  } else if (tid == 64) {
-    int last = 0;
-    long long busy = 0, njobs = 0, nf18 = 0;
-    while (true) {
-      const int cmd = await_change(&L->cmd, last);
-      if (cmd < 0) break;  // stop (or timeout: the heap role is gone)
-      last = cmd;
-      const long long t0 = wall_clock64();
-      const int nj = L->njob;  // read once: the heap role refills the jobs after the last one is done
-      for (int k = 0; k < nj; k++) {
-        const int z = L->jz[k], x = L->jx[k], kind = L->jkind[k];
-        const double* pre;
-        const CellMat cm = init_mat<LDSMAT>(M, L, c.mv, c.mw, z, x, &pre);
-        relax(L, M, c, nz, nx, z, x, (kind & kJobQuirk) ? 1 : 0, cm, pre, &nf18);
-        njobs++;
-        if (kind & kJobAdd) L->S[z * nx + x] = 1;  // valid for the next relaxations (addtree sets the index)
-        post(&L->done, (int)njobs);
-      }
-      busy += wall_clock64() - t0;
-    }
-    L->rbusy = busy;
-    L->rjobs = njobs | (nf18 << 32);
+  } else if (tid >= 64) {
+    relax_role<LDSMAT>(L, M, c.mv, c.mw, RelaxWin{0, 0, nz - 1, nx - 1, nx, 0, 0, nz, nx, c.dnx, c.dnx, nx}, tid - 64);
   }
 }
 
@@ -475,30 +558,9 @@ AF_DEV void main_prefix(Heap& h, const DevModel& M, const InitJob& J, int wz0, i
       if (!pop_two_role(h, seq, jobs, n)) h.err = 1;
     }
     post(&L->cmd, -1);
-  } else if (tid == 64) {
-    int last = 0;
-    long long busy = 0, njobs = 0, nf18 = 0;
-    while (true) {
-      const int cmd = await_change(&L->cmd, last);
-      if (cmd < 0) break;
-      last = cmd;
-      const long long t0 = wall_clock64();
-      const int nj = L->njob;  // read once: the heap role refills the jobs after the last one is done
-      for (int k = 0; k < nj; k++) {
-        const int lz = L->jz[k], lx = L->jx[k], iz = lz + wz0, ix = lx + wx0;
-        const double* pre;
-        const CellMat cm = init_mat<LDSMAT>(M, L, ident, pw, iz, ix, &pre);
-        const double v =
-            eval_node(L->T, L->S, wz0, wx0, wz1, wx1, ww, M, cm, iz, ix, J.dnx, J.dnz, nnz, nnz, nnx, pre, &nf18);
-        njobs++;
-        L->T[lz * ww + lx] = v;
-        if (L->jkind[k] & kJobAdd) L->S[lz * ww + lx] = 1;
-        post(&L->done, (int)njobs);
-      }
-      busy += wall_clock64() - t0;
-    }
-    L->rbusy = busy;
-    L->rjobs = njobs | (nf18 << 32);
+  } else if (tid >= 64) {
+    relax_role<LDSMAT>(L, M, ident, pw, RelaxWin{wz0, wx0, wz1, wx1, ww, wz0, wx0, nnz, nnx, J.dnx, J.dnz, nnz},
+                       tid - 64);
   }
 }
 

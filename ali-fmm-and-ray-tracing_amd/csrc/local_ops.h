@@ -680,9 +680,24 @@ AF_DEV double update_ref(const F& f, const DevModel& M, const CellMat& cm, AF_UP
 // parameters are carried through the selection instead of a 16-way switch, so a wavefront does
 // not serialise over its lanes' stencil cases.  The triangular stage and the velocity are shared
 // with update_ref.  Bit-identical to update_ref (tools/micro/update_bench checksums, GPU tests).
+// update()'s result is upd_finish() of the stencil stage's outputs: two calls whose stencil
+// stages are equal give the same value (the init kernels' parallel relaxation relies on it)
+struct UpdSel {
+    UpdW<AF_UPD_IDX> w;
+    double wt, angle, dist;
+    AF_DEV bool same(const UpdSel& o) const {
+        return w.have == o.w.have && w.x1 == o.w.x1 && w.x2 == o.w.x2 && w.x3 == o.w.x3 && w.z1 == o.w.z1 &&
+               w.z2 == o.w.z2 && w.z3 == o.w.z3 && __double_as_longlong(w.y1) == __double_as_longlong(o.w.y1) &&
+               __double_as_longlong(w.y2) == __double_as_longlong(o.w.y2) &&
+               __double_as_longlong(w.y3) == __double_as_longlong(o.w.y3) &&
+               __double_as_longlong(wt) == __double_as_longlong(o.wt) &&
+               __double_as_longlong(angle) == __double_as_longlong(o.angle) &&
+               __double_as_longlong(dist) == __double_as_longlong(o.dist);
+    }
+};
+
 template <class F>
-AF_DEV double update_nb(const F& f, const DevModel& M, const CellMat& cm, AF_UPD_IDX iz, AF_UPD_IDX ix, double dnx,
-                        AF_UPD_IDX nnz, AF_UPD_IDX nnx) {
+AF_DEV UpdSel update_nb_select(const F& f, AF_UPD_IDX iz, AF_UPD_IDX ix, AF_UPD_IDX nnz, AF_UPD_IDX nnx) {
     using I = AF_UPD_IDX;
     const bool l1 = ix > 0, l2 = ix > 1, r1 = ix < nnx - 1, r2 = ix < nnx - 2;
     const bool u1 = iz > 0, u2 = iz > 1, d1 = iz < nnz - 1, d2 = iz < nnz - 2;
@@ -713,30 +728,41 @@ AF_DEV double update_nb(const F& f, const DevModel& M, const CellMat& cm, AF_UPD
             code = OFF[AP[k]] | (OFF[SA[k]] << 6) | (OFF[SB[k]] << 12);
         }
     }
-    UpdW<I> w{0, 0, 0, 0, 0, 0, 0.0, 0.0, 0.0, false};
-    double wt = 0.0, angle = 0.0, dist = -1.0;
+    UpdSel r{UpdW<I>{0, 0, 0, 0, 0, 0, 0.0, 0.0, 0.0, false}, 0.0, 0.0, -1.0};
     if (sno >= 0) {
         const bool lo = ya < yb;
         const int pa = (code >> 6) & 63, pb = (code >> 12) & 63;
         const int p1 = code & 63, p2 = lo ? pa : pb, p3 = lo ? pb : pa;
-        w.x1 = ix + (p1 & 7) - 2;
-        w.z1 = iz + (p1 >> 3) - 2;
-        w.x2 = ix + (p2 & 7) - 2;
-        w.z2 = iz + (p2 >> 3) - 2;
-        w.x3 = ix + (p3 & 7) - 2;
-        w.z3 = iz + (p3 >> 3) - 2;
-        w.y1 = yap;
-        w.y2 = lo ? ya : yb;
-        w.y3 = lo ? yb : ya;
-        w.have = true;
-        wt = w.y2;
+        r.w.x1 = ix + (p1 & 7) - 2;
+        r.w.z1 = iz + (p1 >> 3) - 2;
+        r.w.x2 = ix + (p2 & 7) - 2;
+        r.w.z2 = iz + (p2 >> 3) - 2;
+        r.w.x3 = ix + (p3 & 7) - 2;
+        r.w.z3 = iz + (p3 >> 3) - 2;
+        r.w.y1 = yap;
+        r.w.y2 = lo ? ya : yb;
+        r.w.y3 = lo ? yb : ya;
+        r.w.have = true;
+        r.wt = r.w.y2;
     }
     if (sno == -1 || ix == 0 || ix == nnx - 1 || iz == 0 || iz == nnz - 1)
-        upd_tri(f, iz, ix, nnz, nnx, sno, min_diff, diff, w, wt, angle, dist);
+        upd_tri(f, iz, ix, nnz, nnx, sno, min_diff, diff, r.w, r.wt, r.angle, r.dist);
+    return r;
+}
+
+AF_DEV double update_nb_finish(const DevModel& M, const CellMat& cm, AF_UPD_IDX iz, AF_UPD_IDX ix, double dnx,
+                               const UpdSel& r) {
+    return upd_finish(M, cm, ix, iz, r.w, r.wt, r.angle, r.dist, dnx);
+}
+
+template <class F>
+AF_DEV double update_nb(const F& f, const DevModel& M, const CellMat& cm, AF_UPD_IDX iz, AF_UPD_IDX ix, double dnx,
+                        AF_UPD_IDX nnz, AF_UPD_IDX nnx) {
+    const UpdSel r = update_nb_select(f, iz, ix, nnz, nnx);
 #ifdef AF_UPD_HOOK
-    AF_UPD_HOOK(wt + angle + dist);  // profiling builds: the stencil stage is done
+    AF_UPD_HOOK(r.wt + r.angle + r.dist);  // profiling builds: the stencil stage is done
 #endif
-    return upd_finish(M, cm, ix, iz, w, wt, angle, dist, dnx);
+    return update_nb_finish(M, cm, iz, ix, dnx, r);
 }
 
 #ifndef AF_UPD_LEAN
