@@ -52,7 +52,13 @@ constexpr int kWaves = kThreads / 64;
 constexpr int kLcap = 2560, kAcap = 1024, kEcap = 1536, kBcap = 512, kDcap = 512, kRcap = 1024;
 constexpr int kHashLog = 13;
 constexpr int kHash = 1 << kHashLog;
-constexpr int kClaimU = 4;        // claim items per lane per pass
+#ifndef AF_CLAIM_U
+#define AF_CLAIM_U 2
+#endif
+#ifndef AF_X1_SLEEP
+#define AF_X1_SLEEP 1
+#endif
+constexpr int kClaimU = AF_CLAIM_U;  // claim items per lane per pass
 constexpr int kHashItems = 6144;  // claim items deduplicated in the LDS hash (more: global stamps)
 constexpr int kStabLds = 64, kPtabLds = 722, kMatLds = 256;
 constexpr int kDirty = (int)0x80000000u;  // close-set slot: committed last step (edge cell)
@@ -173,7 +179,7 @@ AF_DEV bool x1_poll(KX* X, int K, int par, unsigned tag, Lds* sh, int me) {
       ok = (unsigned)(v >> 32) == tag;
     }
     if (__all(ok)) break;
-    __builtin_amdgcn_s_sleep(1);
+    if (AF_X1_SLEEP) __builtin_amdgcn_s_sleep(AF_X1_SLEEP);
     if (++spins > (1L << 25)) return false;
   }
   const unsigned w = (unsigned)v;

@@ -332,6 +332,9 @@ AF_DEV bool pop_two_role(Heap& h, int& seq, int& jobs, int n) {
   return true;
 }
 
+#ifndef AF_INIT_PASS2
+#define AF_INIT_PASS2 1
+#endif
 // The relax role (wavefront 1).  A pop's neighbours are relaxed in order, each seeing the earlier
 // ones' new values (the reference's sequence).  Lane k first evaluates job k against the pop's
 // state (all jobs at once, one SIMD pass); then lane 0 walks the jobs in order: job 0's value
@@ -381,8 +384,9 @@ AF_DEV void relax_role(InitLds* L, const DevModel& M, const MatView& mv, const M
     // pass 2: lane k > 0 re-runs job k's stencil stage on the pop's state with jobs 0..k-1 applied
     // (their pass-1 values; they become valid) — equal to its pass-1 stencil stage: pass-1 value
     // stands, provided every earlier job's does (checked in order by lane 0 below)
-    bool ok = true;
-    if (lane > 0 && lane < nj) {
+    bool ok = !AF_INIT_PASS2 && false;
+    if (AF_INIT_PASS2) ok = true;
+    if (AF_INIT_PASS2 && lane > 0 && lane < nj) {
       const int lz = L->jz[lane], lx = L->jx[lane], kind = L->jkind[lane];
       const int iz = lz + R.oz, ix = lx + R.ox;
       NbFieldT nb;
