@@ -227,48 +227,12 @@ struct WinField {
   }
 };
 
-// update() then fouds18_A() (:1635-1638) on an LDS neighbourhood, for the stage walks and the prefix
+// fouds18_A() (:240-901) on an LDS window: the relaxation's fallback when update() finds no stencil
 AF_DEV double fouds18_win(const WinField& F, const DevModel& M, const CellMat& cm, int iz, int ix, double dnx,
                           double dnz, int nnx, int nnz, const double* pre) {
   return fouds18(F, M, cm, iz, ix, dnx, dnz, nnx, nnz, pre);
 }
 
-AF_DEV double eval_node(const double* T, const short* S, int z0, int x0, int z1, int x1, int w, const DevModel& M,
-                        const CellMat& cm, int iz, int ix, double dnx, double dnz, int nnz_upd, int nnz, int nnx,
-                        const double* pre, long long* nf18) {
-#ifdef AF_INIT_UPD_PROF
-  const long long ta = wall_clock64();
-#endif
-  NbFieldT nb;
-  nb.load_lds(T, S, z0, x0, z1, x1, w, iz, ix);
-#ifdef AF_INIT_UPD_PROF
-  asm volatile("" ::"v"(nb.t0), "v"(nb.t11), "v"(nb.vm));
-  const long long tb = wall_clock64();
-#endif
-  double v = update(nb, M, cm, iz, ix, dnx, nnz_upd, nnx);
-#ifdef AF_INIT_UPD_PROF
-  asm volatile("" ::"v"(v));
-  const long long tc = wall_clock64();
-  af_prof_acc[0] += tb - ta;
-  af_prof_acc[1] += af_upd_mark - tb;
-  af_prof_acc[2] += tc - af_upd_mark;
-#endif
-  if (v == -1.0) {
-    const WinField F{T, S, z0, x0, z1, x1, w};
-    v = fouds18_win(F, M, cm, iz, ix, dnx, dnz, nnx, nnz, pre);
-    *nf18 += 1;
-  }
-  return v;
-}
-
-// relax one neighbour: update() then fouds18_A() (:1635-1638)
-AF_DEV void relax(InitLds* L, const DevModel& M, const StageCfg& c, int nz, int nx, int iz, int ix, int quirk,
-                  const CellMat& cm, const double* pre, long long* nf18) {
-  // rows past nz read as nsts -1 (the padded reads of the stage-1 quirk nnz = nnx1, :1645);
-  // update() bounds-checks every other position itself
-  L->T[iz * nx + ix] =
-      eval_node(L->T, L->S, 0, 0, nz - 1, nx - 1, nx, M, cm, iz, ix, c.dnx, c.dnx, quirk ? nx : nz, nz, nx, pre, nf18);
-}
 
 // Two-wavefront heap walk.  The reference relaxes a popped node's neighbours after downtree, and
 // neither depends on the other: downtree only moves heap entries (keys and the positive heap
