@@ -225,6 +225,9 @@ AF_DEV long long xloop(XHeap& h, const DevModel& M, const XGrid& g, bool stage, 
 // them in the reference's order, finishing a neighbour itself only when its stencil stage differs
 // (update()'s value is a function of its stencil stage: results are the sequential ones bit for
 // bit).  Returns the pops (lane 0's count).
+#ifndef AF_EXACT_PASS2
+#define AF_EXACT_PASS2 1
+#endif
 AF_DEV long long xloop_par(XHeap& h, const DevModel& M, const XGrid& g, bool stage, int isx_s, int isz_s,
                            int max_dist, double tstop, XBox* box, int lane) {
   long long pops = 0;
@@ -267,8 +270,11 @@ AF_DEV long long xloop_par(XHeap& h, const DevModel& M, const XGrid& g, bool sta
       h.H->pval[lane] = update_nb_finish(M, cm, kz, kx, g.dnx, sel);
     }
     // pass 2 (on pass 1's neighbourhood, patched)
-    bool ok = true;
+    bool ok = true;  // the first neighbour's pass-1 value always stands
     if (job && (jm & ((1ull << lane) - 1ull))) {
+      ok = false;
+    }
+    if (AF_EXACT_PASS2 && job && (jm & ((1ull << lane) - 1ull))) {
       for (int j = 0; j < lane; j++) {
         if ((jm >> j) & 1ull) {
           const int jz = j == 2 ? iz - 1 : j == 3 ? iz + 1 : iz, jx = j == 0 ? ix - 1 : j == 1 ? ix + 1 : ix;
