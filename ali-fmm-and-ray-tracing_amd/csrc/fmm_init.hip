@@ -33,7 +33,15 @@ constexpr int kInitMat = 256;         // material records staged in LDS (DevMode
 constexpr int kInitDec = 37 * 37;     // decimated stage-1/2 grid
 constexpr int kInitWin = 53 * 53;     // coarse cells under a stage grid / the prefix window
 constexpr int kInitStab = 64;         // stiffness rows staged in LDS
-constexpr int kInitPtab = 361 * 2;    // phase table staged in LDS (ncol <= 2)
+constexpr int kSpec = 64;             // speculative relaxations kept by the relax role (one per lane)
+
+// a relaxation evaluated ahead of its turn: the node (z << 8 | x, -1: empty), update()'s stencil
+// stage on the state it saw, and the value
+struct SpecEnt {
+  int cell;
+  double val;
+  UpdSel sel;
+};
 
 struct InitLds {
   double T[kInitMaxN];
@@ -42,7 +50,6 @@ struct InitLds {
   double hkey[kInitHeap];          // heap keys: ttn of the node (kept equal to it by add/upd)
   MatRec mat[kInitMat];
   double stab[5 * kInitStab];       // DevModel::stab (nstab <= kInitStab)
-  double ptab[kInitPtab];           // DevModel::ptab (ncol <= 2)
   unsigned short hcell[kInitHeap];  // heap nodes (z << 8) | x
   unsigned char smid[kInitWin];     // material ids of the coarse cells under the current grid
   signed char decC[kInitDec];       // 0 far, 1 known inner, 2 known outer, 3 close
@@ -50,8 +57,7 @@ struct InitLds {
   int cmd, done;                    // sequence numbers (cmd -1: stop)
   int njob;
   int jz[4], jx[4], jkind[4];       // kind: 1 add (far), 2 upd (close), +4: stage-1 quirk nnz
-  UpdSel psel[4];                   // parallel relaxation: each job's stencil stage on the pop's state ...
-  double pval[4];                   // ... and its value
+  SpecEnt spec[kSpec];              // speculative relaxations (relax_role)
   long long rbusy;                  // profile: relax-role ticks of the current walk
   long long rjobs;                  // profile: relaxations | fouds18_A() fallbacks << 32
 };
@@ -296,30 +302,33 @@ AF_DEV bool pop_two_role(Heap& h, int& seq, int& jobs, int n) {
   return true;
 }
 
-#ifndef AF_INIT_PASS2  // 1: validate later jobs in a parallel second pass (measured slower: 89.6 vs 81.1 ms C4)
-#define AF_INIT_PASS2 0
-#endif
 // The relax role (wavefront 1).  A pop's neighbours are relaxed in order, each seeing the earlier
-// ones' new values (the reference's sequence).  Lane k first evaluates job k against the pop's
-// state (all jobs at once, one SIMD pass); then lane 0 walks the jobs in order: job 0's value
-// stands, and job k > 0 re-runs only update()'s cheap stencil stage on the current state — if it
-// equals lane k's (same stencil, same input values) the value is lane k's, else lane 0 finishes it
-// itself.  update()'s value is a function of its stencil stage's outputs, so the result is the
-// sequential one bit for bit; the expensive finish (wavefront angle, phase velocity) of most
-// later jobs runs beside job 0's.  fouds18_A() (no usable stencil) always runs in sequence.
+// ones' new values (the reference's sequence).  Relaxations are evaluated ahead of their turn, 64 at
+// a time: when a job has no usable speculative value, the whole wavefront runs one pass in which
+// lane 0 evaluates that job and every other lane a neighbour of one of the heap's first 16 entries
+// (the next pops), against the current state; each lane keeps its result (SpecEnt).  A job whose
+// node has an entry only re-runs update()'s cheap stencil stage on the state of its turn: equal
+// to the entry's (same stencil, same input values), the entry's value is the job's value —
+// update()'s value is a function of its stencil stage's outputs — so the results are the
+// sequential ones bit for bit, and most jobs skip the expensive finish (wavefront angle, phase
+// velocity).  fouds18_A() (no usable stencil) always runs in turn.  The heap may be mid-sift
+// while the lanes read it: any node read there is only a guess, never trusted.
 struct RelaxWin {
   int z0, x0, z1, x1, w;  // LDS window: rows z0..z1, columns x0..x1 (stage grids: the whole grid)
   int oz, ox;             // job coordinates (LDS-local) + (oz, ox) = operator coordinates
   int nnz, nnx;           // operator bounds
   double dnx, dnz;
   int quirk_nnz;          // update()'s nnz for quirk jobs (stage 1: nnx1, :1645)
+  int has_quirk;          // this walk has quirk jobs (close x-neighbours in stage 1)
 };
 
 template <bool LDSMAT>
 AF_DEV void relax_role(InitLds* L, const DevModel& M, const MatView& mv, const MidWin& mw, const RelaxWin& R,
                        int lane) {
   int last = 0;
-  long long busy = 0, njobs = 0, nf18 = 0, nref = 0;
+  long long busy = 0, njobs = 0, nf18 = 0, nburst = 0;
+  const int wz = R.z1 - R.z0, wx = R.x1 - R.x0;  // local coordinate bounds (0..wz, 0..wx)
+  L->spec[lane].cell = -1;
   while (true) {
     int cmd = 0;
     if (lane == 0) cmd = await_change(&L->cmd, last);
@@ -328,76 +337,107 @@ AF_DEV void relax_role(InitLds* L, const DevModel& M, const MatView& mv, const M
     last = cmd;
     const long long t0 = wall_clock64();
     const int nj = L->njob;  // read once: the heap role refills the jobs after the last one is done
-    if (lane < nj) {
-      const int lz = L->jz[lane], lx = L->jx[lane], kind = L->jkind[lane];
-      const int iz = lz + R.oz, ix = lx + R.ox;
-      const double* pre;
-      const CellMat cm = init_mat<LDSMAT>(M, L, mv, mw, iz, ix, &pre);
-      NbFieldT nb;
-      nb.load_lds(L->T, L->S, R.z0, R.x0, R.z1, R.x1, R.w, iz, ix);
-      const UpdSel sel = update_nb_select(nb, iz, ix, (kind & kJobQuirk) ? R.quirk_nnz : R.nnz, R.nnx);
-      L->psel[lane] = sel;
-      L->pval[lane] = update_nb_finish(M, cm, iz, ix, R.dnx, sel);
-    }
-#ifdef AF_INIT_UPD_PROF
-    const double pv0 = L->pval[0];
-    asm volatile("" ::"v"(pv0));
-    const long long t1 = wall_clock64();
-    if (lane == 0) af_prof_acc[0] += t1 - t0;
-#endif
-    // pass 2: lane k > 0 re-runs job k's stencil stage on the pop's state with jobs 0..k-1 applied
-    // (their pass-1 values; they become valid) — equal to its pass-1 stencil stage: pass-1 value
-    // stands, provided every earlier job's does (checked in order by lane 0 below)
-    bool ok = !AF_INIT_PASS2 && false;
-    if (AF_INIT_PASS2) ok = true;
-    if (AF_INIT_PASS2 && lane > 0 && lane < nj) {
-      const int lz = L->jz[lane], lx = L->jx[lane], kind = L->jkind[lane];
-      const int iz = lz + R.oz, ix = lx + R.ox;
-      NbFieldT nb;
-      nb.load_lds(L->T, L->S, R.z0, R.x0, R.z1, R.x1, R.w, iz, ix);
-      for (int j = 0; j < lane; j++) nb.patch(L->jz[j] - lz, L->jx[j] - lx, L->pval[j]);
-      const UpdSel sel = update_nb_select(nb, iz, ix, (kind & kJobQuirk) ? R.quirk_nnz : R.nnz, R.nnx);
-      ok = sel.same(L->psel[lane]);
-    }
-    const unsigned long long okm = __ballot(ok);
-    if (lane == 0) {
-      bool chain = true;  // every earlier job kept its pass-1 value
-      for (int k = 0; k < nj; k++) {
-        const int lz = L->jz[k], lx = L->jx[k], kind = L->jkind[k];
-        const int iz = lz + R.oz, ix = lx + R.ox;
-        const double* pre;
-        const CellMat cm = init_mat<LDSMAT>(M, L, mv, mw, iz, ix, &pre);
-        double v = L->pval[k];
-        if (k > 0 && !(chain && ((okm >> k) & 1ull))) {
+    int k0 = 0;
+    while (k0 < nj) {
+      // the entries of jobs k0.. (one ballot each), then one pass in which lane k - k0 re-runs job k's
+      // stencil stage on the current state with jobs k0..k-1 set to their entries' values
+      int src[4] = {-1, -1, -1, -1};
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        if (k0 + k < nj) {
+          const int key = (L->jz[k0 + k] << 8) | L->jx[k0 + k];
+          const unsigned long long hm = __ballot(L->spec[lane].cell == key);
+          src[k] = hm ? __ffsll((long long)hm) - 1 : -1;
+        }
+      }
+      bool ok = false;
+      {
+        const int q = lane, k = k0 + lane;
+        int sq = -1;
+#pragma unroll
+        for (int u = 0; u < 4; u++) sq = u == q ? src[u] : sq;
+        bool prior = true;  // every job k0..k-1 has an entry with a usable value
+#pragma unroll
+        for (int u = 0; u < 4; u++) prior = prior && (u >= q || (src[u] >= 0 && L->spec[src[u]].val != -1.0));
+        if (k < nj && sq >= 0 && prior && L->spec[sq].val != -1.0) {
+          const int lz = L->jz[k], lx = L->jx[k], kind = L->jkind[k];
+          const int iz = lz + R.oz, ix = lx + R.ox;
           NbFieldT nb;
           nb.load_lds(L->T, L->S, R.z0, R.x0, R.z1, R.x1, R.w, iz, ix);
-          const UpdSel sel = update_nb_select(nb, iz, ix, (kind & kJobQuirk) ? R.quirk_nnz : R.nnz, R.nnx);
-          if (!sel.same(L->psel[k])) {
-            v = update_nb_finish(M, cm, iz, ix, R.dnx, sel);
-            nref++;
-          }
+#pragma unroll
+          for (int u = 0; u < 3; u++)
+            if (u < q) nb.patch(L->jz[k0 + u] - lz, L->jx[k0 + u] - lx, L->spec[src[u]].val);
+          ok = update_nb_select(nb, iz, ix, (kind & kJobQuirk) ? R.quirk_nnz : R.nnz, R.nnx).same(L->spec[sq].sel);
         }
+      }
+      const unsigned long long okm = __ballot(ok);
+      int hk = 0;  // leading confirmed jobs
+      while (k0 + hk < nj && ((okm >> hk) & 1ull)) hk++;
+      if (lane == 0) {
+        for (int u = 0; u < hk; u++) {
+          const int k = k0 + u, lz = L->jz[k], lx = L->jx[k];
+          L->T[lz * R.w + lx] = L->spec[src[u]].val;
+          if (L->jkind[k] & kJobAdd) L->S[lz * R.w + lx] = 1;  // valid for the next relaxations
+          post(&L->done, (int)(njobs + u + 1));
+        }
+      }
+      njobs += hk;
+      k0 += hk;
+      if (k0 >= nj) break;
+      // job k0 in turn: one pass, this job on lane 0, guesses of the next pops' jobs on the others
+      const int lz = L->jz[k0], lx = L->jx[k0], kind = L->jkind[k0];
+      const int iz = lz + R.oz, ix = lx + R.ox;
+      double v = 0.0;
+      {
+        int cz = lz, cx = lx, cnnz = (kind & kJobQuirk) ? R.quirk_nnz : R.nnz;
+        bool cand = true;
+        if (lane > 0) {
+          const int p = 1 + ((lane - 1) >> 2), d = (lane - 1) & 3;
+          const int hc = L->hcell[p];
+          cz = (hc >> 8) + (d == 2 ? -1 : d == 3 ? 1 : 0);
+          cx = (hc & 255) + (d == 0 ? -1 : d == 1 ? 1 : 0);
+          cand = cz >= 0 && cz <= wz && cx >= 0 && cx <= wx;
+          const int st = cand ? (int)L->S[cz * R.w + cx] : 0;
+          cand = cand && st != 0;
+          cnnz = (R.has_quirk && d < 2 && st > 0) ? R.quirk_nnz : R.nnz;
+        }
+        if (cand) {
+          const int gz = cz + R.oz, gx = cx + R.ox;
+          const double* pre;
+          const CellMat cm = init_mat<LDSMAT>(M, L, mv, mw, gz, gx, &pre);
+          NbFieldT nb;
+          nb.load_lds(L->T, L->S, R.z0, R.x0, R.z1, R.x1, R.w, gz, gx);
+          const UpdSel sel = update_nb_select(nb, gz, gx, cnnz, R.nnx);
+          const double val = update_nb_finish(M, cm, gz, gx, R.dnx, sel);
+          L->spec[lane].cell = (cz << 8) | cx;
+          L->spec[lane].val = val;
+          L->spec[lane].sel = sel;
+          if (lane == 0) v = val;
+        } else {
+          L->spec[lane].cell = -1;
+        }
+        nburst++;
+      }
+      if (lane == 0) {
         if (v == -1.0) {
+          const double* pre;
+          const CellMat cm = init_mat<LDSMAT>(M, L, mv, mw, iz, ix, &pre);
           const WinField F{L->T, L->S, R.z0, R.x0, R.z1, R.x1, R.w};
           v = fouds18_win(F, M, cm, iz, ix, R.dnx, R.dnz, R.nnx, R.nnz, pre);
           nf18++;
         }
-        chain = chain && __double_as_longlong(v) == __double_as_longlong(L->pval[k]);
         L->T[lz * R.w + lx] = v;
-        njobs++;
         if (kind & kJobAdd) L->S[lz * R.w + lx] = 1;  // valid for the next relaxations (addtree sets the index)
-        post(&L->done, (int)njobs);
+        post(&L->done, (int)(njobs + 1));
       }
-#ifdef AF_INIT_UPD_PROF
-      af_prof_acc[1] += wall_clock64() - t1;
-      af_prof_acc[2] += nj;
-#endif
+      njobs++;
+      k0++;
     }
     busy += wall_clock64() - t0;
   }
   if (lane == 0) {
     L->rbusy = busy;
-    L->rjobs = njobs | (nref << 24) | (nf18 << 44);
+    L->rjobs = njobs | (nburst << 24) | (nf18 << 44);
   }
 }
 
@@ -445,7 +485,8 @@ AF_DEV void stage_loop(Heap& h, const DevModel& M, const StageCfg& c, int tid) {
     }
     post(&L->cmd, -1);
   } else if (tid >= 64) {
-    relax_role<LDSMAT>(L, M, c.mv, c.mw, RelaxWin{0, 0, nz - 1, nx - 1, nx, 0, 0, nz, nx, c.dnx, c.dnx, nx}, tid - 64);
+    relax_role<LDSMAT>(L, M, c.mv, c.mw, RelaxWin{0, 0, nz - 1, nx - 1, nx, 0, 0, nz, nx, c.dnx, c.dnx, nx, c.quirk},
+                       tid - 64);
   }
 }
 
@@ -527,7 +568,7 @@ AF_DEV void main_prefix(Heap& h, const DevModel& M, const InitJob& J, int wz0, i
     }
     post(&L->cmd, -1);
   } else if (tid >= 64) {
-    relax_role<LDSMAT>(L, M, ident, pw, RelaxWin{wz0, wx0, wz1, wx1, ww, wz0, wx0, nnz, nnx, J.dnx, J.dnz, nnz},
+    relax_role<LDSMAT>(L, M, ident, pw, RelaxWin{wz0, wx0, wz1, wx1, ww, wz0, wx0, nnz, nnx, J.dnx, J.dnz, nnz, 0},
                        tid - 64);
   }
 }
@@ -546,10 +587,6 @@ __global__ __launch_bounds__(128) void fmm_init_kernel(DevModel M0, InitJob* job
     if (M.stab && M.nstab <= kInitStab) {
       for (int k = threadIdx.x; k < 5 * M.nstab; k += blockDim.x) L->stab[k] = M.stab[k];
       M.stab = L->stab;
-    }
-    if (361 * M.ncol <= kInitPtab) {
-      for (int k = threadIdx.x; k < 361 * M.ncol; k += blockDim.x) L->ptab[k] = M.ptab[k];
-      M.ptab = L->ptab;
     }
   }
   if (src >= njobs) return;

@@ -21,7 +21,7 @@ struct HandoverOut {
   double ttn[kHandoverMax];
   signed char cls[kHandoverMax];  // 1 known inner, 2 known outer (-> close), 3 close
   // profile (wall-clock 100 MHz ticks): [0..3] stage 1, 2, 3, main prefix; [4..7] their pops;
-  // [8..11] relax-role busy ticks per stage; [12..15] relaxations | sequential re-finishes << 24 | fouds18_A() fallbacks << 44
+  // [8..11] relax-role busy ticks per stage; [12..15] relaxations | evaluation passes << 24 | fouds18_A() fallbacks << 44
   long long prof[16];
 };
 

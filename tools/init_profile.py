@@ -26,7 +26,7 @@ for k, name in enumerate(("stage1", "stage2", "stage3", "prefix")):
     out[name] = {"ms": m[k] / 1e5, "pops": m[4 + k], "us_per_pop": m[k] / 100 / max(m[4 + k], 1),
                  "relax_share": m[8 + k] / max(m[k], 1),
                  "jobs": float(np.mean(P[:, 12 + k].astype(np.int64) & 0xffffff)),
-                 "refinish": float(np.mean((P[:, 12 + k].astype(np.int64) >> 24) & 0xfffff)),
+                 "passes": float(np.mean((P[:, 12 + k].astype(np.int64) >> 24) & 0xfffff)),
                  "fouds18": float(np.mean(P[:, 12 + k].astype(np.int64) >> 44))}
 out["sum_ms"] = float(m[:4].sum() / 1e5)
 print(json.dumps(out))
