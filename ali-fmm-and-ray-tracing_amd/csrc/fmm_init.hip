@@ -97,20 +97,25 @@ struct Heap {
     L->hkey[a] = L->hkey[b];
     L->hkey[b] = k;
   }
+  // The moving entry stays in registers while it sifts: one round of LDS reads per level (the
+  // other entry's key and node), the status writes in the reference's order.
   AF_DEV void sift_up(int iz, int ix, int tpc) {
-    int tpp = parent(tpc);
+    const unsigned short mc = (unsigned short)((iz << 8) | ix);
     const double tv = L->hkey[tpc];
+    int tpp = parent(tpc);
     while (tpp > 0) {
-      if (tv < tb(tpp)) {
-        L->S[iz * nx + ix] = (short)tpp;
-        L->S[bz(tpp) * nx + bx(tpp)] = (short)tpc;
-        swap(tpc, tpp);
-        tpc = tpp;
-        tpp = parent(tpc);
-      } else {
-        tpp = 0;
-      }
+      const double kp = L->hkey[tpp];
+      const unsigned short cp = L->hcell[tpp];
+      if (!(tv < kp)) break;
+      L->S[iz * nx + ix] = (short)tpp;
+      L->S[(cp >> 8) * nx + (cp & 255)] = (short)tpc;
+      L->hcell[tpc] = cp;
+      L->hkey[tpc] = kp;
+      tpc = tpp;
+      tpp = parent(tpc);
     }
+    L->hcell[tpc] = mc;
+    L->hkey[tpc] = tv;
   }
   // addtree :94-138
   // fresh: the node is known to be far (a relaxation job; its status already reads 1, set by
@@ -143,33 +148,46 @@ struct Heap {
     for (int k = 1; k <= ntr; k++)
       if (L->hcell[k] == c) L->hkey[k] = t;
   }
-  // downtree :178-237
+  // downtree :178-237 (the moving entry in registers, as in sift_up)
   AF_DEV void down() {
     if (ntr == 1) { ntr -= 1; return; }
-    L->S[bz(ntr) * nx + bx(ntr)] = 1;
-    L->hcell[1] = L->hcell[ntr];
-    L->hkey[1] = L->hkey[ntr];
+    const unsigned short mc = L->hcell[ntr];
+    const double km = L->hkey[ntr];
+    const int ms = (mc >> 8) * nx + (mc & 255);
+    L->S[ms] = 1;
     ntr -= 1;
     int tpp = 1, tpc = 2;
     while (tpc < ntr) {
-      if (tb(tpc) > tb(tpc + 1)) tpc = tpc + 1;
-      if (tb(tpc) < tb(tpp)) {
-        L->S[bz(tpp) * nx + bx(tpp)] = (short)tpc;
-        L->S[bz(tpc) * nx + bx(tpc)] = (short)tpp;
-        swap(tpc, tpp);
-        tpp = tpc;
+      const double k1 = L->hkey[tpc], k2 = L->hkey[tpc + 1];
+      const unsigned short c1 = L->hcell[tpc], c2 = L->hcell[tpc + 1];
+      const bool right = k1 > k2;
+      const int t = right ? tpc + 1 : tpc;
+      const double kc = right ? k2 : k1;
+      const unsigned short cc = right ? c2 : c1;
+      if (kc < km) {
+        L->S[ms] = (short)t;
+        L->S[(cc >> 8) * nx + (cc & 255)] = (short)tpp;
+        L->hcell[tpp] = cc;
+        L->hkey[tpp] = kc;
+        tpp = t;
         tpc = 2 * tpp;
       } else {
         tpc = ntr + 1;
       }
     }
     if (tpc == ntr) {
-      if (tb(tpc) < tb(tpp)) {
-        L->S[bz(tpp) * nx + bx(tpp)] = (short)tpc;
-        L->S[bz(tpc) * nx + bx(tpc)] = (short)tpp;
-        swap(tpc, tpp);
+      const double kc = L->hkey[tpc];
+      const unsigned short cc = L->hcell[tpc];
+      if (kc < km) {
+        L->S[ms] = (short)tpc;
+        L->S[(cc >> 8) * nx + (cc & 255)] = (short)tpp;
+        L->hcell[tpp] = cc;
+        L->hkey[tpp] = kc;
+        tpp = tpc;
       }
     }
+    L->hcell[tpp] = mc;
+    L->hkey[tpp] = km;
   }
 };
 
