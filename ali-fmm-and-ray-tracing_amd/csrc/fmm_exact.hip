@@ -22,11 +22,23 @@ namespace af {
 
 constexpr int kXHeap = 8192;
 
+constexpr int kXSpec = 64;   // speculative relaxations (one per lane)
+constexpr int kXLog = 256;   // ring of the last relaxed nodes (the modifications update() can see)
+
+struct XSpec {
+  int cell;  // -1: empty
+  int ver;   // modifications logged when it was evaluated
+  double val;
+  UpdSel sel;
+};
+
 struct XLds {
   double key[kXHeap];
   int cell[kXHeap];
   UpdSel psel[4];  // parallel relaxation: each neighbour's stencil stage on the pop's state ...
   double pval[4];  // ... and its value
+  XSpec spec[kXSpec];
+  int logc[kXLog];
 };
 
 // addtree / updtree / downtree (:94-237) over a global nsts array, heap slots in LDS.  Keys are
@@ -315,6 +327,138 @@ AF_DEV long long xloop_par(XHeap& h, const DevModel& M, const XGrid& g, bool sta
   return pops;
 }
 
+// The walk with relaxations evaluated ahead of their turn (the HBM-grid counterpart of
+// fmm_init.hip's relax_role): when a neighbour's relaxation has no usable entry, the wavefront
+// runs one pass in which lane 0 evaluates it and every other lane a neighbour of one of the heap's
+// first 16 entries (the next pops), all against the current state (one round of stencil loads).
+// An entry stays usable while no node of its 12-point stencil has been relaxed since it was
+// evaluated: every relaxation is logged (XLds::logc), and the lanes check the log since the entry's
+// version in parallel.  update() reads nothing but those 12 nodes' values and validity, so a
+// usable entry's value is the relaxation's value bit for bit; statuses changing from close to
+// known (pops) are not logged — update() does not distinguish them — and fouds18_A() (no usable
+// stencil: known-ness matters) always runs in turn.  Returns the pops (lane 0's count).
+AF_DEV long long xloop_spec(XHeap& h, const DevModel& M, const XGrid& g, bool stage, int isx_s, int isz_s,
+                            int max_dist, double tstop, XBox* box, int lane, long long* prof = nullptr) {
+  long long pops = 0;
+  bool finished = false;
+  const int nz = g.nz, nx = g.nx;
+  XLds* X = h.H;
+  int mver = 0;  // relaxations logged (wave-uniform)
+  long long npass = 0;
+  X->spec[lane].cell = -1;
+  while (true) {
+    int go = 0, c = 0;
+    if (lane == 0) {
+      go = h.ntr > 0 && !finished && !h.err && !(tstop > 0 && h.H->key[1] >= tstop);
+      c = h.H->cell[1];
+    }
+    go = __shfl(go, 0);
+    if (!go) break;
+    c = __shfl(c, 0);
+    const int iz = c / nx, ix = c - iz * nx;
+    // lane k < 4: neighbour k (x-1, x+1, z-1, z+1), status read before downtree (see xloop)
+    const int kz = lane == 2 ? iz - 1 : lane == 3 ? iz + 1 : iz;
+    const int kx = lane == 0 ? ix - 1 : lane == 1 ? ix + 1 : ix;
+    const bool inb = lane < 4 && (lane < 2 ? (0 <= kx && kx <= nx - 1) : (0 <= kz && kz <= nz - 1));
+    const int st = inb ? g.S[kz * nx + kx] : 0;
+    const bool edge = lane < 4 && !inb && stage && (lane < 2 ? abs(isx_s - kx) : abs(isz_s - kz)) == max_dist + 1;
+    const unsigned long long jm = __ballot(inb && st != 0);
+    if (__ballot(edge) != 0ull) finished = true;
+    int stk[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) stk[k] = __shfl(st, k);
+    if (lane == 0) {
+      g.S[c] = 0;
+      h.down();
+      pops++;
+    }
+    for (int k = 0; k < 4; k++) {
+      if (!((jm >> k) & 1ull)) continue;
+      const int rz = k == 2 ? iz - 1 : k == 3 ? iz + 1 : iz, rx = k == 0 ? ix - 1 : k == 1 ? ix + 1 : ix;
+      const int r = rz * nx + rx;
+      // a usable entry?
+      const unsigned long long hm = __ballot(X->spec[lane].cell == r);
+      bool use = false;
+      double v = 0.0;
+      if (hm) {
+        const int e = __ffsll((long long)hm) - 1;
+        const int ev = X->spec[e].ver;
+        const double ev_val = X->spec[e].val;
+        bool clash = mver - ev > kXLog || ev_val == -1.0;
+        for (int q = ev + lane; !clash && q < mver; q += 64) {
+          const int m = X->logc[q & (kXLog - 1)];
+          const int mz = m / nx, mx = m - mz * nx;
+          const int dz = abs(mz - rz), dx = abs(mx - rx);
+          clash = (dz + dx >= 1) && ((dz + dx <= 1) || (dz == 2 && dx == 0) || (dx == 2 && dz == 0) ||
+                                     (dz == 1 && dx == 1));
+        }
+        use = __ballot(clash) == 0ull;
+        v = ev_val;
+        if (!use && ev_val != -1.0 && mver - ev <= kXLog) {
+          // a stencil node changed: the entry still stands if update()'s stencil stage is unchanged
+          int same = 0;
+          if (lane == 0) {
+            NbField nq;
+            nq.load(g.T, g.S, nz, nx, rz, rx);
+            same = update_nb_select(nq, rz, rx, nz, nx).same(X->spec[e].sel) ? 1 : 0;
+          }
+          use = __shfl(same, 0) != 0;
+        }
+      }
+      if (!use) {  // one pass: this relaxation on lane 0, guesses of the next pops' on the others
+        int cz = rz, cx = rx;
+        bool cand = true;
+        if (lane > 0) {
+          const int p = 1 + ((lane - 1) >> 2), d = (lane - 1) & 3;
+          const int hc = X->cell[p];
+          const int hz = hc / nx, hx = hc - hz * nx;
+          cz = hz + (d == 2 ? -1 : d == 3 ? 1 : 0);
+          cx = hx + (d == 0 ? -1 : d == 1 ? 1 : 0);
+          cand = hc >= 0 && hc < nz * nx && cz >= 0 && cz < nz && cx >= 0 && cx < nx;
+        }
+        NbField nb;
+        CellMat cm;
+        if (cand) {
+          cm = cell_mat(M, g.mv, cz, cx);
+          nb.load(g.T, g.S, nz, nx, cz, cx);
+        }
+        if (cand && lane > 0) cand = ((nb.vm | 1u) != 0u) && g.S[cz * nx + cx] != 0;  // not known (a guess)
+        if (cand) {
+          const UpdSel sel = update_nb_select(nb, cz, cx, nz, nx);
+          const double val = update_nb_finish(M, cm, cz, cx, g.dnx, sel);
+          X->spec[lane].cell = cz * nx + cx;
+          X->spec[lane].ver = mver;
+          X->spec[lane].val = val;
+          X->spec[lane].sel = sel;
+          if (lane == 0) v = val;
+        } else {
+          X->spec[lane].cell = -1;
+        }
+        npass++;
+      }
+      if (lane == 0) {
+        if (v == -1.0) {
+          GField F{g.T, g.S, nz, nx};
+          v = fouds18(F, M, cell_mat(M, g.mv, rz, rx), rz, rx, g.dnx, g.dnz, nx, nz, mat_slo(M, g.mv, rz, rx));
+        }
+        if (box) box->add(rz, rx);
+        g.T[r] = v;
+        if (stk[k] == -1) h.add(r, v, true);
+        else h.upd(r, g.S[r], v);  // its heap index now (earlier sift-ups may have moved it)
+        if (h.ndup) h.sync(r, v);
+        X->logc[mver & (kXLog - 1)] = r;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the commit before any later load
+      }
+      mver++;
+    }
+  }
+  if (prof && lane == 0) {  // diagnostics: relaxations, evaluation passes (BandSrc::sub, read by band_profile)
+    prof[0] += mver;
+    prof[1] += npass;
+  }
+  return pops;
+}
+
 // hand-over of every 3rd node of a stage grid into the next grid, in row-major order (:2391-2425,
 // :2725-2759): ttn copied, known nodes stay known, "outer" known nodes and close nodes -> heap
 AF_DEV void xhandover(XHeap& h, const XGrid& s, int isz_s, int isx_s, const XGrid& d, int isz_d, int isx_d,
@@ -419,7 +563,7 @@ __global__ __launch_bounds__(64) void fmm_exact_kernel(BandParams P) {
     }
     if (lane == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // grid stores before the walk's loads
     {
-      const long long pops = xloop_par(h, M, g, true, isx_s, isz_s, scale * size, 0.0, nullptr, lane);
+      const long long pops = xloop_spec(h, M, g, true, isx_s, isz_s, scale * size, 0.0, nullptr, lane, B->sub);
       if (lane == 0) {
         B->steps[stg] = pops;
         err = h.err;
@@ -448,7 +592,7 @@ __global__ __launch_bounds__(64) void fmm_exact_kernel(BandParams P) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     if (!err) {
-      const long long pops = xloop_par(h, M, g, false, 0, 0, 0, P.tstop, &box, lane);
+      const long long pops = xloop_spec(h, M, g, false, 0, 0, 0, P.tstop, &box, lane, B->sub);
       if (lane == 0) B->steps[2] = pops;
     }
     if (lane == 0) {

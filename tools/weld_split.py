@@ -37,6 +37,8 @@ def main():
         ctx.travel(rx, rz, subgrid=9, copy_out=False)
         t1 = time.perf_counter()
         init_ms, band_ms, total_ms = ctx.last_timing()
+        bp = ctx.band_profile(0)
+        print(json.dumps({"relaxations_src0": int(bp[10]), "evaluation_passes_src0": int(bp[11])}))
         print(json.dumps({"fields": len(rx), "subgrid": 9, "wall_s": t1 - t0, "init_ms": init_ms, "band_ms": band_ms,
                           "steps_src0": ctx.source_stats(0)[0].tolist()}))
     if a.dump:
