@@ -35,8 +35,6 @@ struct XSpec {
 struct XLds {
   double key[kXHeap];
   int cell[kXHeap];
-  UpdSel psel[4];  // parallel relaxation: each neighbour's stencil stage on the pop's state ...
-  double pval[4];  // ... and its value
   XSpec spec[kXSpec];
   int logc[kXLog];
 };
@@ -165,168 +163,6 @@ struct XBox {
   }
 };
 
-// update() then fouds18_A() (:2326-2329 / :2790-2793)
-AF_DEV double xrelax(const DevModel& M, const XGrid& g, int iz, int ix) {
-  CellMat cm = cell_mat(M, g.mv, iz, ix);
-  NbField nb;
-  nb.load(g.T, g.S, g.nz, g.nx, iz, ix);
-  double v = update(nb, M, cm, iz, ix, g.dnx, g.nz, g.nx);
-  if (v == -1.0) {
-    GField F{g.T, g.S, g.nz, g.nx};
-    v = fouds18(F, M, cm, iz, ix, g.dnx, g.dnz, g.nx, g.nz, mat_slo(M, g.mv, iz, ix));
-  }
-  return v;
-}
-
-// the reference's FMM loop (oracle fmm_loop): stage grids stop when a neighbour step leaves the
-// window at max_dist + 1 from the source; the main grid stops when the root reaches tstop
-AF_DEV long long xloop(XHeap& h, const DevModel& M, const XGrid& g, bool stage, int isx_s, int isz_s, int max_dist,
-                       double tstop, XBox* box = nullptr) {
-  long long pops = 0;
-  bool finished = false;
-  const int nz = g.nz, nx = g.nx;
-  while (h.ntr > 0 && !finished && !h.err) {
-    const int c = h.H->cell[1];
-    if (tstop > 0 && h.H->key[1] >= tstop) break;
-    const int iz = c / nx, ix = c - iz * nx;
-    // the four neighbours' statuses in one round trip, issued before downtree: downtree and the
-    // add / upd of earlier neighbours only move heap indices (positive stays positive) and touch
-    // no other neighbour's far / known state, so the reference's per-neighbour classification
-    // (far -1 -> add, close > 0 -> upd, known 0 -> skip) can be read up front.  (Prefetching the
-    // neighbours' whole stencils as well was measured slower: most neighbours are known.)
-    const int nbz[4] = {iz, iz, iz - 1, iz + 1}, nbx[4] = {ix - 1, ix + 1, ix, ix};
-    bool inb[4];
-    int st[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      inb[k] = k < 2 ? (0 <= nbx[k] && nbx[k] <= nx - 1) : (0 <= nbz[k] && nbz[k] <= nz - 1);
-      st[k] = g.S[inb[k] ? nbz[k] * nx + nbx[k] : c];  // branch-free: the 4 loads issue together
-    }
-    g.S[c] = 0;
-    h.down();
-    pops++;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      if (inb[k]) {
-        const int r = nbz[k] * nx + nbx[k];
-        if (box && st[k] != 0) box->add(nbz[k], nbx[k]);
-        if (st[k] == -1) {
-          const double v = xrelax(M, g, nbz[k], nbx[k]);
-          g.T[r] = v;
-          h.add(r, v);
-          if (h.ndup) h.sync(r, v);
-        } else if (st[k] > 0) {
-          // the heap index read up front is still the node's: only earlier neighbours' sift-ups
-          // move heap entries in between, and they may move this node — re-read it from S then
-          const double v = xrelax(M, g, nbz[k], nbx[k]);
-          g.T[r] = v;
-          h.upd(r, g.S[r], v);
-          if (h.ndup) h.sync(r, v);
-        }
-      } else if (stage && (k < 2 ? abs(isx_s - nbx[k]) : abs(isz_s - nbz[k])) == max_dist + 1) {
-        finished = true;
-      }
-    }
-  }
-  return pops;
-}
-
-// xloop run by the whole wavefront: lane 0 keeps the heap; the popped node's neighbours are
-// evaluated on lanes 0..3 at once against the pop's state (pass 1), lane k > 0 re-runs its
-// stencil stage with the earlier neighbours' pass-1 values applied (pass 2), and lane 0 commits
-// them in the reference's order, finishing a neighbour itself only when its stencil stage differs
-// (update()'s value is a function of its stencil stage: results are the sequential ones bit for
-// bit).  Returns the pops (lane 0's count).
-#ifndef AF_EXACT_PASS2
-#define AF_EXACT_PASS2 1
-#endif
-AF_DEV long long xloop_par(XHeap& h, const DevModel& M, const XGrid& g, bool stage, int isx_s, int isz_s,
-                           int max_dist, double tstop, XBox* box, int lane) {
-  long long pops = 0;
-  bool finished = false;
-  const int nz = g.nz, nx = g.nx;
-  while (true) {
-    int go = 0, c = 0;
-    if (lane == 0) {
-      go = h.ntr > 0 && !finished && !h.err && !(tstop > 0 && h.H->key[1] >= tstop);
-      c = h.H->cell[1];
-    }
-    go = __shfl(go, 0);
-    if (!go) break;
-    c = __shfl(c, 0);
-    const int iz = c / nx, ix = c - iz * nx;
-    // lane k < 4: neighbour k (x-1, x+1, z-1, z+1), status read before downtree (see xloop)
-    const int kz = lane == 2 ? iz - 1 : lane == 3 ? iz + 1 : iz;
-    const int kx = lane == 0 ? ix - 1 : lane == 1 ? ix + 1 : ix;
-    const bool inb = lane < 4 && (lane < 2 ? (0 <= kx && kx <= nx - 1) : (0 <= kz && kz <= nz - 1));
-    const int st = inb ? g.S[kz * nx + kx] : 0;
-    const bool edge = lane < 4 && !inb && stage && (lane < 2 ? abs(isx_s - kx) : abs(isz_s - kz)) == max_dist + 1;
-    const unsigned long long jm = __ballot(inb && st != 0);
-    if (__ballot(edge) != 0ull) finished = true;
-    int stk[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) stk[k] = __shfl(st, k);
-    const bool job = (jm >> lane) & 1ull;
-    if (lane == 0) {
-      g.S[c] = 0;
-      h.down();
-      pops++;
-    }
-    // pass 1
-    NbField nb;
-    if (job) {
-      const CellMat cm = cell_mat(M, g.mv, kz, kx);
-      nb.load(g.T, g.S, nz, nx, kz, kx);
-      const UpdSel sel = update_nb_select(nb, kz, kx, nz, nx);
-      h.H->psel[lane] = sel;
-      h.H->pval[lane] = update_nb_finish(M, cm, kz, kx, g.dnx, sel);
-    }
-    // pass 2 (on pass 1's neighbourhood, patched)
-    bool ok = true;  // the first neighbour's pass-1 value always stands
-    if (job && (jm & ((1ull << lane) - 1ull))) {
-      ok = false;
-    }
-    if (AF_EXACT_PASS2 && job && (jm & ((1ull << lane) - 1ull))) {
-      for (int j = 0; j < lane; j++) {
-        if ((jm >> j) & 1ull) {
-          const int jz = j == 2 ? iz - 1 : j == 3 ? iz + 1 : iz, jx = j == 0 ? ix - 1 : j == 1 ? ix + 1 : ix;
-          nb.patch(jz - kz, jx - kx, h.H->pval[j]);
-        }
-      }
-      ok = update_nb_select(nb, kz, kx, nz, nx).same(h.H->psel[lane]);
-    }
-    const unsigned long long okm = __ballot(ok);
-    // commit in order (lane 0)
-    if (lane == 0) {
-      bool chain = true;
-      for (int k = 0; k < 4; k++) {
-        if (!((jm >> k) & 1ull)) continue;
-        const int rz = k == 2 ? iz - 1 : k == 3 ? iz + 1 : iz, rx = k == 0 ? ix - 1 : k == 1 ? ix + 1 : ix;
-        const int r = rz * nx + rx;
-        double v = h.H->pval[k];
-        if (!(chain && ((okm >> k) & 1ull))) {
-          NbField nq;
-          nq.load(g.T, g.S, nz, nx, rz, rx);
-          const UpdSel sel = update_nb_select(nq, rz, rx, nz, nx);
-          if (!sel.same(h.H->psel[k])) v = update_nb_finish(M, cell_mat(M, g.mv, rz, rx), rz, rx, g.dnx, sel);
-        }
-        if (v == -1.0) {
-          GField F{g.T, g.S, nz, nx};
-          v = fouds18(F, M, cell_mat(M, g.mv, rz, rx), rz, rx, g.dnx, g.dnz, nx, nz, mat_slo(M, g.mv, rz, rx));
-        }
-        chain = chain && __double_as_longlong(v) == __double_as_longlong(h.H->pval[k]);
-        if (box) box->add(rz, rx);
-        g.T[r] = v;
-        if (stk[k] == -1) h.add(r, v, true);
-        else h.upd(r, g.S[r], v);  // its heap index now (earlier sift-ups may have moved it)
-        if (h.ndup) h.sync(r, v);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the commits before the next pop's loads
-    }
-  }
-  return pops;
-}
-
 // The walk with relaxations evaluated ahead of their turn (the HBM-grid counterpart of
 // fmm_init.hip's relax_role): when a neighbour's relaxation has no usable entry, the wavefront
 // runs one pass in which lane 0 evaluates it and every other lane a neighbour of one of the heap's
@@ -356,7 +192,10 @@ AF_DEV long long xloop_spec(XHeap& h, const DevModel& M, const XGrid& g, bool st
     if (!go) break;
     c = __shfl(c, 0);
     const int iz = c / nx, ix = c - iz * nx;
-    // lane k < 4: neighbour k (x-1, x+1, z-1, z+1), status read before downtree (see xloop)
+    // lane k < 4: neighbour k (x-1, x+1, z-1, z+1); its status is read before downtree: downtree and
+    // the add / upd of earlier neighbours only move heap indices (positive stays positive) and touch
+    // no other neighbour's far / known state, so the reference's per-neighbour classification
+    // (far -1 -> add, close > 0 -> upd, known 0 -> skip) can be read up front
     const int kz = lane == 2 ? iz - 1 : lane == 3 ? iz + 1 : iz;
     const int kx = lane == 0 ? ix - 1 : lane == 1 ? ix + 1 : ix;
     const bool inb = lane < 4 && (lane < 2 ? (0 <= kx && kx <= nx - 1) : (0 <= kz && kz <= nz - 1));

@@ -11,15 +11,6 @@
 // stage-3 nodes that the band kernel hands over to the main grid (:2006-2040), as (cell, ttn,
 // class) triples.
 #define CR_LDS_TABLES  // cr_math.h tables in LDS (crm::lds_init at kernel start)
-#ifdef AF_INIT_UPD_PROF  // diagnostic builds: wall clock between update()'s stencil stage and its finish
-__device__ long long af_upd_mark;
-__device__ long long af_prof_acc[3];  // load, stencil stage, finish (all sources, one lane each)
-#define AF_UPD_HOOK(dep)                                               \
-  do {                                                                 \
-    asm volatile("" ::"v"(dep));                                       \
-    af_upd_mark = wall_clock64();                                      \
-  } while (0)
-#endif
 #include "device_common.h"
 #include "local_ops.h"
 #include "kernels.h"
@@ -89,14 +80,6 @@ struct Heap {
   AF_DEV int bx(int k) const { return L->hcell[k] & 255; }
   AF_DEV double tb(int k) const { return L->hkey[k]; }
   AF_DEV static int parent(int t) { return (int)rint((double)t / 2.0); }  // half-even (:123)
-  AF_DEV void swap(int a, int b) {
-    unsigned short e = L->hcell[a];
-    L->hcell[a] = L->hcell[b];
-    L->hcell[b] = e;
-    double k = L->hkey[a];
-    L->hkey[a] = L->hkey[b];
-    L->hkey[b] = k;
-  }
   // The moving entry stays in registers while it sifts: one round of LDS reads per level (the
   // other entry's key and node), the status writes in the reference's order.
   AF_DEV void sift_up(int iz, int ix, int tpc) {
@@ -746,13 +729,6 @@ __global__ __launch_bounds__(128) void fmm_init_kernel(DevModel M0, InitJob* job
       if (lane == 0) {
         O->prof[11] = L->rbusy;
         O->prof[15] = L->rjobs;
-#ifdef AF_INIT_UPD_PROF
-        if (src == 0) {  // diagnostic builds: the accumulators (whole launch so far) replace [8..10]
-          O->prof[8] = af_prof_acc[0];
-          O->prof[9] = af_prof_acc[1];
-          O->prof[10] = af_prof_acc[2];
-        }
-#endif
       }
       // emit every touched window node: known (1) / close (3)
       if (lane == 0) {
