@@ -270,6 +270,10 @@ def main():
         if cpu:
             out["speedup_vs_cpu_baseline"] = value / cpu["value"]
             out["speedup_vs_cpu_all_physical_cores_extrapolated"] = value / cpu["value_all_physical_cores_extrapolated"]
+            # the numba reference itself, by the measured per-core calibration of the port
+            out["speedup_vs_numba_reference_same_cores"] = value / (cpu["value"] / PORT_VS_REFERENCE_PER_CORE)
+            out["speedup_vs_numba_reference_all_physical_cores"] = value / (
+                cpu["value_all_physical_cores_extrapolated"] / PORT_VS_REFERENCE_PER_CORE)
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
