@@ -45,6 +45,12 @@ template <class T>
 AF_DEV void gst(T* p, T v) {
   *(AF_GLOBAL T*)p = v;
 }
+// the same pointer with its global address space made visible (an addrspace cast round trip):
+// plain loads and stores through it compile to global_* instead of flat_*
+template <class T>
+AF_DEV T* gptr(T* p) {
+  return (T*)(AF_GLOBAL T*)p;
+}
 AF_DEV int gatomic_max(int* p, int v) { return __atomic_fetch_max((AF_GLOBAL int*)p, v, __ATOMIC_RELAXED); }
 // sc1 (L1-bypassing load, write-through store) accesses for data another CU writes or reads
 // within the same launch (MI355X_MICROARCH.md "inter-workgroup visibility": sc1 stores, drained

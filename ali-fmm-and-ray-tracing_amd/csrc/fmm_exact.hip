@@ -37,6 +37,7 @@ struct XLds {
   int cell[kXHeap];
   XSpec spec[kXSpec];
   int logc[kXLog];
+  int dup[8];  // XHeap's nodes with two heap entries (here, not in XHeap: see InitLds::dup)
 };
 
 // addtree / updtree / downtree (:94-237) over a global nsts array, heap slots in LDS.  Keys are
@@ -51,7 +52,6 @@ struct XHeap {
   int ntr;
   int err;
   int ndup = 0;
-  int dup[kXDup];
   AF_DEV void setS(int c, int v) { S[c] = v; }
   AF_DEV static int parent(int t) { return (int)rint((double)t / 2.0); }  // half-even (:123)
   AF_DEV void swap(int a, int b) {
@@ -91,7 +91,7 @@ struct XHeap {
         err = 3;
         return;
       }
-      dup[ndup++] = c;
+      H->dup[ndup++] = c;
     }
     setS(c, ntr);
     H->cell[ntr] = c;
@@ -107,7 +107,7 @@ struct XHeap {
   // node c's ttn is now key: every heap entry of a node with two entries takes it
   AF_DEV void sync(int c, double key) {
     bool d = false;
-    for (int k = 0; k < ndup; k++) d |= dup[k] == c;
+    for (int k = 0; k < ndup; k++) d |= H->dup[k] == c;
     if (!d) return;
     for (int k = 1; k <= ntr; k++)
       if (H->cell[k] == c) H->key[k] = key;
@@ -261,7 +261,7 @@ AF_DEV long long xloop_spec(XHeap& h, const DevModel& M, const XGrid& g, bool st
           cm = cell_mat(M, g.mv, cz, cx);
           nb.load(g.T, g.S, nz, nx, cz, cx);
         }
-        if (cand && lane > 0) cand = ((nb.vm | 1u) != 0u) && g.S[cz * nx + cx] != 0;  // not known (a guess)
+        if (cand && lane > 0) cand = g.S[cz * nx + cx] != 0;  // not known (a guess)
         if (cand) {
           const UpdSel sel = update_nb_select(nb, cz, cx, nz, nx);
           const double val = update_nb_finish(M, cm, cz, cx, g.dnx, sel);
@@ -358,8 +358,8 @@ __global__ __launch_bounds__(64) void fmm_exact_kernel(BandParams P) {
       err = 4;
       break;
     }
-    g.T = B->Ts[stg];
-    g.S = B->Ss[stg];
+    g.T = gptr(B->Ts[stg]);
+    g.S = gptr(B->Ss[stg]);
     g.mv = MatView{scale, (scale - 1) / 2, bottom, scale, (scale - 1) / 2, left, sg, sgside, 0, 0, 1};
     g.dnx = g.dnz = P.dnx / scale;
     const int isx_s = scale * (int)(isx - left), isz_s = scale * (int)(isz - bottom);
@@ -417,8 +417,8 @@ __global__ __launch_bounds__(64) void fmm_exact_kernel(BandParams P) {
   // fine main grid (memset by the host: T 0, S -1): hand-over, then the exact prefix
   {
     XGrid g;
-    g.T = B->T;
-    g.S = B->S;
+    g.T = gptr(B->T);
+    g.S = gptr(B->S);
     g.nz = nnz;
     g.nx = nnx;
     g.mv = MatView{sg, sgside, 0, sg, sgside, 0, 1, 0, 0, 0, 1};

@@ -42,6 +42,9 @@ struct InitLds {
   MatRec mat[kInitMat];
   double stab[5 * kInitStab];       // DevModel::stab (nstab <= kInitStab)
   unsigned short hcell[kInitHeap];  // heap nodes (z << 8) | x
+  unsigned short dup[8];            // Heap: nodes with two heap entries (in LDS, not in the Heap
+                                    // object: a dynamically indexed member would put the whole heap
+                                    // state, LDS pointer included, in scratch -> flat LDS accesses)
   unsigned char smid[kInitWin];     // material ids of the coarse cells under the current grid
   signed char decC[kInitDec];       // 0 far, 1 known inner, 2 known outer, 3 close
   // heap role -> relax role hand-off of one pop's neighbours (two-wavefront heap walk)
@@ -75,7 +78,6 @@ struct Heap {
   int err;
   int ndup = 0;
   int pops = 0;
-  unsigned short dup[kInitDup];
   AF_DEV int bz(int k) const { return L->hcell[k] >> 8; }
   AF_DEV int bx(int k) const { return L->hcell[k] & 255; }
   AF_DEV double tb(int k) const { return L->hkey[k]; }
@@ -108,7 +110,7 @@ struct Heap {
     if (ntr >= kInitHeap) { err = 1; ntr = kInitHeap - 1; return; }
     if (!fresh && L->S[iz * nx + ix] > 0) {  // already in the heap: a second entry
       if (ndup == kInitDup) { err = 1; return; }
-      dup[ndup++] = (unsigned short)((iz << 8) | ix);
+      L->dup[ndup++] = (unsigned short)((iz << 8) | ix);
     }
     L->S[iz * nx + ix] = (short)ntr;
     L->hcell[ntr] = (unsigned short)((iz << 8) | ix);
@@ -125,7 +127,7 @@ struct Heap {
   AF_DEV void sync(int iz, int ix) {
     const unsigned short c = (unsigned short)((iz << 8) | ix);
     bool d = false;
-    for (int k = 0; k < ndup; k++) d |= dup[k] == c;
+    for (int k = 0; k < ndup; k++) d |= L->dup[k] == c;
     if (!d) return;
     const double t = L->T[iz * nx + ix];
     for (int k = 1; k <= ntr; k++)
