@@ -131,6 +131,10 @@ class Context:
         for k, v in (("cdelta", cdelta), ("r0", r0), ("batch", batch)):
             if v is not None:
                 self.set_option(k, v)
+        # experiments: ALIFMM_OPT_<NAME>=value sets alifmm_set_option(name, value) on every context
+        for k, v in os.environ.items():
+            if k.startswith("ALIFMM_OPT_"):
+                self.set_option(k[len("ALIFMM_OPT_"):].lower(), float(v))
 
     def _chk(self, rc, what):
         if rc != 0:

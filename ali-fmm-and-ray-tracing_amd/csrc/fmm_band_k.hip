@@ -47,7 +47,12 @@
 namespace af {
 namespace kb {
 
-constexpr int kThreads = 512;
+// 768 threads: 12 waves, 3 per SIMD (the kernel fits 168 VGPRs): the claim and accept passes
+// hide more latency (C4 128 sources: 456 -> 437 ms with 512 -> 768, tools/kbench.py)
+#ifndef AF_THREADS
+#define AF_THREADS 768
+#endif
+constexpr int kThreads = AF_THREADS;
 constexpr int kWaves = kThreads / 64;
 constexpr int kLcap = 2560, kAcap = 1024, kEcap = 1536, kBcap = 512, kDcap = 512, kRcap = 1024;
 constexpr int kHashLog = 13;
@@ -58,6 +63,23 @@ constexpr int kHash = 1 << kHashLog;
 #ifndef AF_X1_SLEEP
 #define AF_X1_SLEEP 1
 #endif
+// claim item -> thread: 1 = item q0 + u * kThreads + tid (a short list is spread over every wave,
+// u = 0 first), 0 = wave-contiguous blocks of 64 * kClaimU items
+#ifndef AF_CLAIM_SPREAD
+#define AF_CLAIM_SPREAD 1
+#endif
+// evaluate: the next cell's stencil (and material id) is loaded before update() of the current one
+#ifndef AF_EVAL_PF
+#define AF_EVAL_PF 0
+#endif
+// accepted list ordered by 8x8 tile (counting sort over kSortB buckets) before the claim, when it
+// has more than AF_SORT_ACC entries (0: never): the claim's status loads and, through the claim
+// order, the evaluation's stencil loads of one wavefront then touch few cache lines
+#ifndef AF_SORT_ACC
+#define AF_SORT_ACC 256
+#endif
+constexpr int kSortB = 512;
+AF_DEV int tile_bucket(int c) { return ((pkz(c) >> 3) & 15) << 5 | ((pkx(c) >> 3) & 31); }
 constexpr int kClaimU = AF_CLAIM_U;  // claim items per lane per pass
 constexpr int kHashItems = 6144;  // claim items deduplicated in the LDS hash (more: global stamps)
 constexpr int kStabLds = 64, kPtabLds = 722, kMatLds = 256;
@@ -82,6 +104,11 @@ struct Lds {
   double Dv[kDcap];  // ... and their T
   int Rx[kRcap];  // claim items from the neighbour members' accepted rim cells; fallback list
   alignas(16) int H[kHash];
+#if AF_SORT_ACC
+  int As[kAcap];     // the accepted list in tile order
+  int Sb[kSortB];    // bucket counts -> offsets
+  int Sw[kWaves];    // per-wave bucket sums of the scan
+#endif
   double tmin_g, thr;
   unsigned long long nE2;  // claimed-list lengths: interior (low half), boundary (high half)
   int nA, nF, hi, taken, nD, nR, nRx, live_g, err_g, err, nFb;
@@ -393,6 +420,9 @@ __global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
       }
     }
     for (int k = tid * 4; k < kHash; k += kThreads * 4) *(int4*)&sh->H[k] = make_int4(0, 0, 0, 0);
+#if AF_SORT_ACC
+    for (int k = tid; k < kSortB; k += kThreads) sh->Sb[k] = 0;
+#endif
     tmin = wave_min(tmin);
     if (lane == 0) sh->red[wv] = tmin;
     if (tid == 0) {
@@ -538,23 +568,47 @@ __global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
     AF_SUBT(1, trr)
     AF_TICK(1)
     const int nA = min(sh->nA, capL), nRx = min(sh->nRx, capC);
+    int* alist = sh->Al;
+#if AF_SORT_ACC
+    if (nA > AF_SORT_ACC && nA <= kAcap) {  // (uniform) counting sort of the accepted list by tile
+      for (int a = tid; a < nA; a += kThreads) atomicAdd(&sh->Sb[tile_bucket(sh->Al[a])], 1);
+      __syncthreads();
+      static_assert(kSortB % 64 == 0 && kSortB / 64 <= kWaves, "one bucket per thread of the first waves");
+      int cnt = tid < kSortB ? sh->Sb[tid] : 0, wsum;
+      const int ex = wave_excl_scan(cnt, wsum);
+      if (lane == 0 && wv < kSortB / 64) sh->Sw[wv] = wsum;
+      __syncthreads();
+      if (tid < kSortB) {
+        int base = 0;
+        for (int w = 0; w < wv; w++) base += sh->Sw[w];
+        sh->Sb[tid] = base + ex;
+      }
+      __syncthreads();
+      for (int a = tid; a < nA; a += kThreads) {
+        const int c = sh->Al[a];
+        sh->As[atomicAdd(&sh->Sb[tile_bucket(c)], 1)] = c;
+      }
+      __syncthreads();
+      alist = sh->As;
+    }
+#endif
     // ---- P3b: claim ----
     const int nItems = 4 * nA + nRx;
     const bool use_hash = nItems <= kHashItems;
     const bool lds_items = nA <= kAcap && nRx <= kRcap;
     const int stamp = (int)steps;
-    for (int q0 = wv * 64 * kClaimU; q0 < nItems; q0 += kThreads * kClaimU) {
+    for (int q0 = AF_CLAIM_SPREAD ? 0 : wv * 64 * kClaimU; q0 < nItems; q0 += kThreads * kClaimU) {
       int r[kClaimU], s[kClaimU], o[kClaimU];
       const long long tdd = prof ? wall_clock64() : 0;
       unsigned hh[kClaimU];
       int pv[kClaimU];
 #pragma unroll
       for (int u = 0; u < kClaimU; u++) {
-        const int q = q0 + u * 64 + lane;
+        const int q = AF_CLAIM_SPREAD ? q0 + u * kThreads + tid : q0 + u * 64 + lane;
         int c = -1;
         if (q < nItems) {
           if (q < 4 * nA) {
-            c = nb_cell(lds_items ? AL.lds(q >> 2) : AL.get(q >> 2), q & 3, nz, nx);
+            c = nb_cell(lds_items ? alist[q >> 2] : AL.get(q >> 2), q & 3, nz, nx);
             if (c >= 0 && g.owner(pkx(c)) != me) c = -1;  // claimed by its owner (from my rim list)
           } else {
             c = lds_items ? RX.lds(q - 4 * nA) : RX.get(q - 4 * nA);
@@ -668,14 +722,7 @@ __global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
     // ---- P4: evaluate ----
     const bool lds_e = nE <= kEcap;
     const double dnx_e = launder_u(R.dnx);
-    for (int e = tid; e < nE; e += kThreads) {
-      const int r = lds_e ? EL.lds(e) : EL.get(e);
-      const int z = pkz(r), x = pkx(r);
-      NbFieldT nb;  // stencil loads first, then the material id: one memory round trip
-      if (e - lane + 64 <= nEi) nb.load(T, nz, nx, z, x);  // (wave-uniform) interior cells: T only
-      else load_nb(nb, T, eprv, cells + 2 * ecells, g, z, x);
-      const CellMat cm = band_mat<LDSMAT>(M, sh->mat, sh->stab, R.mv, z, x);
-      const double v = update(nb, M, cm, z, x, dnx_e, nz, nx);
+    auto eval_done = [&](int e, double v) {
       if (lds_e) VL.put_lds(e, v);
       else VL.put(e, v);
       myupd++;
@@ -687,6 +734,47 @@ __global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
         if (lane == fl) fb = atomicAdd(&sh->nFb, __popcll(fm));
         fb = __shfl(fb, fl) + __popcll(fm & ((1ull << lane) - 1ull));
         if (v == -1.0 && fb < kRcap) sh->Rx[fb] = e;
+      }
+    };
+    // stencil loads first, then the material id: one memory round trip per cell
+    auto eval_load = [&](int e, NbFieldT& nb, int& r) {
+      r = lds_e ? EL.lds(e) : EL.get(e);
+      const int z = pkz(r), x = pkx(r);
+      if (e - lane + 64 <= nEi) nb.load(T, nz, nx, z, x);  // (wave-uniform) interior cells: T only
+      else load_nb(nb, T, eprv, cells + 2 * ecells, g, z, x);
+    };
+    if (AF_EVAL_PF && LDSMAT) {
+      // software pipeline: cell e + kThreads's loads are in flight during update() of cell e
+      NbFieldT nb;
+      int r = 0, id = 0;
+      int e = tid;
+      if (e < nE) {
+        eval_load(e, nb, r);
+        id = band_mat_id(M, R.mv, pkz(r), pkx(r));
+      }
+      for (; e < nE; e += kThreads) {
+        const int en = e + kThreads;
+        NbFieldT nbn;
+        int rn = 0, idn = 0;
+        if (en < nE) {
+          eval_load(en, nbn, rn);
+          idn = band_mat_id(M, R.mv, pkz(rn), pkx(rn));
+        }
+        const int z = pkz(r), x = pkx(r);
+        const CellMat cm = band_mat_rec(sh->mat, sh->stab, R.mv, id);
+        eval_done(e, update(nb, M, cm, z, x, dnx_e, nz, nx));
+        nb = nbn;
+        r = rn;
+        id = idn;
+      }
+    } else {
+      for (int e = tid; e < nE; e += kThreads) {
+        NbFieldT nb;
+        int r;
+        eval_load(e, nb, r);
+        const int z = pkz(r), x = pkx(r);
+        const CellMat cm = band_mat<LDSMAT>(M, sh->mat, sh->stab, R.mv, z, x);
+        eval_done(e, update(nb, M, cm, z, x, dnx_e, nz, nx));
       }
     }
     AF_TICK(3)

@@ -34,6 +34,8 @@ sys.path.insert(0, os.path.join(REPO, "ali-fmm-and-ray-tracing_amd"))
 sys.path.insert(0, os.path.join(REPO, "tests"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+VALU_SIMDS = 256 * 4  # 256 CUs x 4 SIMDs
+CLOCK_HZ = 2.4e9      # peak engine clock
 # algorithmic bytes per cell-sweep (T f32 read + write 8, orientation 4,
 # vel_map 4, material id 1, halo 1.06)
 BYTES_PER_SWEEP = 18.1
@@ -207,6 +209,7 @@ def main():
               "band_workgroups_per_source": members, "cdelta": args.cdelta}
     # HBM-side bytes per launch: rocprofv3 PMC passes (tools/profile.sh) on this library and workload
     traffic_bytes = None
+    valu = None
     try:
         import glob
         import hashlib
@@ -217,6 +220,8 @@ def main():
             if (t.get("libalifmm_sha256") == lib_sha and t.get("traffic_bytes_per_launch")
                     and t.get("sources_per_gpu") == ns and t.get("grid") == [n, n]):
                 traffic_bytes = t["traffic_bytes_per_launch"]
+                if t.get("valu_insts_per_launch"):
+                    valu = t
     except OSError:
         pass
 
@@ -263,7 +268,14 @@ def main():
                          "cell_sweeps_per_launch": int(sweeps),
                          "algorithmic_bytes_per_launch": BYTES_PER_SWEEP * int(sweeps),
                          "traffic_over_algorithmic": (traffic_bytes / (BYTES_PER_SWEEP * sweeps))
-                         if traffic_bytes else None},
+                         if traffic_bytes else None,
+                         # what does bound it: f64 VALU issue (a wave64 VALU op occupies a SIMD for
+                         # >= 4 cycles), from the SQ pass of the same build: VALU cycles / SIMD cycles
+                         "valu_issue": ({"insts_per_launch": valu["valu_insts_per_launch"],
+                                         "floor_ms": valu["valu_insts_per_launch"] * 4 / VALU_SIMDS / CLOCK_HZ * 1e3,
+                                         "frac": valu["valu_insts_per_launch"] * 4 / VALU_SIMDS / CLOCK_HZ / band_avg_s,
+                                         "sq_wait_any_frac": valu.get("sq_wait_any_frac")}
+                                        if valu and band_avg_s > 0 else None)},
             "result_return": ret,
             "cpu_baseline": cpu,
         }

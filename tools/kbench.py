@@ -22,10 +22,7 @@ def main():
     name = sys.argv[1]
     sizes = [int(a) for a in sys.argv[2:]] or [128, 16]
     ctx = _alifmm.Context(0)
-    for opt in ("members", "stripe_log", "cdelta"):  # ALIFMM_OPT_<NAME>=value
-        v = os.environ.get("ALIFMM_OPT_" + opt.upper())
-        if v is not None:
-            ctx.set_option(opt, float(v))
+    # ALIFMM_OPT_<NAME>=value options are applied by _alifmm.Context itself
     vt = W.default_table()
     ctx.set_model(*W.weldlike_model(), vt, vt, W.weldlike_dnx())
     sx, sz = W.c4_sources(128)

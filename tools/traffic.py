@@ -32,19 +32,21 @@ def per_launch(d, counter):
 
 
 fetch_kb = per_launch("pmc_fetch", "FETCH_SIZE")
+# issue profile (optional SQ pass): VALU wave-instructions per launch and the memory-wait share
+sq = {c: per_launch("pmc_sq", c) for c in ("SQ_INSTS_VALU", "SQ_WAIT_ANY", "SQ_WAVE_CYCLES", "SQ_ACTIVE_INST_VALU")}
 write_kb = per_launch("pmc_write", "WRITE_SIZE")
 lib = os.path.join(repo, "ali-fmm-and-ray-tracing_amd", "lib", "libalifmm.so")
 # the workload the passes profiled (the bench line each pass printed): bench.py applies the
 # figure only to a run of the same configuration
 bench_config = None
-for f in ("pmc_fetch.log", "pmc_write.log"):
+for f in ("pmc_fetch.log", "pmc_write.log", "pmc_sq.log"):
     try:
         line = [l for l in open(os.path.join(out, f)) if l.startswith('{"metric"')][-1]
         cfg = json.loads(line)["config"]
         cfg.pop("total_sources", None)  # per-GPU workload: the same launch at any world size
         cfg.setdefault("cdelta", None)  # bench lines before these keys ran the defaults
         if bench_config is not None and cfg != bench_config:
-            sys.exit("FETCH and WRITE passes profiled different workloads: %s vs %s" % (bench_config, cfg))
+            sys.exit("the PMC passes profiled different workloads: %s vs %s" % (bench_config, cfg))
         bench_config = cfg
     except (OSError, IndexError):
         pass
@@ -57,6 +59,9 @@ res = {
                   "L2 memory-side requests (Infinity-Cache hits included)",
     "libalifmm_sha256": hashlib.sha256(open(lib, "rb").read()).hexdigest(),
     "bench_config": bench_config,
+    "valu_insts_per_launch": sq["SQ_INSTS_VALU"],
+    "sq_wait_any_frac": (sq["SQ_WAIT_ANY"] / sq["SQ_WAVE_CYCLES"]) if sq["SQ_WAIT_ANY"] and sq["SQ_WAVE_CYCLES"] else None,
+    "sq_active_valu_frac": (sq["SQ_ACTIVE_INST_VALU"] / sq["SQ_WAVE_CYCLES"]) if sq["SQ_ACTIVE_INST_VALU"] and sq["SQ_WAVE_CYCLES"] else None,
     # the workload keys bench.py matches before it reports the figure as roofline.traffic
     "sources_per_gpu": (bench_config or {}).get("sources_per_gpu"),
     "grid": (bench_config or {}).get("grid"),
