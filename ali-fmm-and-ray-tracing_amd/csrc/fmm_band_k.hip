@@ -68,6 +68,10 @@ constexpr int kHash = 1 << kHashLog;
 #ifndef AF_CLAIM_SPREAD
 #define AF_CLAIM_SPREAD 1
 #endif
+// fallback fouds18_A(): four lanes per cell (1) or one (0)
+#ifndef AF_F18_SPLIT
+#define AF_F18_SPLIT 1
+#endif
 // evaluate: the next cell's stencil (and material id) is loaded before update() of the current one
 #ifndef AF_EVAL_PF
 #define AF_EVAL_PF 0
@@ -815,7 +819,31 @@ __global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
           if (kn) atomicOr(&wmask[i / 25], 1u << o);
         }
         __syncthreads();
-        if (tid < nr) {
+        if (AF_F18_SPLIT) {
+          // four lanes per cell, one candidate of each stencil family per lane (fouds18_part)
+          static_assert(4 * kFbRound <= kThreads, "four lanes per fallback cell");
+          if (tid < 4 * nr) {
+            const int ci = tid >> 2, part = tid & 3;
+            const int q = r0 + ci;
+            const int e = q < nlist ? sh->Rx[q] : q - nlist;
+            if (q < nlist || VL.get(e) == -1.0) {  // (the same for the cell's four lanes)
+              const int c = EL.get(e);
+              const int z = pkz(c), x = pkx(c);
+              const Win5 F{win + 25 * ci, wmask[ci], z, x};
+              const CellMat cm = band_mat<LDSMAT>(M, sh->mat, sh->stab, R.mv, z, x);
+              const double dnx_f = launder_u(R.dnx), dnz_f = launder_u(R.dnz);
+              F18Part fp = fouds18_part<LDSMAT>(F, M, cm, z, x, dnx_f, dnz_f, nx, nz, mat_slo(M, R.mv, z, x), part);
+#pragma unroll
+              for (int o = 1; o <= 2; o <<= 1) {
+                F18Part ot;
+#pragma unroll
+                for (int k = 0; k < 4; k++) ot.m[k] = __shfl_xor(fp.m[k], o);
+                fp = f18_min(fp, ot);
+              }
+              if (part == 0) VL.put(e, fouds18_combine(fp, F.tt(z, x)));
+            }
+          }
+        } else if (tid < nr) {
           const int q = r0 + tid;
           const int e = q < nlist ? sh->Rx[q] : q - nlist;
           if (q < nlist || VL.get(e) == -1.0) {

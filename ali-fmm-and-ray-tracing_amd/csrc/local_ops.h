@@ -28,9 +28,19 @@ AF_DEV double fouds18_slowness(const DevModel& M, const CellMat& cm, int q) {
 // fouds18_A(), and the persistent kernels cannot afford its registers in the step loop), or null.
 // PRE_ONLY: the caller guarantees pre != null, so the group-velocity code is not compiled in at all
 // (fouds18_A() alone then needs 87 VGPRs instead of 181)
+//
+// fouds18_part(): the four stencil families' minima over the candidates of one PART (0..3: the
+// family's candidate number part, -1: all of them; +inf where a family has no candidate), so that
+// four lanes can evaluate one cell and combine their parts (fouds18_combine, the reference's
+// combination :696-897).  Each family's result is a minimum over its candidates (the reference's
+// running min, order-free: no candidate is NaN), so any split gives the same bits.
+struct F18Part {
+    double m[4];
+};
 template <bool PRE_ONLY = false, class F>
-AF_DEV double fouds18(const F& f, const DevModel& M, const CellMat& cm, long iz, long ix, double dnx, double dnz,
-                      long nnx, long nnz, const double* pre = nullptr) {
+AF_DEV F18Part fouds18_part(const F& f, const DevModel& M, const CellMat& cm, long iz, long ix, double dnx,
+                            double dnz, long nnx, long nnz, const double* pre, int part) {
+    F18Part P;
 #define N_(z, x) f.st((z), (x))
 #define T_(z, x) f.tt((z), (x))
     /* ---- 0 deg stencil (:281-459) ---- */
@@ -76,7 +86,7 @@ AF_DEV double fouds18(const F& f, const DevModel& M, const CellMat& cm, long iz,
             #pragma unroll 1
             for (int kk_ = 0; kk_ < 2; kk_++) {
                 long k = kk_ == 0 ? iz - 1 : iz + 1;
-                if (0 <= k && k <= nnz - 1) {
+                if (0 <= k && k <= nnz - 1 && (part < 0 || part == jj_ * 2 + kk_)) {
                     int swk = -1;
                     long k2;
                     if (k == iz - 1) {
@@ -168,6 +178,7 @@ AF_DEV double fouds18(const F& f, const DevModel& M, const CellMat& cm, long iz,
             }
         }
     }
+    P.m[0] = tsw1 ? travm : INFINITY;
     /* ---- 45 deg stencil (:467-696) ---- */
     int tsw2 = 0;
     double travmd = 0;
@@ -197,7 +208,7 @@ AF_DEV double fouds18(const F& f, const DevModel& M, const CellMat& cm, long iz,
             for (int q_ = 0; q_ < 2; q_++) {
                 long jj = (q_ == 0) ? ix - 1 : ix + 1;
                 long kk = (jj == ix - 1) ? iz - 1 : iz + 1;
-                if (0 <= jj && jj <= nnx - 1 && 0 <= kk && kk <= nnz - 1) {
+                if (0 <= jj && jj <= nnx - 1 && 0 <= kk && kk <= nnz - 1 && (part < 0 || part == jj_ * 2 + q_)) {
                     int swskew = -1;
                     long jj2, kk2;
                     if (jj == ix - 1) {
@@ -293,11 +304,9 @@ AF_DEV double fouds18(const F& f, const DevModel& M, const CellMat& cm, long iz,
             }
         }
     }
-    if (travmd != 0) travmd = (travm < travmd) ? travm : travmd;
-    else travmd = travm;
+    P.m[1] = tsw2 ? travmd : INFINITY;
 
     /* ---- atan(1/2) stencils (:698-897) ---- */
-    double travmt = 0, travms = 0;
     #pragma unroll 1
     for (int pass = 0; pass < 2; pass++) {
         slown = pass == 0 ? slo2 : slo3;
@@ -313,7 +322,7 @@ AF_DEV double fouds18(const F& f, const DevModel& M, const CellMat& cm, long iz,
         for (int lp = 0; lp < 4; lp++) {
             long j = JV(lp), k = KV(lp), jj = JV(lp + 1), kk = KV(lp + 1);
             if (0 <= j && j <= nnx - 1 && 0 <= k && k <= nnz - 1 && 0 <= jj && jj <= nnx - 1 && 0 <= kk &&
-                kk <= nnz - 1) {
+                kk <= nnz - 1 && (part < 0 || part == lp)) {
                 int swsol = 0;
                 double a = 0, b = 0, c = 0, tref = 0, u;
                 if (N_(k, j) == 0) {
@@ -350,23 +359,42 @@ AF_DEV double fouds18(const F& f, const DevModel& M, const CellMat& cm, long iz,
                 }
             }
         }
-        if (pass == 0) {
-            travmt = tm;
-            if (travmt != 0) travmt = (travmt < travmd) ? travmt : travmd;
-            else travmt = travmd;
-        } else {
-            travms = tm;
-            if (travms != 0) travms = (travmt < travms) ? travmt : travms;
-            else travms = travmt;
-        }
+        P.m[2 + pass] = tsw ? tm : INFINITY;
     }
 #undef JV
 #undef KV
-    double cur = f.tt(iz, ix);
-    if (cur != 0) travms = (travms < cur) ? travms : cur;
-    return travms;
+    return P;
 #undef N_
 #undef T_
+}
+
+// the minimum of two parts' family results (lanes of one cell)
+AF_DEV F18Part f18_min(const F18Part& a, const F18Part& b) {
+    F18Part r;
+    for (int k = 0; k < 4; k++) r.m[k] = (a.m[k] < b.m[k]) ? a.m[k] : b.m[k];
+    return r;
+}
+
+// the reference's combination of the families (:696-697, :798-800, :895-897) and of the current ttn
+AF_DEV double fouds18_combine(const F18Part& P, double cur) {
+    const double travm = P.m[0] == INFINITY ? 0.0 : P.m[0];
+    double travmd = P.m[1] == INFINITY ? 0.0 : P.m[1];
+    if (travmd != 0) travmd = (travm < travmd) ? travm : travmd;
+    else travmd = travm;
+    double travmt = P.m[2] == INFINITY ? 0.0 : P.m[2];
+    if (travmt != 0) travmt = (travmt < travmd) ? travmt : travmd;
+    else travmt = travmd;
+    double travms = P.m[3] == INFINITY ? 0.0 : P.m[3];
+    if (travms != 0) travms = (travmt < travms) ? travmt : travms;
+    else travms = travmt;
+    if (cur != 0) travms = (travms < cur) ? travms : cur;
+    return travms;
+}
+
+template <bool PRE_ONLY = false, class F>
+AF_DEV double fouds18(const F& f, const DevModel& M, const CellMat& cm, long iz, long ix, double dnx, double dnz,
+                      long nnx, long nnz, const double* pre = nullptr) {
+    return fouds18_combine(fouds18_part<PRE_ONLY>(f, M, cm, iz, ix, dnx, dnz, nnx, nnz, pre, -1), f.tt(iz, ix));
 }
 
 
