@@ -621,6 +621,11 @@ __global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
         r[u] = c;
         hh[u] = hslot(c);
       }
+      // the items' statuses (own cells, stored by this workgroup only): loads issued before the
+      // dedupe, whose LDS round trips then cover their latency (a duplicate's load is wasted)
+#pragma unroll
+      for (int u = 0; u < kClaimU; u++)
+        s[u] = r[u] >= 0 ? gld(S + ((long)pkz(r[u]) * nx + pkx(r[u]))) : (int)kKnown;
       if (use_hash) {
 #pragma unroll
         for (int u = 0; u < kClaimU; u++) pv[u] = r[u] >= 0 ? atomicCAS(&sh->H[hh[u]], 0, r[u] + 1) : 0;
@@ -658,7 +663,6 @@ __global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
 #pragma unroll
       for (int u = 0; u < kClaimU; u++) {
         const long f = r[u] >= 0 ? (long)pkz(r[u]) * nx + pkx(r[u]) : 0;
-        s[u] = r[u] >= 0 ? gld(S + f) : (int)kKnown;  // own cells, stored by this workgroup only
         o[u] = (!use_hash && r[u] >= 0) ? gatomic_max(own + f, stamp) : -1;
       }
       // u-major list order: consecutive entries are neighbours of consecutive accepted cells, so
@@ -669,7 +673,7 @@ __global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
       int ci = 0, cb = 0;
 #pragma unroll
       for (int u = 0; u < kClaimU; u++) {
-        const bool take = s[u] != kKnown && o[u] < stamp;
+        const bool take = r[u] >= 0 && s[u] != kKnown && o[u] < stamp;
         const bool bnd = take && g.edge(pkx(r[u]));
         bi[u] = __ballot(take && !bnd);
         bb[u] = __ballot(bnd);
