@@ -85,6 +85,10 @@ constexpr int kHash = 1 << kHashLog;
 constexpr int kSortB = 512;
 AF_DEV int tile_bucket(int c) { return ((pkz(c) >> 3) & 15) << 5 | ((pkx(c) >> 3) & 31); }
 constexpr int kClaimU = AF_CLAIM_U;  // claim items per lane per pass
+#ifndef AF_ACC_U
+#define AF_ACC_U 1
+#endif
+constexpr int kAccU = AF_ACC_U;  // close-set entries per lane per accept pass (2 and 4 measured slower)
 constexpr int kHashItems = 6144;  // claim items deduplicated in the LDS hash (more: global stamps)
 constexpr int kStabLds = 64, kPtabLds = 722, kMatLds = 256;
 constexpr int kDirty = (int)0x80000000u;  // close-set slot: committed last step (edge cell)
@@ -500,42 +504,72 @@ __global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
       rpt = gld_sc1(rimt + ((long)q * 2 + par) * P.capR + e);
     }
     // ---- P2: accept own close cells; copy last step's commits of edge cells forward ----
+    // kAccU entries per lane and pass, one LDS atomic pair per wave and pass for the accepted ones
     auto accept = [&](auto lds_only) {
       constexpr bool LO = decltype(lds_only)::value;
-      for (int e0 = wv * 64; e0 < hi; e0 += kThreads) {
-        const int e = e0 + lane;
-        const double t = e < hi ? (LO ? Lt.lds(e) : Lt.get(e)) : INFINITY;
-        const bool live = t < INFINITY;
-        const bool acc = t <= thr;
-        const int raw = live ? (LO ? L.lds(e) : L.get(e)) : 0;
-        const int c = raw & kCell;
-        if (K > 1 && live) {
-          const bool ed = g.edge(pkx(c));
-          if (raw < 0 || (acc && ed)) {  // dirty (committed last step) or accepted edge cell
-            gst_sc1(Epar + g.eidx(pkz(c), pkx(c)), acc ? -t : t);
-            if (raw < 0 && !acc) {
-              if (LO) L.put_lds(e, c);
-              else L.put(e, c);
+      for (int e0 = wv * 64 * kAccU; e0 < hi; e0 += kThreads * kAccU) {
+        double t[kAccU];
+        int c[kAccU];
+        bool acc[kAccU];
+        unsigned long long m[kAccU];
+        int tot = 0;
+#pragma unroll
+        for (int u = 0; u < kAccU; u++) {
+          const int e = e0 + u * 64 + lane;
+          t[u] = e < hi ? (LO ? Lt.lds(e) : Lt.get(e)) : INFINITY;
+          const bool live = t[u] < INFINITY;
+          acc[u] = t[u] <= thr;
+          const int raw = live ? (LO ? L.lds(e) : L.get(e)) : 0;
+          c[u] = raw & kCell;
+          if (K > 1 && live) {
+            const bool ed = g.edge(pkx(c[u]));
+            if (raw < 0 || (acc[u] && ed)) {  // dirty (committed last step) or accepted edge cell
+              gst_sc1(Epar + g.eidx(pkz(c[u]), pkx(c[u])), acc[u] ? -t[u] : t[u]);
+              if (raw < 0 && !acc[u]) {
+                if (LO) L.put_lds(e, c[u]);
+                else L.put(e, c[u]);
+              }
+            }
+            const int d = wave_push(&sh->nD, acc[u] && ed, capC, &sh->err);
+            if (d >= 0) {
+              DC.put(d, c[u]);
+              DV.put(d, t[u]);
             }
           }
-          const int d = wave_push(&sh->nD, acc && ed, capC, &sh->err);
-          if (d >= 0) {
-            DC.put(d, c);
-            DV.put(d, t);
-          }
+          m[u] = __ballot(acc[u]);
+          tot += __popcll(m[u]);
         }
-        int sa, sf;
-        wave_push2(&sh->nA, &sh->nF, acc, capL, &sh->err, sa, sf);
-        if (sa >= 0) {
-          AL.put(sa, c);
-          gst(S + pk_flat(c, nx), (int)kKnown);
-          if (LO) {
-            Lt.put_lds(e, INFINITY);
-            FS.put_lds(sf, e);
-          } else {
-            Lt.put(e, INFINITY);
-            FS.put(sf, e);
+        if (tot == 0) continue;
+        int ba = 0, bf = 0;
+        if (lane == 0) {
+          ba = atomicAdd(&sh->nA, tot);
+          bf = atomicAdd(&sh->nF, tot);
+        }
+        ba = __shfl(ba, 0);
+        bf = __shfl(bf, 0);
+        const unsigned long long lt = (1ull << lane) - 1ull;
+#pragma unroll
+        for (int u = 0; u < kAccU; u++) {
+          if (acc[u]) {
+            const int e = e0 + u * 64 + lane;
+            const int off = __popcll(m[u] & lt);
+            const int sa = ba + off, sf = bf + off;
+            if (sa >= capL || sf >= capL) {
+              sh->err = 2;
+            } else {
+              AL.put(sa, c[u]);
+              gst(S + pk_flat(c[u], nx), (int)kKnown);
+              if (LO) {
+                Lt.put_lds(e, INFINITY);
+                FS.put_lds(sf, e);
+              } else {
+                Lt.put(e, INFINITY);
+                FS.put(sf, e);
+              }
+            }
           }
+          ba += __popcll(m[u]);
+          bf += __popcll(m[u]);
         }
       }
     };
