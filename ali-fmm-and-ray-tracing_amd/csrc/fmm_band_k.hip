@@ -172,7 +172,11 @@ AF_DEV void load_nb(NbFieldT& nb, const double* T, int eprv, int total, const KG
 // LDS — T at the end of the previous step (NaN -> 0 as GField) and known-ness (own cell: status 0;
 // another member's: known in the previous edge buffer, or close with T <= thr) — then one lane per
 // cell runs fouds18_A() on the staged window (few registers: the accessor is two LDS reads).
-constexpr int kFbRound = 128;  // cells per staging round (25 doubles each in the claim-hash space)
+#ifndef AF_FB_ROUND
+#define AF_FB_ROUND 128
+#endif
+constexpr int kFbRound = AF_FB_ROUND;  // cells per staging round (25 doubles each in the claim-hash space)
+static_assert(kFbRound * 25 * sizeof(double) <= kHash * sizeof(int), "staging windows fit the claim hash");
 struct Win5 {
   const double* t;  // 25 values, row-major (dz + 2) * 5 + (dx + 2)
   unsigned known;   // bit (dz + 2) * 5 + (dx + 2)
