@@ -145,20 +145,6 @@ struct RunCfg {
 };
 
 // material of main-grid cell (z, x): LDSMAT = one id load + the LDS record; else four arrays
-// (split in two: the id load, and the record from the LDS table)
-AF_DEV int band_mat_id(const DevModel& M, const MatView& v, int z, int x) {
-  const long i = mv_cell(M, v, z, x);
-  return M.mid8 ? (int)gld(M.mid8 + i) : gld(M.mid + i);
-}
-AF_DEV CellMat band_mat_rec(const MatRec* mat, const double* stab, const MatView& v, int id) {
-  const MatRec m = mat[id];
-  CellMat r;
-  r.velpn = m.velpn;
-  r.veln = v.quant ? (double)(int)m.veln : m.veln;
-  r.vm = v.quant ? (double)(float)m.vm : m.vm;
-  r.stif = m.sidx >= 0 ? stab + 5 * m.sidx : nullptr;
-  return r;
-}
 template <bool LDSMAT>
 AF_DEV CellMat band_mat(const DevModel& M, const MatRec* mat, const double* stab, const MatView& v, int z, int x) {
   if (!LDSMAT) return cell_mat(M, v, z, x);

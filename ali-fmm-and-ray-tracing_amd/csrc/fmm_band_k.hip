@@ -68,13 +68,16 @@ constexpr int kHash = 1 << kHashLog;
 #ifndef AF_CLAIM_SPREAD
 #define AF_CLAIM_SPREAD 1
 #endif
+#ifndef AF_PROF_FBWAIT
+#define AF_PROF_FBWAIT 0
+#endif
 // fallback fouds18_A(): four lanes per cell (1) or one (0)
 #ifndef AF_F18_SPLIT
 #define AF_F18_SPLIT 1
 #endif
-// evaluate: the next cell's stencil (and material id) is loaded before update() of the current one
-#ifndef AF_EVAL_PF
-#define AF_EVAL_PF 0
+// evaluate: boundary cells in the first pass (1) or last (0: measured faster, 416 vs 422 ms)
+#ifndef AF_EVAL_BFIRST
+#define AF_EVAL_BFIRST 0
 #endif
 // accepted list ordered by 8x8 tile (counting sort over kSortB buckets) before the claim, when it
 // has more than AF_SORT_ACC entries (0: never): the claim's status loads and, through the claim
@@ -451,7 +454,9 @@ __global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
     const long long tdr = prof ? wall_clock64() : 0;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores have completed
     __syncthreads();
+#if !AF_PROF_FBWAIT
     AF_SUBT(3, tdr)
+#endif
     const long long tx1 = prof ? wall_clock64() : 0;
     if (K > 1) {
       if (tid == 0) {
@@ -782,50 +787,28 @@ __global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
         if (v == -1.0 && fb < kRcap) sh->Rx[fb] = e;
       }
     };
-    // stencil loads first, then the material id: one memory round trip per cell
-    auto eval_load = [&](int e, NbFieldT& nb, int& r) {
-      r = lds_e ? EL.lds(e) : EL.get(e);
+    // stencil loads first, then the material id: one memory round trip per cell.  Pass order
+    // (AF_EVAL_BFIRST): the boundary cells (the list's tail; their edge-buffer lines come from
+    // further away) go to the first pass's lanes, so their latency overlaps the interior passes
+    // instead of trailing the phase.  Every wave whose cells are all interior loads T only.
+    for (int j = tid; j < nE; j += kThreads) {
+      const int e = AF_EVAL_BFIRST ? (j < nEb ? nEi + j : j - nEb) : j;
+      const bool interior = AF_EVAL_BFIRST ? j - lane >= nEb : e - lane + 64 <= nEi;  // (wave-uniform)
+      const int r = lds_e ? EL.lds(e) : EL.get(e);
       const int z = pkz(r), x = pkx(r);
-      if (e - lane + 64 <= nEi) nb.load(T, nz, nx, z, x);  // (wave-uniform) interior cells: T only
-      else load_nb(nb, T, eprv, cells + 2 * ecells, g, z, x);
-    };
-    if (AF_EVAL_PF && LDSMAT) {
-      // software pipeline: cell e + kThreads's loads are in flight during update() of cell e
       NbFieldT nb;
-      int r = 0, id = 0;
-      int e = tid;
-      if (e < nE) {
-        eval_load(e, nb, r);
-        id = band_mat_id(M, R.mv, pkz(r), pkx(r));
-      }
-      for (; e < nE; e += kThreads) {
-        const int en = e + kThreads;
-        NbFieldT nbn;
-        int rn = 0, idn = 0;
-        if (en < nE) {
-          eval_load(en, nbn, rn);
-          idn = band_mat_id(M, R.mv, pkz(rn), pkx(rn));
-        }
-        const int z = pkz(r), x = pkx(r);
-        const CellMat cm = band_mat_rec(sh->mat, sh->stab, R.mv, id);
-        eval_done(e, update(nb, M, cm, z, x, dnx_e, nz, nx));
-        nb = nbn;
-        r = rn;
-        id = idn;
-      }
-    } else {
-      for (int e = tid; e < nE; e += kThreads) {
-        NbFieldT nb;
-        int r;
-        eval_load(e, nb, r);
-        const int z = pkz(r), x = pkx(r);
-        const CellMat cm = band_mat<LDSMAT>(M, sh->mat, sh->stab, R.mv, z, x);
-        eval_done(e, update(nb, M, cm, z, x, dnx_e, nz, nx));
-      }
+      if (interior) nb.load(T, nz, nx, z, x);
+      else load_nb(nb, T, eprv, cells + 2 * ecells, g, z, x);
+      const CellMat cm = band_mat<LDSMAT>(M, sh->mat, sh->stab, R.mv, z, x);
+      eval_done(e, update(nb, M, cm, z, x, dnx_e, nz, nx));
     }
     AF_TICK(3)
     // ---- P4b: fouds18_A() over the compacted fallback list, in staged rounds ----
+    const long long tfw = prof ? wall_clock64() : 0;
     __syncthreads();
+#if AF_PROF_FBWAIT  // diagnostic: sub[3] = the wait for the other waves' evaluation
+    AF_SUBT(3, tfw)
+#endif
     {
       const int nFb = sh->nFb;
       const double thr_f = sh->thr;
