@@ -185,12 +185,9 @@ CR_HD double atan(double x) {
   return copysign(atan_accurate(a), x);
 }
 
-CR_HD void sincos(double x, double* sp, double* cp) {
-  if (!(fabs(x) < 0x1p14)) {
-    *sp = ::sin(x);
-    *cp = ::cos(x);
-    return;
-  }
+// sin x ~ s + ls and cos x ~ c + lc (|x| < 2^14), each within 2^-62 of the result relative to it
+// (the bound the rounding tests below rely on)
+CR_HD void sincos_fast(double x, double& s, double& ls, double& c, double& lc) {
   const double jd = nearbyint(x * k128OverPi);
   const int j = (int)jd;
   const double r1 = x - jd * kP1;
@@ -216,8 +213,20 @@ CR_HD void sincos(double x, double* sp, double* cp) {
   const dd pc = two_prod(-sj.h, rh);
   const dd c0 = two_sum(cj.h, pc.h);
   const double cl = c0.l + (pc.l + cj.l + cj.h * C - sj.h * sr_l - sj.l * rh);
-  const double s = s0.h + sl, c = c0.h + cl;
-  const double ls = sl - (s - s0.h), lc = cl - (c - c0.h);
+  s = s0.h + sl;
+  c = c0.h + cl;
+  ls = sl - (s - s0.h);
+  lc = cl - (c - c0.h);
+}
+
+CR_HD void sincos(double x, double* sp, double* cp) {
+  if (!(fabs(x) < 0x1p14)) {
+    *sp = ::sin(x);
+    *cp = ::cos(x);
+    return;
+  }
+  double s, ls, c, lc;
+  sincos_fast(x, s, ls, c, lc);
   if (rounds_same(s, ls, fabs(s) * 0x1p-62) && rounds_same(c, lc, fabs(c) * 0x1p-62)) {
     *sp = fabs(x) < 0x1p-26 ? x : s;
     *cp = c;
@@ -239,9 +248,17 @@ CR_HD double cos(double x) {
   sincos(x, &s, &c);
   return c;
 }
+// tan = sin / cos from the fast path's pairs (relative error below 2^-61 + the quotient's
+// 2^-104), rounding test at 2^-59; the double-double evaluation decides the rest
 CR_HD double tan(double x) {
   if (!(fabs(x) < 0x1p14)) return ::tan(x);
   if (fabs(x) < 0x1p-27) return x;
+  double sh, sl, ch, cl;
+  sincos_fast(x, sh, sl, ch, cl);
+  const double q = sh / ch;
+  const double r = ((fma(-q, ch, sh) + sl) - q * cl) / ch;
+  const double h = q + r, l = r - (h - q);
+  if (rounds_same(h, l, fabs(h) * 0x1p-59)) return h;
   dd s, c;
   sincos_dd(x, s, c);
   const dd t = div(s, c);

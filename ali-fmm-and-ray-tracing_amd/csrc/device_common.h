@@ -185,7 +185,9 @@ AF_DEV double christoffel_group(const double* s, double eff, double vm) {
     pa = pymod(AF_ATAN((-B - sqrt(disc)) / (C - A)), M_PI);
   else
     pa = pymod(AF_ATAN((-B + sqrt(disc)) / (C - A)), M_PI);
-  double lam = 0.5 * (AF_COS(2 * pa) * (c22 - c44) + AF_SIN(2 * pa) * (c23 + c44) * tan_ang + c22 + c44);
+  double s2, c2;  // sin and cos of 2 pa from one reduction
+  AF_SINCOS(2 * pa, &s2, &c2);
+  double lam = 0.5 * (c2 * (c22 - c44) + s2 * (c23 + c44) * tan_ang + c22 + c44);
   return 1000 * vm * sqrt(lam / sigma) / AF_COS(eff * kDeg2Rad - pa);
 }
 
@@ -199,11 +201,43 @@ AF_DEV double christoffel_phase(const double* s, double eff, double vm) {
   return 1000 * vm * sqrt((A + C + sqrt((A - C) * (A - C) + 4 * (B * B))) / (2 * s[4]));
 }
 
-// group velocity with the selector 'velpn != 0 or stif_den == None' (:287, :2950)
-AF_DEV double group_vel_cell(const DevModel& M, const CellMat& c, double eff) {
-  if (c.velpn != 0 || c.stif == nullptr) return table_vel(M.gtab, M.ncol, eff, c.velpn, c.vm);
+// group velocity with the selector 'velpn != 0 or stif_den == None' (:287, :2950); gtab: the
+// group-velocity table (M.gtab or a copy in LDS)
+AF_DEV double group_vel_cell(const DevModel& M, const CellMat& c, double eff, const double* gtab) {
+  if (c.velpn != 0 || c.stif == nullptr) return table_vel(gtab, M.ncol, eff, c.velpn, c.vm);
   return christoffel_group(c.stif, eff, c.vm);
 }
+AF_DEV double group_vel_cell(const DevModel& M, const CellMat& c, double eff) {
+  return group_vel_cell(M, c, eff, M.gtab);
+}
+
+// Material sources of time_between_points() on the coarse grid (identity view): the model
+// arrays in HBM, or the material-id bytes plus the distinct records, stiffness rows and group
+// table staged in LDS by the kernel (the same values: the records are the model's).
+struct MatGlobal {
+  const DevModel& M;
+  AF_DEV int id(int z, int x) const { return M.mid ? gld(M.mid + (long)z * M.nx0 + x) : -1; }
+  AF_DEV CellMat cm(int, int z, int x) const {
+    const MatView ident{1, 0, 0, 1, 0, 0, 1, 0, 0, 0, 0};
+    return cell_mat(M, ident, z, x);
+  }
+  AF_DEV const double* gtab() const { return M.gtab; }
+};
+struct MatLds {
+  const DevModel& M;
+  const MatRec* mat;
+  const double* stab;
+  const double* gt;
+  AF_DEV int id(int z, int x) const {
+    const long c = (long)z * M.nx0 + x;
+    return M.mid8 ? (int)gld(M.mid8 + c) : gld(M.mid + c);
+  }
+  AF_DEV CellMat cm(int id, int, int) const {
+    const MatRec m = mat[id];
+    return CellMat{m.veln, m.vm, m.velpn, m.sidx >= 0 ? stab + 5 * m.sidx : nullptr};
+  }
+  AF_DEV const double* gtab() const { return gt; }
+};
 
 // wavefront_angle_dist :1413-1460
 template <class I>
@@ -229,7 +263,8 @@ AF_DEV void wad(I ix, I iz, I x1, I x2, I x3, I z1, I z2, I z3, double y1, doubl
 }
 
 // time_between_points :2835-2989 (coarse material, numba negative-index wrap)
-AF_DEV double tbp(const DevModel& M, double x1, double x2, double y1, double y2, double dnx, int sg) {
+template <class MS>
+AF_DEV double tbp(const DevModel& M, const MS& ms, double x1, double x2, double y1, double y2, double dnx, int sg) {
   x1 = x1 / (double)sg;
   x2 = x2 / (double)sg;
   y1 = y1 / (double)sg;
@@ -247,7 +282,6 @@ AF_DEV double tbp(const DevModel& M, double x1, double x2, double y1, double y2,
   int dir_y = (start_y < end_y) ? 1 : -1;
   double next_x = (double)pyround(start_x) + dir_x * 0.5;
   double next_y = (double)pyround(start_y) + dir_y * 0.5;
-  const MatView ident{1, 0, 0, 1, 0, 0, 1, 0, 0, 0, 0};
   int last_id = -1;
   double slown = 0.0;
   while (!(fin_x && fin_y)) {
@@ -292,11 +326,11 @@ AF_DEV double tbp(const DevModel& M, double x1, double x2, double y1, double y2,
     // the slowness depends on the cell only through its material record (the angle is fixed for
     // the segment), so consecutive pieces in the same material reuse it: the same value, without
     // the group-velocity evaluation (the per-cell material id identifies the record exactly)
-    const int id = M.mid ? gld(M.mid + mv_cell(M, ident, (int)y_pos, (int)x_pos)) : -1;
+    const int id = ms.id((int)y_pos, (int)x_pos);
     if (id < 0 || id != last_id) {
-      CellMat cm = cell_mat(M, ident, (int)y_pos, (int)x_pos);
+      CellMat cm = ms.cm(id, (int)y_pos, (int)x_pos);
       double eff = pymod(cm.veln - angle, 180);
-      double velocity = group_vel_cell(M, cm, eff);
+      double velocity = group_vel_cell(M, cm, eff, ms.gtab());
       slown = 1.0 / velocity;
       last_id = id;
     }
@@ -307,6 +341,9 @@ AF_DEV double tbp(const DevModel& M, double x1, double x2, double y1, double y2,
     prev_y = nyv;
   }
   return section_time;
+}
+AF_DEV double tbp(const DevModel& M, double x1, double x2, double y1, double y2, double dnx, int sg) {
+  return tbp(M, MatGlobal{M}, x1, x2, y1, y2, dnx, sg);
 }
 
 }  // namespace af

@@ -10,7 +10,13 @@
 // exactly the candidate the reference's sequential strict-'<' scan selects.  ray_time (:2992-3022) is
 // accumulated segment by segment as the ray grows, i.e. in the reference's summation order, so
 // times match the CPU to the last bit
-// except where ocml's atan/tan/sin/cos differ from glibc.  All arithmetic is double precision.
+// (the trigonometry is correctly rounded, cr_math.h).  All arithmetic is double precision.
+// Every candidate's time_between_points() is a chain of dependent reads (material id, material
+// record, stiffness row or group table, the trig tables): with LDSMAT the records, stiffness rows,
+// group table and the CR trig tables are staged in LDS once per workgroup, so only the material-id
+// byte comes from memory.
+#define CR_LDS_TABLES  // cr_math.h tables in LDS (crm::lds_init at kernel start)
+#include <type_traits>
 #include "kernels.h"
 
 namespace af {
@@ -19,6 +25,7 @@ namespace af {
 
 constexpr int kRayWaves = 4;
 constexpr int kMaxCand = 256;
+constexpr int kRayMatLds = 256, kRayStabLds = 64, kRayGtabLds = 722;
 
 struct Key {
   double v;
@@ -27,11 +34,25 @@ struct Key {
 };
 AF_DEV bool key_less(const Key& a, const Key& b) { return a.v < b.v || (a.v == b.v && a.order < b.order); }
 
-template <int G>
+template <int G, bool LDSMAT>
 __global__ __launch_bounds__(64 * kRayWaves) void find_ray_kernel(RayParams P) {
   constexpr int kGroups = 64 / G;             // rays per wavefront
   constexpr int kTT = kMaxCand / kGroups;      // candidate slots per ray
   __shared__ double TTs[kRayWaves][kMaxCand];
+  __shared__ MatRec smat[LDSMAT ? kRayMatLds : 1];
+  __shared__ double sstab[LDSMAT ? 5 * kRayStabLds : 1];
+  __shared__ double sgtab[LDSMAT ? kRayGtabLds : 1];
+  crm::lds_init();
+  if (LDSMAT) {
+    for (int k = threadIdx.x; k < P.M.nmat; k += blockDim.x) smat[k] = P.M.mtab[k];
+    for (int k = threadIdx.x; k < 5 * P.M.nstab; k += blockDim.x) sstab[k] = P.M.stab[k];
+    for (int k = threadIdx.x; k < 361 * P.M.ncol; k += blockDim.x) sgtab[k] = P.M.gtab[k];
+  }
+  __syncthreads();
+  const std::conditional_t<LDSMAT, MatLds, MatGlobal> ms = [&] {
+    if constexpr (LDSMAT) return MatLds{P.M, smat, sstab, sgtab};
+    else return MatGlobal{P.M};
+  }();
   const int lane = threadIdx.x & (G - 1), w = threadIdx.x >> 6, grp = (threadIdx.x & 63) / G;
   const int ray = (blockIdx.x * kRayWaves + w) * kGroups + grp;
   if (ray >= P.nrays) return;
@@ -124,16 +145,16 @@ __global__ __launch_bounds__(64 * kRayWaves) void find_ray_kernel(RayParams P) {
         double t;
         if (dir == 0) {
           long xv = i + base0;
-          t = RT(xv, c_value) + tbp(P.M, last_x, (double)c_value, last_y, (double)xv, P.dnx, sg);
+          t = RT(xv, c_value) + tbp(P.M, ms, last_x, (double)c_value, last_y, (double)xv, P.dnx, sg);
         } else if (dir == 1) {
           long xc = base0 + i, yc = -xc + c_value;
-          t = RT(yc, xc) + tbp(P.M, last_x, (double)xc, last_y, (double)yc, P.dnx, sg);
+          t = RT(yc, xc) + tbp(P.M, ms, last_x, (double)xc, last_y, (double)yc, P.dnx, sg);
         } else if (dir == 2) {
           long yv = i + base0;
-          t = RT(c_value, yv) + tbp(P.M, last_x, (double)yv, last_y, (double)c_value, P.dnx, sg);
+          t = RT(c_value, yv) + tbp(P.M, ms, last_x, (double)yv, last_y, (double)c_value, P.dnx, sg);
         } else {
           long xc = base0 + i, yc = xc + c_value;
-          t = RT(yc, xc) + tbp(P.M, last_x, (double)xc, last_y, (double)yc, P.dnx, sg);
+          t = RT(yc, xc) + tbp(P.M, ms, last_x, (double)xc, last_y, (double)yc, P.dnx, sg);
         }
         TT[i] = t;
       }
@@ -213,7 +234,7 @@ __global__ __launch_bounds__(64 * kRayWaves) void find_ray_kernel(RayParams P) {
   for (long k0 = 0; k0 < npts - 1; k0 += G) {
     const long k = k0 + lane;
     double seg = 0.0;
-    if (k < npts - 1) seg = tbp(P.M, gld(rxo + k), gld(rxo + k + 1), gld(ryo + k), gld(ryo + k + 1), P.dnx, sg);
+    if (k < npts - 1) seg = tbp(P.M, ms, gld(rxo + k), gld(rxo + k + 1), gld(ryo + k), gld(ryo + k + 1), P.dnx, sg);
     const int m = (int)min((long)G, npts - 1 - k0);
     for (int l = 0; l < m; l++) tt += __shfl(seg, l, G);
   }
@@ -252,8 +273,19 @@ extern "C" hipError_t af_launch_rays(const af::RayParams* P, hipStream_t stream)
   const int G = ncand <= 16 ? 16 : ncand <= 32 ? 32 : 64;
   const int per_block = af::kRayWaves * (64 / G);
   const dim3 grid((P->nrays + per_block - 1) / per_block), block(64 * af::kRayWaves);
-  if (G == 16) hipLaunchKernelGGL(af::find_ray_kernel<16>, grid, block, 0, stream, *P);
-  else if (G == 32) hipLaunchKernelGGL(af::find_ray_kernel<32>, grid, block, 0, stream, *P);
-  else hipLaunchKernelGGL(af::find_ray_kernel<64>, grid, block, 0, stream, *P);
+  // material records, stiffness rows and the group table in LDS when they fit (the per-cell ids
+  // index the records)
+  const bool lds = P->M.mid && P->M.mtab && P->M.nmat <= af::kRayMatLds && P->M.nstab <= af::kRayStabLds &&
+                   361 * P->M.ncol <= af::kRayGtabLds;
+  if (G == 16) {
+    if (lds) hipLaunchKernelGGL((af::find_ray_kernel<16, true>), grid, block, 0, stream, *P);
+    else hipLaunchKernelGGL((af::find_ray_kernel<16, false>), grid, block, 0, stream, *P);
+  } else if (G == 32) {
+    if (lds) hipLaunchKernelGGL((af::find_ray_kernel<32, true>), grid, block, 0, stream, *P);
+    else hipLaunchKernelGGL((af::find_ray_kernel<32, false>), grid, block, 0, stream, *P);
+  } else {
+    if (lds) hipLaunchKernelGGL((af::find_ray_kernel<64, true>), grid, block, 0, stream, *P);
+    else hipLaunchKernelGGL((af::find_ray_kernel<64, false>), grid, block, 0, stream, *P);
+  }
   return hipGetLastError();
 }

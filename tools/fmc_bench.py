@@ -47,9 +47,12 @@ def main():
     xs = 8 + 16 * np.arange(256)
     rx = xs[:: 256 // a.receivers][: a.receivers]
     src = np.stack([xs[: a.sources].astype(float), np.zeros(a.sources)], 1)
-    # warm-up on a small batch (code objects, arena)
+    # warm-up (code objects, the travel arena, and the ray point buffers at the timed call's size:
+    # the context keeps them, as it does across the drop-in's calls)
     ctx.travel(dnx * rx[:2].astype(float), np.full(2, dnx * (n - 1)), first_slot=0, copy_out=False)
-    ctx.find_rays([0] * 8, src[:8], np.tile([float(rx[0]), float(n - 1)], (8, 1)), with_points=False)
+    nw = min(8192, a.sources * len(rx))
+    ctx.find_rays([0] * nw, np.tile(src, (nw // len(src) + 1, 1))[:nw],
+                  np.tile([float(rx[0]), float(n - 1)], (nw, 1)), with_points=False)
     t0 = time.perf_counter()
     ctx.travel(dnx * rx.astype(float), np.full(len(rx), dnx * (n - 1)), first_slot=0, copy_out=False)
     t1 = time.perf_counter()
