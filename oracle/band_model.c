@@ -226,7 +226,7 @@ int oband_travel(double scx, double scz, int nnz, int nnx, const double *veln, c
         for (long i = 0; i < (long)nnz * nnx; i++) h.nsts[i] = -1;
         /* rebuild the reference hand-over into the heap (row-major addtree order) */
         memset(ttn, 0, sizeof(double) * (size_t)nnz * nnx);
-        if (!have_b) { fprintf(stderr, "exact_r needs band stages off\n"); }
+        if (have_b) { fprintf(stderr, "exact_r needs band stages off\n"); }
         handover(&hprev_keep, pisz, pisx, &h, isz, isx);
         loopcfg_t ce = c;
         ce.tstop = exact_r * dnx / vmax;

@@ -499,6 +499,41 @@ def test_sharded_contexts_bit_identical(A, monkeypatch):
                 np.testing.assert_array_equal(a, b)
 
 
+@pytest.mark.parametrize("n", [61, 81])
+def test_many_materials_paths(ctx, envelope, n):
+    """Models past the kernels' LDS material tables: per-cell random orientations give n^2 distinct
+    materials — 3 721 (> 256: the band kernel reads the model arrays, the ray tracer the per-cell
+    ids and records from HBM) and 6 561 (> 4 096: no material ids at all).
+      * field vs the CPU band model (oracle/band_model.c: the same band-synchronous reformulation,
+        same band width, near-source schedule and exact prefix): the device arithmetic, <= 1e-9;
+      * field vs the heap oracle: the reformulation's error on this (extreme) model, measured equal
+        to the CPU band model's own (1.16e-2 / 1.2e-4 at n = 61): <= 2.5e-2 max, 4e-4 mean;
+      * a ray through the GPU field vs the oracle's on the same field: <= 1e-12."""
+    rng = np.random.default_rng(n)
+    dnx = 1e-3
+    veln = rng.uniform(0.0, 180.0, (n, n))
+    velpn = np.zeros((n, n), dtype=np.int64)
+    vm = 1.0 + 0.2 * rng.random((n, n))
+    sd = W.stif_field(n, n)
+    vt = W.default_table()
+    sx, sz = 17, 23
+    ctx.set_model(veln, velpn, vm, sd, vt, vt, dnx)
+    ctx.travel([dnx * sx], [dnx * sz], copy_out=False)
+    T = ctx.get_field(0, 1)
+    B, _ = O.band_travel(dnx * sx, dnx * sz, veln, velpn, vm, sd, vt, vt, ctx.get_option("vmax"),
+                         cdelta=ctx.get_option("cdelta"), exact_init=True, r0=ctx.get_option("r0"),
+                         exact_r=ctx.get_option("exact_r"), dnx=dnx)
+    dm = float(np.max(np.abs(T - B) / np.maximum(B, 1e-300)))
+    envelope["many_materials_vs_band_model_%d" % n] = dm
+    assert dm <= 1e-9, (n, dm)
+    R = O.travel(dnx * sx, dnx * sz, veln, velpn, vm, sd, vt, vt, dnx=dnx)
+    _check_field(envelope, "many_materials_%d" % n, T, R, (sx, sz), tol=(2.5e-2, 4e-4))
+    t, lens, flags, rays = ctx.find_rays([0], [[n - 5, n - 3]], [[sx, sz]])
+    ox, oy, ot = O.find_ray(dnx, vt, [n - 5, n - 3], [sx, sz], T, veln, velpn, vm, sd, 1)
+    envelope["many_materials_ray_%d" % n] = float(abs(t[0] - ot) / ot)
+    assert int(lens[0]) == len(ox) and abs(t[0] - ot) <= EXACT * ot, (n, t[0], ot, int(lens[0]), len(ox))
+
+
 def test_empty_and_degenerate_requests(A, ctx, envelope):
     """Edge cases of the drop-in surface: no selected sources, no ray pairs, a 1-column grid, a
     source outside the grid (reference: IndexError-like failure -> the C-ABI's argument error)."""
