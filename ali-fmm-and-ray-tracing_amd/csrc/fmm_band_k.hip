@@ -68,6 +68,9 @@ constexpr int kHash = 1 << kHashLog;
 #ifndef AF_CLAIM_SPREAD
 #define AF_CLAIM_SPREAD 1
 #endif
+#ifndef AF_DIAG_DBL
+#define AF_DIAG_DBL 0
+#endif
 #ifndef AF_PROF_FBWAIT
 #define AF_PROF_FBWAIT 0
 #endif
@@ -800,7 +803,16 @@ __global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
       if (interior) nb.load(T, nz, nx, z, x);
       else load_nb(nb, T, eprv, cells + 2 * ecells, g, z, x);
       const CellMat cm = band_mat<LDSMAT>(M, sh->mat, sh->stab, R.mv, z, x);
+#if AF_DIAG_DBL  // diagnostic: a second, opaque update() per cell (its marginal cost), same results
+      NbFieldT nb2 = nb;
+      double d0 = nb.t0;
+      asm volatile("" : "+v"(d0));
+      nb2.t0 = d0;
+      const double v2 = update(nb2, M, cm, z, x, dnx_e, nz, nx);
+      eval_done(e, update(nb, M, cm, z, x, dnx_e, nz, nx) + 0.0 * v2);
+#else
       eval_done(e, update(nb, M, cm, z, x, dnx_e, nz, nx));
+#endif
     }
     AF_TICK(3)
     // ---- P4b: fouds18_A() over the compacted fallback list, in staged rounds ----
