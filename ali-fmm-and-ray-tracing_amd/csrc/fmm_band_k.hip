@@ -56,14 +56,18 @@ constexpr int kThreads = AF_THREADS;
 constexpr int kWaves = kThreads / 64;
 // LDS heads of the lists (longer lists spill to the global arrays, HList): sized to the LDS left
 // (157 KB of 160), the close set to the C4 peak (3 295 live slots of one member at K = 2): 2560 / 1536
-// -> 3328 / 1792 took the C4 band from 416 to 405 ms
+// -> 3328 / 1792 took the C4 band from 416 to 405 ms, the accepted list 1024 -> 1536 (the claim
+// then stays in LDS and tile-sorted in the widest steps) to 388 ms; 161 KB of LDS in all
 #ifndef AF_LCAP
 #define AF_LCAP 3328
 #endif
 #ifndef AF_ECAP
 #define AF_ECAP 1792
 #endif
-constexpr int kLcap = AF_LCAP, kAcap = 1024, kEcap = AF_ECAP, kBcap = 512, kDcap = 512, kRcap = 1024;
+#ifndef AF_ACAP
+#define AF_ACAP 1536
+#endif
+constexpr int kLcap = AF_LCAP, kAcap = AF_ACAP, kEcap = AF_ECAP, kBcap = 512, kDcap = 512, kRcap = 1024;
 constexpr int kHashLog = 13;
 constexpr int kHash = 1 << kHashLog;
 #ifndef AF_CLAIM_U
