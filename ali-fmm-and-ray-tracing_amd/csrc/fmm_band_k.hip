@@ -84,6 +84,9 @@ constexpr int kHash = 1 << kHashLog;
 #ifndef AF_DIAG_DBL
 #define AF_DIAG_DBL 0
 #endif
+#ifndef AF_PROF_SPILL
+#define AF_PROF_SPILL 0
+#endif
 #ifndef AF_PROF_FBWAIT
 #define AF_PROF_FBWAIT 0
 #endif
@@ -470,7 +473,7 @@ __global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
     const long long tdr = prof ? wall_clock64() : 0;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores have completed
     __syncthreads();
-#if !AF_PROF_FBWAIT
+#if !AF_PROF_FBWAIT && !AF_PROF_SPILL
     AF_SUBT(3, tdr)
 #endif
     const long long tx1 = prof ? wall_clock64() : 0;
@@ -974,6 +977,10 @@ __global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
       ls[1] += nA;
       ls[2] += nE;
       lmax = max(lmax, (long long)hi);
+#if AF_PROF_SPILL  // diagnostic: sub[3] counts the steps whose lists outgrew their LDS heads
+      sub[3] += (sh->nA > kAcap ? 1 : 0) + (nE > kEcap ? 1000 : 0) + (hi > kLcap ? 1000000 : 0) +
+                (nItems > kHashItems ? 1000000000LL : 0);
+#endif
     }
     steps++;
     __syncthreads();

@@ -46,7 +46,7 @@ def main():
         prof.update({k: round(p[10 + i] / 100.0 / st, 2) for i, k in enumerate(SUB)})
         # list sizes of member 0: mean live close set, accepted and claimed cells per step, max close-set high-water
         prof.update({"live_mean": round(p[6] / st, 1), "acc_mean": round(p[7] / st, 1), "claimed_mean": round(p[8] / st, 1),
-                     "close_hi_max": int(p[9])})
+                     "close_hi_max": int(p[9]), "sub3_raw": int(p[13]), "steps": st})
         out[str(ns)] = {"k": int(ctx.get_option("last_k")), "band_ms": round(best, 1), "init_ms": round(ti, 1),
                         "fields": h.hexdigest()[:16], "us_per_step": prof}
     print(json.dumps(out), flush=True)
