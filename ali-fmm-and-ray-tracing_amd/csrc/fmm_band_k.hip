@@ -112,7 +112,14 @@ constexpr int kClaimU = AF_CLAIM_U;  // claim items per lane per pass
 #endif
 constexpr int kAccU = AF_ACC_U;  // close-set entries per lane per accept pass (2 and 4 measured slower)
 constexpr int kHashItems = 6144;  // claim items deduplicated in the LDS hash (more: global stamps)
-constexpr int kStabLds = 64, kPtabLds = 722, kMatLds = 256;
+// model tables staged in LDS (more materials / stiffness rows: the model arrays are read instead)
+#ifndef AF_MATLDS
+#define AF_MATLDS 256
+#endif
+#ifndef AF_STABLDS
+#define AF_STABLDS 64
+#endif
+constexpr int kStabLds = AF_STABLDS, kPtabLds = 722, kMatLds = AF_MATLDS;
 constexpr int kDirty = (int)0x80000000u;  // close-set slot: committed last step (edge cell)
 constexpr int kCell = 0x7fffffff;
 
