@@ -111,7 +111,10 @@ constexpr int kClaimU = AF_CLAIM_U;  // claim items per lane per pass
 #define AF_ACC_U 1
 #endif
 constexpr int kAccU = AF_ACC_U;  // close-set entries per lane per accept pass (2 and 4 measured slower)
-constexpr int kHashItems = 6144;  // claim items deduplicated in the LDS hash (more: global stamps)
+#ifndef AF_HASH_ITEMS
+#define AF_HASH_ITEMS 6144
+#endif
+constexpr int kHashItems = AF_HASH_ITEMS;  // claim items deduplicated in the LDS hash (more: global stamps)
 // model tables staged in LDS (more materials / stiffness rows: the model arrays are read instead)
 #ifndef AF_MATLDS
 #define AF_MATLDS 256
