@@ -40,6 +40,12 @@ _EARLY_MSG = "Travel time to receiver increasing: Finishing ray early"
 # compact RayStore (ALI_FMM.rays), e.g. for the 4096² full-matrix capture (86 GB per dense array).
 ray_dense_limit_bytes = 4 << 30
 
+# How update_parallel() returns the fields of several GPUs: "d2h" — every GPU copies its own fields
+# into the caller's stack at once (one host thread per GPU; host bandwidth adds up over the PCIe
+# links); "rccl" — the fields are first gathered onto GPU 0 over xGMI (alifmm_gather_fields, the
+# counterpart of the reference's queue2 result return :3610, :3659), then copied out from there.
+result_return = "d2h"
+
 
 # ------------------------------------------------------------------------------------------------
 def _device_map():
@@ -78,40 +84,47 @@ def _prep_model(veln, velpn, vel_map, stif_den, group_tab, phase_tab):
     return veln, velpn, vel_map, stif, gt, pt
 
 
+# The resident model is keyed on a digest of the FULL content of every model argument, computed on
+# every call (the reference recomputes from its arguments on every call, :1463): an in-place edit
+# of any cell, or new data at a recycled address, always reaches the GPU.  xxh3 runs at ~8 GB/s
+# here, ~0.15 s for the C4 model (4096^2, stiffness 0.67 GB); the class methods hash once per call
+# for all their GPUs.  trust_model_identity = True opts into an identity cache (object, buffer,
+# shape, strides) that skips the hash when the same arrays come back — only valid for callers that
+# never edit a model array in place.
+trust_model_identity = False
+_identity_cache = {}
+
+
 def _identity(a):
-    """Cheap identity of a model argument: the object, its buffer, shape, dtype and strides, plus a
-    digest of a strided sample of ~4096 elements (so that an in-place edit of a sampled element,
-    or of the first or last row, is noticed without hashing the whole array)."""
     if a is None:
         return None
     if not isinstance(a, np.ndarray):
         return ("obj", _digest(np.asarray(a)))
-    flat = a.reshape(-1) if a.flags.c_contiguous else np.ravel(a)
-    step = max(1, flat.size // 4096)
-    edge = min(flat.size, a.shape[-1] if a.ndim else 1)
-    return (id(a), a.__array_interface__["data"][0], a.shape, a.dtype.str, a.strides,
-            _digest(flat[::step], flat[:edge], flat[flat.size - edge:]))
-
-
-# identity of the model arguments -> full content digest: module-level calls (travel, find_ray, ...)
-# pass the same arrays over and over; each pass would otherwise re-hash up to ~1 GB (C4 stiffness)
-_digest_cache = {}
+    return (id(a), a.__array_interface__["data"][0], a.shape, a.dtype.str, a.strides)
 
 
 def _model_digest(arrays):
+    if not trust_model_identity:
+        return _digest(*_prep_model(*arrays))
     ident = tuple(_identity(a) for a in arrays)
-    d = _digest_cache.get(ident)
+    d = _identity_cache.get(ident)
     if d is None:
         d = _digest(*_prep_model(*arrays))
-        if len(_digest_cache) >= 8:
-            _digest_cache.pop(next(iter(_digest_cache)))
-        _digest_cache[ident] = d
+        if len(_identity_cache) >= 8:
+            _identity_cache.pop(next(iter(_identity_cache)))
+        _identity_cache[ident] = d
     return d
 
 
-def _load_model(ctx, veln, velpn, vel_map, stif_den, group_tab, phase_tab, dnx, dnz, gox=0.0, goz=0.0):
+def _model_key(veln, velpn, vel_map, stif_den, group_tab, phase_tab, dnx, dnz, gox=0.0, goz=0.0):
+    return (_model_digest((veln, velpn, vel_map, stif_den, group_tab, phase_tab)), float(dnx), float(dnz),
+            float(gox), float(goz))
+
+
+def _load_model(ctx, veln, velpn, vel_map, stif_den, group_tab, phase_tab, dnx, dnz, gox=0.0, goz=0.0, key=None):
     args = (veln, velpn, vel_map, stif_den, group_tab, phase_tab)
-    key = (_model_digest(args), float(dnx), float(dnz), float(gox), float(goz))
+    if key is None:
+        key = _model_key(*args, dnx, dnz, gox, goz)
     if ctx.model_key != key:
         veln, velpn, vel_map, stif, gt, pt = _prep_model(*args)
         ctx.set_model(veln, velpn, vel_map, stif, gt, pt, dnx, dnz, gox, goz, key=key)
@@ -308,6 +321,11 @@ def ray_time(ray_x, ray_y, dnx, subgrid_size, velocity_dat, veln, velpn, vel_map
     return t
 
 
+def _fine_shape(veln, subgrid_size):
+    sg = int(subgrid_size)
+    return (sg * (np.shape(veln)[0] - 1) + 1, sg * (np.shape(veln)[1] - 1) + 1)
+
+
 def _cell(a, iz, ix):
     return np.asarray(a)[iz, ix]
 
@@ -369,6 +387,7 @@ class ALI_FMM:
         self.ray_paths_x = self.ray_paths_y = self.ray_len = None
         self.rays = None  # RayStore of the last find_all_TTF_rays* call (compact layout)
         self._ctxs = {}
+        self._comms = {}  # device tuple -> _alifmm.Comm (result_return = "rccl")
 
     @classmethod
     def _check_stiffness(cls, stif_den):
@@ -408,25 +427,36 @@ class ALI_FMM:
         n = max(1, min(int(n_threads), len(_device_map())))
         return list(range(n))
 
-    def _fields(self, veln, velpn, vel_map, stif_den, subgrid_size, idx, devices, copy_out=True, slot_of=None):
-        """Fields of the sources `idx`, block-distributed over `devices` (one host thread per GPU)."""
+    def _fields(self, veln, velpn, vel_map, stif_den, subgrid_size, idx, devices, copy_out=True, dest=None):
+        """Fields of the sources `idx`, block-distributed over `devices` (one host thread per GPU).
+
+        copy_out: each GPU's fields come back to the host; with `dest` (an (nsrc, fz, fx) float64
+        C-contiguous array) straight into dest[i] (one copy, no intermediate stack), else as
+        per-source arrays.  copy_out=False leaves them resident (results carry (device, slot))."""
         idx = list(idx)
         parts = sharding.deal(idx, len(devices))
         results = {}
         errors = []
+        key = _model_key(veln, velpn, vel_map, stif_den, self.velocity_dat, self.phase_vel, self.dnx, self.dnz,
+                         self.gox, self.goz)
 
         def work(dev, ids):
             try:
                 ctx = self._ctx(dev)
                 _load_model(ctx, veln, velpn, vel_map, stif_den, self.velocity_dat, self.phase_vel, self.dnx,
-                            self.dnz, self.gox, self.goz)
+                            self.dnz, self.gox, self.goz, key=key)
                 if not ids:
                     return
                 x = np.array([float(self.scx[i]) for i in ids])
                 z = np.array([float(self.scz[i]) for i in ids])
-                out = ctx.travel(x, z, subgrid=int(subgrid_size), first_slot=0, copy_out=copy_out)
-                if copy_out:  # the host has the fields: free their device slots
-                    ctx.release_fields()
+                ctx.travel(x, z, subgrid=int(subgrid_size), first_slot=0, copy_out=False)
+                out = None
+                if copy_out:
+                    if dest is not None:
+                        ctx.copy_fields_into(0, dest, ids, int(subgrid_size))
+                    else:
+                        out = ctx.copy_fields(0, len(ids), int(subgrid_size))[0]
+                    ctx.release_fields()  # the host has the fields: free their device slots
                 for k, i in enumerate(ids):
                     results[i] = (dev, k, None if out is None else out[k])
             except Exception as e:  # surfaced below
@@ -457,12 +487,9 @@ class ALI_FMM:
         if type(sources) == type(None):
             sources = np.ones(len(self.scx))
         idx = [i for i in range(self.nsrc) if sources[i] == 1]
-        res = self._fields(veln, velpn, self.vel_map, stif_den, subgrid_size, idx, [0])
-        ctx = self._ctx(0)
-        fz, fx = ctx.field_shape(subgrid_size)
-        travel_time_field = np.zeros((self.nsrc, fz, fx))
-        for i, (_, _, T) in res.items():
-            travel_time_field[i] = T
+        # the caller's stack is the copy's destination (one copy per field, no intermediate stack)
+        travel_time_field = np.zeros((self.nsrc,) + _fine_shape(veln, subgrid_size))
+        self._fields(veln, velpn, self.vel_map, stif_den, subgrid_size, idx, [0], dest=travel_time_field)
         return travel_time_field
 
     def update_parallel(self, veln, velpn, vel_map=None, stif_den=None, subgrid_size=1, sources=None, n_threads=2,
@@ -480,16 +507,43 @@ class ALI_FMM:
         if type(sources) == type(None):
             sources = np.ones(len(self.scx), dtype=int)
         idx = [i for i in range(self.nsrc) if sources[i] == 1]
-        res = self._fields(veln, velpn, self.vel_map, stif_den, subgrid_size, idx, self._devices(n_threads))
-        if low_mem:
-            for i, (_, _, T) in res.items():
-                np.save("temp_TTF_" + str(i) + ".npy", T)
+        devices = self._devices(n_threads)
+        if low_mem:  # one field at a time from its GPU to its file: host memory stays at one field
+            res = self._fields(veln, velpn, self.vel_map, stif_den, subgrid_size, idx, devices, copy_out=False)
+            try:
+                for i, (dev, slot, _) in sorted(res.items()):
+                    np.save("temp_TTF_" + str(i) + ".npy", self._ctx(dev).get_field(slot, int(subgrid_size)))
+            finally:
+                for d in devices:
+                    self._ctx(d).release_fields()
             return None
-        fz, fx = self._ctx(0).field_shape(subgrid_size)
-        travel_time_field = np.zeros((self.nsrc, fz, fx))
-        for i, (_, _, T) in res.items():
-            travel_time_field[i] = T
+        travel_time_field = np.zeros((self.nsrc,) + _fine_shape(veln, subgrid_size))
+        if result_return == "rccl":
+            self._fields(veln, velpn, self.vel_map, stif_den, subgrid_size, idx, devices, copy_out=False)
+            self._gather_into(devices, sharding.deal(idx, len(devices)), int(subgrid_size), travel_time_field)
+        else:
+            self._fields(veln, velpn, self.vel_map, stif_den, subgrid_size, idx, devices, dest=travel_time_field)
         return travel_time_field
+
+    def _gather_into(self, devices, parts, sg, dest):
+        """RCCL gather of the resident fields of every device onto devices[0] (one communicator per
+        device set, kept), then one copy from there into dest rows parts[r][k]."""
+        key = tuple(devices)
+        comm = self._comms.get(key)
+        if comm is None:
+            comm = _alifmm.Comm.all([self._ctx(d) for d in devices])
+            self._comms[key] = comm
+        counts = [len(p) for p in parts]
+        off = _alifmm.gather_layout(counts)
+        try:
+            comm.gather(0, sg, [0] * len(devices), counts, dst_slot=0)
+            root = self._ctx(devices[0])
+            for r, p in enumerate(parts):
+                if p:
+                    root.copy_fields_into(int(off[r]), dest, p, sg)
+        finally:
+            for d in devices:
+                self._ctx(d).release_fields()
 
     def update_i(self, source_i, veln, velpn, vel_map, stif_den=None, subgrid_size=1):
         """Travel-time field of one source (reference :4053-4088)."""

@@ -3,9 +3,11 @@
 The library is built in-tree (csrc/Makefile -> lib/libalifmm.so).  There is no CPU fallback:
 if the library or a GPU is missing, every entry point raises AlifmmError.
 """
+import atexit
 import ctypes
 import os
 import threading
+import weakref
 
 import numpy as np
 
@@ -14,7 +16,9 @@ LIB_PATH = os.environ.get("ALIFMM_LIB") or os.path.join(HERE, "lib", "libalifmm.
 
 _d, _i, _l, _p = ctypes.c_double, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p
 _lib = None
+_lib_closed = False
 _lock = threading.Lock()
+_live = weakref.WeakSet()  # open Contexts (shutdown() destroys them)
 
 
 class AlifmmError(RuntimeError):
@@ -47,6 +51,8 @@ def _load():
     with _lock:
         if _lib is not None:
             return _lib
+        if _lib_closed:
+            raise AlifmmError("libalifmm.so was unloaded by shutdown() (interpreter exit)")
         if not os.path.exists(LIB_PATH):
             raise AlifmmError("libalifmm.so not built (%s); run `make -C %s/csrc` or __graft_entry__.build()"
                               % (LIB_PATH, HERE))
@@ -76,6 +82,12 @@ def _load():
             "alifmm_local_ops": (_i, [_p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i,
                                       _p]),
             "alifmm_fouds18_band": (_i, [_p, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _p]),
+            "alifmm_comm_unique_id": (_i, [_p]),
+            "alifmm_comm_init_rank": (_i, [_p, _i, _i, _p, _p]),
+            "alifmm_comm_init_all": (_i, [_p, _i, _p]),
+            "alifmm_comm_destroy": (_i, [_p]),
+            "alifmm_comm_last_error": (ctypes.c_char_p, [_p]),
+            "alifmm_gather_fields": (_i, [_p, _i, _i, _p, _p, _i, _p]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -87,6 +99,36 @@ def _load():
 
 def lib():
     return _load()
+
+
+def shutdown():
+    """Destroy every open context, then unload the library — at interpreter exit (atexit), while
+    the HIP runtime and anything attached to it (rocprofv3's tool) are still intact.
+
+    Why: the library's HIP module destructor (__hip_module_dtor -> __hipUnregisterFatBinary, which
+    hipcc registers with __cxa_atexit when the library is loaded) otherwise runs from exit() AFTER
+    handlers registered later — rocprofv3's finalisation is registered at the first HIP call, after
+    the library was loaded — and calls into a torn-down runtime (the SIGSEGV at exit of round 2's
+    profiled runs).  dlclose() runs the destructor now, and contexts destroyed here release their
+    streams, events, pinned buffers and device memory in order instead of leaving them to the
+    runtime's own static teardown."""
+    global _lib, _lib_closed
+    live = list(_live)
+    for c in [c for c in live if isinstance(c, Comm)] + [c for c in live if not isinstance(c, Comm)]:
+        try:
+            c.close()
+        except Exception:
+            pass
+    _default.clear()
+    with _lock:
+        L, _lib, _lib_closed = _lib, None, True
+    if L is not None:
+        import _ctypes
+
+        _ctypes.dlclose(L._handle)
+
+
+atexit.register(shutdown)
 
 
 def device_count():
@@ -126,15 +168,22 @@ class Context:
                               % (device, rc))
         self._h = h
         self.device = device
+        _live.add(self)
         self._model_key = None
         self.shape = None
         for k, v in (("cdelta", cdelta), ("r0", r0), ("batch", batch)):
             if v is not None:
                 self.set_option(k, v)
-        # experiments: ALIFMM_OPT_<NAME>=value sets alifmm_set_option(name, value) on every context
+        # experiments (tools/*.sh): ALIFMM_OPT_<NAME>=value sets alifmm_set_option(name, value) on
+        # every context (README "Options"); a bad name or value is reported and ignored, never fatal
         for k, v in os.environ.items():
             if k.startswith("ALIFMM_OPT_"):
-                self.set_option(k[len("ALIFMM_OPT_"):].lower(), float(v))
+                try:
+                    self.set_option(k[len("ALIFMM_OPT_"):].lower(), float(v))
+                except (ValueError, AlifmmError) as e:
+                    import warnings
+
+                    warnings.warn("ignoring %s=%r: %s" % (k, v, e))
 
     def _chk(self, rc, what):
         if rc != 0:
@@ -142,9 +191,9 @@ class Context:
             raise AlifmmError("%s failed (rc=%d): %s" % (what, rc, msg.decode() if msg else ""))
 
     def close(self):
-        if getattr(self, "_h", None) is not None and self._h.value:
-            lib().alifmm_ctx_destroy(self._h)
-            self._h = None
+        if getattr(self, "_h", None) is not None and self._h.value and _lib is not None:
+            _lib.alifmm_ctx_destroy(self._h)
+        self._h = None
 
     def __del__(self):
         try:
@@ -230,6 +279,31 @@ class Context:
         self._chk(lib().alifmm_copy_fields(self._h, int(first_slot), int(n), _ptr(out), int(dst_kind), ctypes.byref(g)),
                   "copy_fields")
         return out, g.value
+
+    def copy_fields_into(self, first_slot, dest, rows, subgrid, dst_kind=0):
+        """Resident slots first_slot, first_slot+1, ... straight into dest[rows[0]], dest[rows[1]], ...
+        of a caller-visible C-contiguous float64 (n, fnz, fnx) stack: one copy per field, no
+        intermediate array (runs of consecutive rows go in one alifmm_copy_fields call).
+        dst_kind 0: through the pinned staging ring; 3: DMA straight into dest (registered for the
+        copy).  Returns the bytes copied."""
+        if not (isinstance(dest, np.ndarray) and dest.dtype == np.float64 and dest.flags.c_contiguous
+                and dest.ndim == 3):
+            raise ValueError("dest must be a C-contiguous float64 (n, fnz, fnx) array")
+        if dest.shape[1:] != self.field_shape(subgrid):
+            raise ValueError("dest fields %s, resident fields %s" % (dest.shape[1:], self.field_shape(subgrid)))
+        rows = [int(r) for r in rows]
+        if rows and (min(rows) < 0 or max(rows) >= dest.shape[0]):
+            raise IndexError("copy_fields_into: row outside dest")
+        g = ctypes.c_double(0)
+        k = 0
+        while k < len(rows):
+            e = k + 1
+            while e < len(rows) and rows[e] == rows[e - 1] + 1:
+                e += 1
+            self._chk(lib().alifmm_copy_fields(self._h, int(first_slot + k), e - k, dest[rows[k]].ctypes.data,
+                                               int(dst_kind), ctypes.byref(g)), "copy_fields")
+            k = e
+        return len(rows) * dest[0].nbytes
 
     def copy_fields_to_device(self, first_slot, n, dev_ptr):
         """Copy resident fields into device memory of this GPU at dev_ptr (e.g. a torch tensor's
@@ -338,6 +412,70 @@ class Context:
         self._chk(lib().alifmm_fouds18_band(self._h, n, pz, px, _ptr(ttn), _ptr(nsts), *[_ptr(a) for a in args],
                                             int(quant), _ptr(out)), "fouds18_band")
         return out
+
+
+class Comm:
+    """RCCL communicator over contexts on distinct GPUs (include/alifmm.h alifmm_comm_*): gathers
+    resident fields onto one GPU over xGMI.  Comm.all(ctxs): one process driving every context;
+    Comm.rank(ctx, nranks, rank, uid): one process per GPU, uid = Comm.unique_id() made by one rank
+    and shared by the caller (e.g. torch.distributed.broadcast_object_list)."""
+
+    def __init__(self, handle, ctxs):
+        self._h = handle
+        self.ctxs = list(ctxs)
+        _live.add(self)
+
+    @staticmethod
+    def unique_id():
+        buf = ctypes.create_string_buffer(128)
+        if lib().alifmm_comm_unique_id(buf) != 0:
+            raise AlifmmError("alifmm_comm_unique_id failed (RCCL unavailable)")
+        return buf.raw
+
+    @classmethod
+    def all(cls, ctxs):
+        arr = (ctypes.c_void_p * len(ctxs))(*[c._h.value for c in ctxs])
+        h = ctypes.c_void_p()
+        ctxs[0]._chk(lib().alifmm_comm_init_all(arr, len(ctxs), ctypes.byref(h)), "comm_init_all")
+        return cls(h, ctxs)
+
+    @classmethod
+    def rank(cls, ctx, nranks, rank, uid):
+        if len(uid) != 128:
+            raise ValueError("RCCL unique id must be 128 bytes")
+        h = ctypes.c_void_p()
+        ctx._chk(lib().alifmm_comm_init_rank(ctx._h, int(nranks), int(rank), ctypes.create_string_buffer(uid, 128),
+                                             ctypes.byref(h)), "comm_init_rank")
+        return cls(h, [ctx])
+
+    def gather(self, root, subgrid, first_slot, count, dst_slot=0):
+        """Rank r's slots first_slot[r] .. +count[r]-1 -> the root's slots dst_slot + sum(count[:r]) + i.
+        Every rank passes the same lists.  Returns the wall time [ms]."""
+        fs = np.ascontiguousarray(first_slot, dtype=np.int32)
+        cn = np.ascontiguousarray(count, dtype=np.int32)
+        ms = ctypes.c_double(0)
+        rc = lib().alifmm_gather_fields(self._h, int(root), int(subgrid), _ptr(fs), _ptr(cn), int(dst_slot),
+                                        ctypes.byref(ms))
+        if rc != 0:
+            msg = lib().alifmm_comm_last_error(self._h)
+            raise AlifmmError("gather_fields failed (rc=%d): %s" % (rc, msg.decode() if msg else ""))
+        return ms.value
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value and _lib is not None:
+            _lib.alifmm_comm_destroy(self._h)
+        self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def gather_layout(counts):
+    """Root slot offset of every rank's first field in alifmm_gather_fields (rank order)."""
+    return np.concatenate(([0], np.cumsum(np.asarray(counts, dtype=np.int64))))[:-1]
 
 
 _default = {}

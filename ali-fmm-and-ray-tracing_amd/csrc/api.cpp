@@ -19,100 +19,8 @@
 #include <vector>
 
 #include "../../include/alifmm.h"
+#include "context.h"
 #include "kernels.h"
-
-namespace {
-
-struct Field {
-  double* d = nullptr;
-  size_t bytes = 0;  // the field (fnz x fnx doubles)
-  size_t alloc = 0;  // allocated: the field + the K-member band kernel's edge buffers after it
-  int sg = 0, nz = 0, nx = 0;
-  int64_t steps[4] = {0, 0, 0, 0};
-  int64_t sweeps = 0;
-  int64_t prof[14] = {};  // band profile: 6 phase ticks, 3 list sums, max close, 4 sub-phase ticks
-};
-
-struct Arena {  // per-chunk scratch, reused across calls
-  int nsrc = 0;
-  long cells = 0, capL = 0, capC = 0, capS = 0;
-  int* S = nullptr;
-  int* own = nullptr;
-  int* lists = nullptr;    // Lin | FS | A | L | C | Cp | D | Rx | Bl | Bp per source
-  double* dlists = nullptr;  // Lt | V | Dv per source
-  int K = 0;                 // K-member kernel: members the rim lists are sized for
-  long capR = 0, ecells = 0;
-  int* rimc = nullptr;       // K-member kernel: rim lists [src][K][2][capR]
-  double* rimt = nullptr;
-  af::KX* kx = nullptr;      // K-member kernel: exchange blocks
-  double* Ts = nullptr;  // stage grids (travel_finer_grid), 2 per source
-  int* Ss = nullptr;
-  af::BandSrc* srcs = nullptr;
-  af::HandoverOut* ho = nullptr;
-  af::InitJob* jobs = nullptr;
-  double* dscx = nullptr;
-  double* dscz = nullptr;
-};
-
-}  // namespace
-
-struct alifmm_ctx {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  hipStream_t fill = nullptr;  // field initialisation, overlapped with the source-init kernel
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-  hipEvent_t ev_fill = nullptr;
-  std::string err;
-  // model
-  bool have_model = false;
-  int nz0 = 0, nx0 = 0, ncol = 0;
-  double dnx = 0, dnz = 0, gox = 0, goz = 0, vmax = 0;
-  double* d_veln = nullptr;
-  double* d_vm = nullptr;
-  int* d_velpn = nullptr;
-  int* d_sidx = nullptr;
-  double* d_stab = nullptr;
-  int nstab = 0;
-  int* d_mid = nullptr;
-  unsigned char* d_mid8 = nullptr;  // the same ids as bytes when there are <= 256 materials
-  af::MatRec* d_mtab = nullptr;
-  double* d_mslo = nullptr;  // fouds18_A() slownesses per material (DevModel::mslo)
-  int nmat = 0;
-  double* d_gtab = nullptr;
-  double* d_ptab = nullptr;
-  // options
-  double cdelta = 0.5, r0 = 40.0;
-  int exact_r = 20;
-  int batch = 256;
-  int prof = 0;
-  int members = 0;     // band kernel: workgroups per source (0: as many as the device fits, <= 16)
-  int stripe_log = 0;  // band kernel: stripe width log2 (0: 6 for K <= 4, 4 for K >= 8)
-  int last_k = 0;      // members per source of the last band launch
-  int n_cu = 0;
-  long cap_scale = 1;
-  // state
-  std::vector<Field> fields;
-  Arena arena;
-  double t_init = 0, t_band = 0, t_total = 0;
-  // packed points of the last alifmm_find_rays(ray_xy = NULL, ray_xy_cap = ALIFMM_KEEP_RAYS) call,
-  // per ray in the caller's order, until alifmm_take_rays() copies them out
-  std::vector<std::vector<double>> kept_rays;
-  int64_t kept_pts = 0;
-  // ray-tracer work buffers, kept across alifmm_find_rays calls (sized for the largest chunk seen)
-  struct RayBufs {
-    size_t pts = 0;  // capacity of rx / ry in doubles
-    int rays = 0;    // capacity of the per-ray arrays
-    double *rx = nullptr, *ry = nullptr, *t = nullptr;
-    int *len = nullptr, *flags = nullptr;
-    af::RayJob* jobs = nullptr;
-    long long* off = nullptr;
-  } rb;
-  // pinned staging ring of alifmm_copy_fields (pageable destinations)
-  static constexpr int kPinBufs = 4;
-  static constexpr size_t kPinBytes = 32u << 20;
-  void* pin[kPinBufs] = {};
-  hipEvent_t pin_ev[kPinBufs] = {};
-};
 
 static void free_ray_bufs(alifmm_ctx* c) {
   auto& b = c->rb;
@@ -120,31 +28,6 @@ static void free_ray_bufs(alifmm_ctx* c) {
     if (p) (void)hipFree(p);
   b = alifmm_ctx::RayBufs();
 }
-
-static int fail(alifmm_ctx* c, int code, const char* fmt, ...) {
-  char buf[512];
-  va_list ap;
-  va_start(ap, fmt);
-  vsnprintf(buf, sizeof buf, fmt, ap);
-  va_end(ap);
-  if (c) c->err = buf;
-  return code;
-}
-
-#define HIPCHK(call)                                                                          \
-  do {                                                                                        \
-    hipError_t e_ = (call);                                                                   \
-    if (e_ != hipSuccess) return fail(ctx, ALIFMM_E_HIP, "%s: %s", #call, hipGetErrorString(e_)); \
-  } while (0)
-
-template <class T>
-static hipError_t dalloc(T** p, size_t n) {
-  return hipMalloc((void**)p, std::max<size_t>(n, 1) * sizeof(T));
-}
-static void dfree(void* p) {
-  if (p) (void)hipFree(p);
-}
-
 static void free_arena(Arena& a) {
   dfree(a.S); dfree(a.own); dfree(a.lists); dfree(a.dlists); dfree(a.Ts); dfree(a.Ss); dfree(a.srcs); dfree(a.ho); dfree(a.jobs);
   dfree(a.rimc); dfree(a.rimt); dfree(a.kx);
@@ -234,6 +117,7 @@ int alifmm_release_fields(alifmm_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   for (auto& f : ctx->fields) dfree(f.d);
   ctx->fields.clear();
+  free_ray_bufs(ctx);  // the ray tracer's point buffers (chunk x max_pts per coordinate) go with the fields
   return ALIFMM_OK;
 }
 
@@ -503,7 +387,7 @@ static int ensure_arena(alifmm_ctx* ctx, int nsrc, long cells, long capL, long c
   return ALIFMM_OK;
 }
 
-static int ensure_field(alifmm_ctx* ctx, int slot, int sg, int fz, int fx, long extra_cells = 0) {
+int af_ensure_field(alifmm_ctx* ctx, int slot, int sg, int fz, int fx, long extra_cells) {
   if ((int)ctx->fields.size() <= slot) ctx->fields.resize(slot + 1);
   Field& f = ctx->fields[slot];
   const size_t bytes = (size_t)fz * fx * sizeof(double), need = bytes + (size_t)extra_cells * sizeof(double);
@@ -573,7 +457,7 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
   std::vector<af::BandSrc> hs(n);
   for (int i = 0; i < n; i++) {
     int slot = first_slot + i;
-    if ((rc = ensure_field(ctx, slot, sg, fz, fx, 2 * ecells))) return rc;  // + the edge buffers
+    if ((rc = af_ensure_field(ctx, slot, sg, fz, fx, 2 * ecells))) return rc;  // + the edge buffers
     af::BandSrc& b = hs[i];
     memset(&b, 0, sizeof b);
     b.T = ctx->fields[slot].d;
@@ -787,7 +671,7 @@ static void team_memcpy(char* dst, const char* src, size_t n, int nthreads) {
 }
 
 int alifmm_copy_fields(alifmm_ctx* ctx, int first_slot, int n, double* dst, int dst_kind, double* gbps) {
-  if (!ctx || n < 0 || first_slot < 0 || (n > 0 && !dst) || dst_kind < 0 || dst_kind > 2)
+  if (!ctx || n < 0 || first_slot < 0 || (n > 0 && !dst) || dst_kind < 0 || dst_kind > 3)
     return fail(ctx, ALIFMM_E_ARG, "copy_fields: bad args");
   if (n == 0) return ALIFMM_OK;
   if (first_slot + n > (int)ctx->fields.size()) return fail(ctx, ALIFMM_E_ARG, "copy_fields: slots out of range");
@@ -798,11 +682,21 @@ int alifmm_copy_fields(alifmm_ctx* ctx, int first_slot, int n, double* dst, int 
   HIPCHK(hipSetDevice(ctx->device));
   const auto t0 = std::chrono::steady_clock::now();
   char* out = (char*)dst;
+  bool registered = false;
+  if (dst_kind == 3) {  // pageable destination registered for this copy: the DMA writes it directly
+    HIPCHK(hipHostRegister(dst, (size_t)n * fb, hipHostRegisterDefault));
+    registered = true;
+    dst_kind = 1;
+  }
   if (dst_kind != 0) {  // one DMA per field (device -> device, or into host memory the DMA can write)
     const hipMemcpyKind kind = dst_kind == 2 ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
-    for (int i = 0; i < n; i++)
-      HIPCHK(hipMemcpyAsync(out + (size_t)i * fb, ctx->fields[first_slot + i].d, fb, kind, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
+    hipError_t e = hipSuccess;
+    for (int i = 0; i < n && e == hipSuccess; i++)
+      e = hipMemcpyAsync(out + (size_t)i * fb, ctx->fields[first_slot + i].d, fb, kind, ctx->stream);
+    const hipError_t es = hipStreamSynchronize(ctx->stream);
+    if (registered) (void)hipHostUnregister(dst);
+    if (e != hipSuccess || es != hipSuccess)
+      return fail(ctx, ALIFMM_E_HIP, "copy_fields: %s", hipGetErrorString(e != hipSuccess ? e : es));
   } else {
     // pageable: pieces of kPinBytes through kPinBufs pinned buffers; the DMA of the next pieces
     // runs while a thread team copies the current one out of its buffer
@@ -1049,7 +943,7 @@ int alifmm_put_field(alifmm_ctx* ctx, int slot, int subgrid, const double* data)
   int rc = alifmm_field_shape(ctx, subgrid, &fz, &fx);
   if (rc) return rc;
   HIPCHK(hipSetDevice(ctx->device));
-  if ((rc = ensure_field(ctx, slot, subgrid, fz, fx))) return rc;
+  if ((rc = af_ensure_field(ctx, slot, subgrid, fz, fx))) return rc;
   HIPCHK(hipMemcpy(ctx->fields[slot].d, data, (size_t)fz * fx * 8, hipMemcpyHostToDevice));
   return ALIFMM_OK;
 }

@@ -1,0 +1,132 @@
+// context.h — the host-side context behind include/alifmm.h (one GPU): resident model, work
+// arena, resident fields, ray buffers, pinned staging ring.  Shared by api.cpp (travel, copy,
+// rays) and comm.cpp (RCCL gather of resident fields).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "../../include/alifmm.h"
+#include "kernels.h"
+
+struct Field {
+  double* d = nullptr;
+  size_t bytes = 0;  // the field (fnz x fnx doubles)
+  size_t alloc = 0;  // allocated: the field + the K-member band kernel's edge buffers after it
+  int sg = 0, nz = 0, nx = 0;
+  int64_t steps[4] = {0, 0, 0, 0};
+  int64_t sweeps = 0;
+  int64_t prof[14] = {};  // band profile: 6 phase ticks, 3 list sums, max close, 4 sub-phase ticks
+};
+
+struct Arena {  // per-chunk scratch, reused across calls
+  int nsrc = 0;
+  long cells = 0, capL = 0, capC = 0, capS = 0;
+  int* S = nullptr;
+  int* own = nullptr;
+  int* lists = nullptr;    // Lin | FS | A | L | C | Cp | D | Rx | Bl | Bp per source
+  double* dlists = nullptr;  // Lt | V | Dv per source
+  int K = 0;                 // K-member kernel: members the rim lists are sized for
+  long capR = 0, ecells = 0;
+  int* rimc = nullptr;       // K-member kernel: rim lists [src][K][2][capR]
+  double* rimt = nullptr;
+  af::KX* kx = nullptr;      // K-member kernel: exchange blocks
+  double* Ts = nullptr;  // stage grids (travel_finer_grid), 2 per source
+  int* Ss = nullptr;
+  af::BandSrc* srcs = nullptr;
+  af::HandoverOut* ho = nullptr;
+  af::InitJob* jobs = nullptr;
+  double* dscx = nullptr;
+  double* dscz = nullptr;
+};
+
+
+struct alifmm_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipStream_t fill = nullptr;  // field initialisation, overlapped with the source-init kernel
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t ev_fill = nullptr;
+  std::string err;
+  // model
+  bool have_model = false;
+  int nz0 = 0, nx0 = 0, ncol = 0;
+  double dnx = 0, dnz = 0, gox = 0, goz = 0, vmax = 0;
+  double* d_veln = nullptr;
+  double* d_vm = nullptr;
+  int* d_velpn = nullptr;
+  int* d_sidx = nullptr;
+  double* d_stab = nullptr;
+  int nstab = 0;
+  int* d_mid = nullptr;
+  unsigned char* d_mid8 = nullptr;  // the same ids as bytes when there are <= 256 materials
+  af::MatRec* d_mtab = nullptr;
+  double* d_mslo = nullptr;  // fouds18_A() slownesses per material (DevModel::mslo)
+  int nmat = 0;
+  double* d_gtab = nullptr;
+  double* d_ptab = nullptr;
+  // options
+  double cdelta = 0.5, r0 = 40.0;
+  int exact_r = 20;
+  int batch = 256;
+  int prof = 0;
+  int members = 0;     // band kernel: workgroups per source (0: as many as the device fits, <= 16)
+  int stripe_log = 0;  // band kernel: stripe width log2 (0: 6 for K <= 4, 4 for K >= 8)
+  int last_k = 0;      // members per source of the last band launch
+  int n_cu = 0;
+  long cap_scale = 1;
+  // state
+  std::vector<Field> fields;
+  Arena arena;
+  double t_init = 0, t_band = 0, t_total = 0;
+  // packed points of the last alifmm_find_rays(ray_xy = NULL, ray_xy_cap = ALIFMM_KEEP_RAYS) call,
+  // per ray in the caller's order, until alifmm_take_rays() copies them out
+  std::vector<std::vector<double>> kept_rays;
+  int64_t kept_pts = 0;
+  // ray-tracer work buffers, kept across alifmm_find_rays calls (sized for the largest chunk seen)
+  struct RayBufs {
+    size_t pts = 0;  // capacity of rx / ry in doubles
+    int rays = 0;    // capacity of the per-ray arrays
+    double *rx = nullptr, *ry = nullptr, *t = nullptr;
+    int *len = nullptr, *flags = nullptr;
+    af::RayJob* jobs = nullptr;
+    long long* off = nullptr;
+  } rb;
+  // pinned staging ring of alifmm_copy_fields (pageable destinations)
+  static constexpr int kPinBufs = 4;
+  static constexpr size_t kPinBytes = 32u << 20;
+  void* pin[kPinBufs] = {};
+  hipEvent_t pin_ev[kPinBufs] = {};
+};
+
+static inline int fail(alifmm_ctx* c, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (c) c->err = buf;
+  return code;
+}
+
+#define HIPCHK(call)                                                                          \
+  do {                                                                                        \
+    hipError_t e_ = (call);                                                                   \
+    if (e_ != hipSuccess) return fail(ctx, ALIFMM_E_HIP, "%s: %s", #call, hipGetErrorString(e_)); \
+  } while (0)
+
+template <class T>
+static inline hipError_t dalloc(T** p, size_t n) {
+  return hipMalloc((void**)p, std::max<size_t>(n, 1) * sizeof(T));
+}
+static inline void dfree(void* p) {
+  if (p) (void)hipFree(p);
+}
+
+
+// slot `slot` holds an (fz, fx) field of subgrid sg (+ extra_cells doubles after it); api.cpp
+extern "C" int af_ensure_field(alifmm_ctx* ctx, int slot, int sg, int fz, int fx, long extra_cells = 0);

@@ -182,13 +182,22 @@ AF_DEV void load_nb(NbFieldT& nb, const double* T, int eprv, int total, const KG
     cb[c] = ot[c] ? eprv + g.ecol(x + c - 2) * g.nz : x + c - 2;
   }
   double t[12];
+  // 32-bit byte offsets (scalar base + vector offset form) while field + edge buffers stay below
+  // 4 GB (2^29 doubles, every C1..C5 grid); larger allocations address with 64-bit pointers
+  const bool off32 = total < (1 << 29);  // (uniform)
+  int idx[12];
 #pragma unroll
   for (int k = 0; k < 12; k++) {
     const int r = dz[k] + 2, c = dx[k] + 2;
-    int idx = cb[c] + (ot[c] ? zc[r] : ro[r]);
-    idx = idx < 0 ? 0 : idx >= total ? total - 1 : idx;
-    // 32-bit byte offset: the compiler can then use the scalar base + vector offset form
-    t[k] = fabs(gld_sc1((const double*)((const char*)T + ((unsigned)idx << 3))));
+    const int i = cb[c] + (ot[c] ? zc[r] : ro[r]);
+    idx[k] = i < 0 ? 0 : i >= total ? total - 1 : i;
+  }
+  if (off32) {
+#pragma unroll
+    for (int k = 0; k < 12; k++) t[k] = fabs(gld_sc1((const double*)((const char*)T + ((unsigned)idx[k] << 3))));
+  } else {
+#pragma unroll
+    for (int k = 0; k < 12; k++) t[k] = fabs(gld_sc1(T + idx[k]));
   }
   unsigned m = 0;
 #pragma unroll

@@ -27,45 +27,49 @@ def bench_sources(rank, n_sources, n, dnx):
     return scx, scz
 
 
-def gather_fields(ctx, n_local, fnz, fnx, rank, world, device, first_slot=0):
-    """RCCL gather of every rank's resident fields to rank 0 (the result-return leg of bench.py).
+def gather_plan(n_sources, world):
+    """Where bench.py's strong deal puts every source after the RCCL gather to rank 0: rank r holds
+    sources deal(range(n_sources), world)[r] in its slots 0, 1, ...; alifmm_gather_fields stacks
+    them on the root rank after rank (slot offset sum(count[:r]) + k, _alifmm.gather_layout).
+    Returns (counts, root_slot_of_source)."""
+    parts = deal(range(n_sources), world)
+    counts = [len(p) for p in parts]
+    off = np.concatenate(([0], np.cumsum(counts)))[:-1]
+    slot = np.empty(n_sources, dtype=np.int64)
+    for r, p in enumerate(parts):
+        slot[p] = off[r] + np.arange(len(p))
+    return counts, slot
 
-    Each rank copies its n_local fields device-to-device into one contiguous buffer
-    (alifmm_copy_fields, kind 2) and joins one dist.gather over an RCCL ("nccl") group onto rank
-    0's device; ranks with fewer fields pad to the largest count.  torch is imported before the
-    library is loaded (bench.py), so both share one HIP runtime and device pointers are valid
-    in both.  Returns the timings (max over ranks) and rates of the two parts."""
+
+def gather_fields(ctx, n_local, subgrid, rank, world, first_slot=0):
+    """RCCL gather of every rank's resident fields to rank 0 through the library's C-ABI
+    (alifmm_comm_init_rank + alifmm_gather_fields: one ncclSend / ncclRecv per field over xGMI,
+    no padding), the result-return leg of bench.py for N > 1.  torch.distributed (gloo, CPU) only
+    carries the 128-byte RCCL id and the per-rank counts.  Returns the timings (max over ranks)."""
     import time
 
-    import torch
     import torch.distributed as dist
 
-    torch.cuda.set_device(device)
-    g = dist.new_group(backend="nccl")
-    counts = torch.tensor([n_local], dtype=torch.int64)
-    cmax = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
-    dist.all_gather(cmax, counts)
-    nmax = int(max(int(c) for c in cmax))
-    buf = torch.empty((nmax, fnz, fnx), dtype=torch.float64, device="cuda")
-    recv = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
-    dist.barrier(group=g)
-    torch.cuda.synchronize()
+    import _alifmm
+
+    uid = [_alifmm.Comm.unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(uid, src=0)
+    counts = [None] * world
+    dist.all_gather_object(counts, int(n_local))
     t0 = time.perf_counter()
-    d2d_gbps = ctx.copy_fields_to_device(first_slot, n_local, buf.data_ptr()) if n_local else 0.0
-    t1 = time.perf_counter()
-    dist.gather(buf, recv, dst=0, group=g)
-    torch.cuda.synchronize()
-    t2 = time.perf_counter()
-    copy_s = max_over_ranks(t1 - t0, dist)
-    gather_s = max_over_ranks(t2 - t1, dist)
-    total = int(sum(int(c) for c in cmax)) * fnz * fnx * 8
-    remote = total - n_local * fnz * fnx * 8 if rank == 0 else 0
-    remote = int(max_over_ranks(remote, dist))
-    del recv, buf
-    dist.destroy_process_group(g)
-    return {"pack_d2d_ms": copy_s * 1e3, "pack_d2d_GBps": d2d_gbps, "rccl_gather_ms": gather_s * 1e3,
-            "rccl_gather_bytes_into_rank0": remote,
-            "rccl_gather_GBps_into_rank0": remote / gather_s / 1e9 if gather_s > 0 else None}
+    comm = _alifmm.Comm.rank(ctx, world, rank, uid[0])
+    init_s = max_over_ranks(time.perf_counter() - t0, dist)
+    try:
+        dist.barrier()
+        ms = comm.gather(0, subgrid, [first_slot] * world, counts, dst_slot=first_slot)
+    finally:
+        comm.close()
+    gather_s = max_over_ranks(ms / 1e3, dist)
+    fz, fx = ctx.field_shape(subgrid)
+    remote = (sum(counts) - counts[0]) * fz * fx * 8
+    return {"rccl_init_ms": init_s * 1e3, "rccl_gather_ms": gather_s * 1e3, "rccl_gather_bytes_into_rank0": remote,
+            "rccl_gather_GBps_into_rank0": remote / gather_s / 1e9 if gather_s > 0 else None,
+            "rccl_gather": "alifmm_gather_fields (library C-ABI, librccl), one message per field"}
 
 
 def max_over_ranks(value, dist=None):

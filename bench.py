@@ -56,6 +56,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: the CPUs this job is granted (affinity, cgroup quota)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-return", action="store_true", help="skip the result-return measurement")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end ALI_FMM.update() measurement")
     ap.add_argument("--gather", action="store_true", help="N > 1: also time an RCCL gather of all fields to rank 0")
     ap.add_argument("--members", type=int, default=None, help="band-kernel workgroups per source (0: auto)")
     ap.add_argument("--cdelta", type=float, default=None)
@@ -235,10 +236,38 @@ def main():
         d2h = sharding.max_over_ranks(time.perf_counter() - t1, dist)
         ret.update({"d2h_ms": d2h * 1e3, "d2h_GBps_per_gpu": gbps, "bytes_per_gpu": int(cells * 8 * ns),
                     "d2h": "pageable host memory through the library's pinned staging ring, every GPU at once"})
+        # the same copy DMA'd straight into the pageable destination, registered for the copy
+        dst = np.empty((ns, n, n))
+        barrier()
+        t1 = time.perf_counter()
+        ctx.copy_fields_into(0, dst, range(ns), 1, dst_kind=3)
+        d2h_reg = sharding.max_over_ranks(time.perf_counter() - t1, dist)
+        del dst
+        ret.update({"d2h_registered_ms": d2h_reg * 1e3, "d2h_registered_GBps_per_gpu": cells * 8 * ns / d2h_reg / 1e9})
         if world > 1 and "ALIFMM_BENCH_DEVICE" in os.environ:
             ret["rccl_gather"] = "skipped: every rank on one device (RCCL needs one GPU per rank)"
         elif world > 1 and args.gather:
-            ret.update(sharding.gather_fields(ctx, ns, n, n, rank, world, dev))
+            ret.update(sharding.gather_fields(ctx, ns, 1, rank, world))
+    # end to end through the drop-in (N = 1): ALI_FMM.update() on the C4 sources — model digest,
+    # fields, and their single copy into the caller's (nsrc, 4096, 4096) stack; the second call is
+    # timed (the first uploads the model into the object's own context)
+    e2e = None
+    if world == 1 and not args.no_e2e:
+        import Anis_TTF_rays as A
+
+        ctx.release_fields()
+        M = A.ALI_FMM(model[0], model[1], model[2], scx, scz, stif_den=model[3], dnx=dnx)
+        M.update(model[0], model[1], model[2], model[3])
+        t1 = time.perf_counter()
+        F = M.update(model[0], model[1], model[2], model[3])
+        te = time.perf_counter() - t1
+        e2e = {"update_s": te, "cell_updates_per_s": cells * ns / te, "sources_per_s": ns / te,
+               "stack_bytes": int(F.nbytes), "fields_ms": M._ctx(0).last_timing()[2],
+               "what": "ALI_FMM.update() at C4: model digest (xxh3 of every array) + fields on the GPU + one "
+                       "copy of each field into the returned stack (no intermediate array; host peak = one stack)"}
+        del F
+        for c in M._ctxs.values():
+            c.close()
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args, scx, scz, model, vt, dnx, cells)
@@ -277,6 +306,7 @@ def main():
                                          "sq_wait_any_frac": valu.get("sq_wait_any_frac")}
                                         if valu and band_avg_s > 0 else None)},
             "result_return": ret,
+            "update_end_to_end": e2e,
             "cpu_baseline": cpu,
         }
         if cpu:

@@ -79,7 +79,9 @@ int alifmm_release_fields(alifmm_ctx* ctx);
  * workers return over queue2 :3610, :3659).  dst_kind 0: pageable host memory, copied through a
  * ring of pinned staging buffers (the DMA of one piece overlaps the host copy of the previous);
  * 1: host memory the DMA engine can write directly (pinned or registered); 2: device memory of
- * this context's GPU (e.g. a communication buffer).  *gbps (nullable) = bytes / wall time. */
+ * this context's GPU (e.g. a communication buffer); 3: pageable host memory registered with the
+ * DMA engine for the duration of the copy (hipHostRegister), then written directly.
+ * *gbps (nullable) = bytes / wall time. */
 int alifmm_copy_fields(alifmm_ctx* ctx, int first_slot, int n, double* dst, int dst_kind, double* gbps);
 
 /* Trace npairs rays (replaces find_ray() :3104-3465 incl. ray_time() :2992-3022).
@@ -147,6 +149,27 @@ int alifmm_fouds18_band(alifmm_ctx* ctx, int n, int pz, int px, const double* tt
                         const int32_t* iz, const int32_t* ix, const double* dnx, const double* dnz,
                         const int32_t* nnz_arg, const int32_t* nnx_arg, const int32_t* mz, const int32_t* mx,
                         int quant, double* out);
+
+/* ---- RCCL gather of resident fields onto one GPU (replaces the reference's result return over
+ * multiprocessing queue2: parallel_TTF :3610, parallel_TTF_finer_grid :3659, parallel_TTF_rays
+ * :3733).  librccl is loaded on first use.  A communicator spans one GPU per rank:
+ *   alifmm_comm_init_all   one process driving n contexts on n distinct GPUs (ranks = array order)
+ *   alifmm_comm_init_rank  one process per GPU; every rank passes the same 128-byte id, made by one
+ *                          rank with alifmm_comm_unique_id and shared by the caller's own means. */
+typedef struct alifmm_comm alifmm_comm;
+int alifmm_comm_unique_id(char* id128);
+int alifmm_comm_init_rank(alifmm_ctx* ctx, int nranks, int rank, const char* id128, alifmm_comm** out);
+int alifmm_comm_init_all(alifmm_ctx* const* ctxs, int n, alifmm_comm** out);
+int alifmm_comm_destroy(alifmm_comm* comm);
+const char* alifmm_comm_last_error(alifmm_comm* comm);
+/* Every rank calls it with the same arrays (indexed by rank): rank r's resident slots
+ * first_slot[r] .. first_slot[r]+count[r]-1 (fields of `subgrid`, one shape) arrive on the root as
+ * resident slots dst_slot + count[0] + ... + count[r-1] + i, rank after rank (one ncclSend /
+ * ncclRecv per field in one group; no padding).  The root's own fields stay in place when their
+ * destination equals their slots, else they are copied device-to-device into free slots.
+ * *ms (nullable) = wall time of the gather on this process. */
+int alifmm_gather_fields(alifmm_comm* comm, int root, int subgrid, const int* first_slot, const int* count,
+                         int dst_slot, double* ms);
 
 #ifdef __cplusplus
 }

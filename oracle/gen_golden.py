@@ -258,6 +258,49 @@ def gen_c4():
     save("c4_weldlike", **res)
 
 
+CORRIDOR_R = 6  # Chebyshev radius (fine nodes) kept around each rounded ray point at subgrid 1
+
+
+def gen_c4_corridor():
+    """F7 rays pinned on the reference's OWN 4096^2 receiver field: the field is kept only in a
+    corridor of CORRIDOR_R nodes around each reference ray's points (find_ray :3104-3465 reads the
+    plane sg ahead of round(last point), +-(3 sg + 1) candidates along it), NaN elsewhere.  The
+    reference's find_ray is re-run on the corridor field and must return the identical ray and
+    time, which proves the corridor holds every node the reference reads."""
+    veln, velpn, vm, sd = W.weldlike_model()
+    vt = W.default_table()
+    dnx = W.weldlike_dnx()
+    rec = (2056, 4095)
+    t0 = time.time()
+    TR = tr(dnx * rec[0], dnx * rec[1], veln, velpn, vm, sd, vt, vt, dnx)
+    print("C4 receiver TTF %.1fs" % (time.time() - t0), flush=True)
+    nz, nx = TR.shape
+    keep = np.zeros(TR.shape, dtype=bool)
+    res = {"receiver": np.array(rec, dtype=np.float64), "radius": np.array(CORRIDOR_R)}
+    xs = [8, 1032, 2056, 3080, 4088]
+    rays = {}
+    for x in xs:
+        rx, ry, t = ref().find_ray(dnx, vt, np.array([float(x), 0.0]), np.array([float(rec[0]), float(rec[1])]), TR,
+                                   veln, velpn, vm, sd, 1)
+        rays[x] = (rx.copy(), ry.copy(), float(t))
+        for px, pz in zip(np.round(rx).astype(int), np.round(ry).astype(int)):
+            keep[max(0, pz - CORRIDOR_R):pz + CORRIDOR_R + 1, max(0, px - CORRIDOR_R):px + CORRIDOR_R + 1] = True
+        res["ray_x_%d" % x], res["ray_y_%d" % x], res["time_%d" % x] = rx.copy(), ry.copy(), np.array(t)
+        print("  ray x=%d time %.10e npts %d" % (x, t, len(rx)), flush=True)
+    TC = np.full(TR.shape, np.nan)
+    TC[keep] = TR[keep]
+    for x in xs:  # the corridor suffices: the reference on it == the reference on the whole field
+        rx, ry, t = ref().find_ray(dnx, vt, np.array([float(x), 0.0]), np.array([float(rec[0]), float(rec[1])]), TC,
+                                   veln, velpn, vm, sd, 1)
+        assert t == rays[x][2] and np.array_equal(rx, rays[x][0]) and np.array_equal(ry, rays[x][1]), x
+    idx = np.flatnonzero(keep).astype(np.int32)
+    res["corridor_idx"] = idx
+    res["corridor_val"] = TR.reshape(-1)[idx]
+    res["shape"] = np.array([nz, nx])
+    print("corridor %d nodes (%.2f %% of the field)" % (len(idx), 100.0 * len(idx) / TR.size), flush=True)
+    save("c4_ray_corridor", **res)
+
+
 def gen_local_ops():
     """update()/fouds18_A() on random 7x7 neighbourhoods.  Both read material only at (iz, ix)
     (:1368-1406, :286-315), so each case stores its centre material and fills the patch with it."""
@@ -366,7 +409,7 @@ def gen_group_vel():
 
 
 GENS = {"fmm_small": gen_fmm_small, "c1": gen_c1, "kat": gen_kat, "weld1": lambda: gen_weld(1),
-        "weld9": lambda: gen_weld(9), "c3": gen_c3, "c4": gen_c4, "local_ops": gen_local_ops, "tbp": gen_tbp,
+        "weld9": lambda: gen_weld(9), "c3": gen_c3, "c4": gen_c4, "c4_corridor": gen_c4_corridor, "local_ops": gen_local_ops, "tbp": gen_tbp,
         "group_vel": gen_group_vel}
 
 if __name__ == "__main__":

@@ -9,6 +9,8 @@ import socket
 import numpy as np
 import pytest
 
+import workloads as W
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 
@@ -110,47 +112,75 @@ def _free_port():
 
 def _rank_main(rank, world, port, q):
     import sys
+    import types
 
     sys.path.insert(0, os.path.join(REPO, "ali-fmm-and-ray-tracing_amd"))
-    import torch
+    sys.path.insert(0, REPO)
     import torch.distributed as dist
 
+    import bench
     import sharding
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    scx, scz = sharding.bench_sources(rank, 128, 4096, 2.5e-5)
-    xs = torch.tensor(np.round(scx / 2.5e-5).astype(np.int64))
-    allx = [torch.zeros_like(xs) for _ in range(world)]
-    dist.all_gather(allx, xs)
+    out = {}
+    for weak in (True, False):  # --weak (every rank 128 sources) and the default strong deal
+        args = types.SimpleNamespace(weak=weak, sources=128, n=4096)
+        scx, scz, ids = bench.rank_sources(args, rank, world, 2.5e-5)
+        allx, allid = [None] * world, [None] * world  # ragged shards: object gathers over gloo
+        dist.all_gather_object(allx, np.round(scx / 2.5e-5).astype(np.int64))
+        dist.all_gather_object(allid, np.asarray(ids, dtype=np.int64))
+        out[weak] = (allx, allid, scz.tolist())
+    # the counts every rank passes to alifmm_gather_fields (sharding.gather_fields), exchanged as there
+    counts = [None] * world
+    dist.all_gather_object(counts, len(out[False][0][rank]))
     m = sharding.max_over_ranks(float(rank) + 0.5, dist)
     if rank == 0:
-        q.put(([a.numpy() for a in allx], m, scz.tolist()))
+        q.put((out, counts, m))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_sharding_world2_gloo():
-    """bench.py's N>1 path on CPU: two gloo ranks get disjoint, complete C4 shards and the
-    max-over-ranks reduction picks the slowest rank."""
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharding_gloo(world):
+    """bench.py's N>1 path on CPU with gloo ranks: --weak gives disjoint complete 128-source sets
+    (rank 0 = BASELINE C4's); the default strong deal splits C4's 128 sources block-cyclically with
+    nothing lost or doubled; the RCCL gather's layout (counts exchanged over gloo, rank after rank
+    on the root: sharding.gather_plan / _alifmm.gather_layout) puts every source in its own root
+    slot; the max-over-ranks reduction picks the slowest rank."""
     import torch.multiprocessing as mp
+
+    import sharding
+    import _alifmm
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    allx, m, scz = q.get(timeout=120)
+    out, counts, m = q.get(timeout=180)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    a, b = allx
-    assert len(set(a.tolist())) == 128 and len(set(b.tolist())) == 128
-    assert not set(a.tolist()) & set(b.tolist())
-    assert a.tolist() == [16 + 32 * k for k in range(128)]  # rank 0 = BASELINE C4 sources
-    assert m == 1.5 and set(scz) == {0.0}
+    xw, _, szw = out[True]
+    for a in xw:
+        assert len(set(a.tolist())) == 128
+    assert not set(xw[0].tolist()) & set(xw[1].tolist())
+    assert xw[0].tolist() == [16 + 32 * k for k in range(128)]  # rank 0 = BASELINE C4 sources
+    xs, ids, szs = out[False]
+    allids = np.concatenate(ids)
+    assert sorted(allids.tolist()) == list(range(128))  # strong: every C4 source exactly once
+    assert np.array_equal(np.concatenate(xs), 16 + 32 * allids)
+    assert [len(a) for a in ids] == counts and sum(counts) == 128 and max(counts) - min(counts) <= 1
+    cnt, slot = sharding.gather_plan(128, world)
+    assert cnt == counts
+    assert sorted(slot.tolist()) == list(range(128))  # one root slot per source
+    off = _alifmm.gather_layout(counts)
+    for r in range(world):
+        assert np.array_equal(slot[ids[r]], off[r] + np.arange(counts[r]))
+    assert m == world - 0.5 and set(szw) == {0.0} and set(szs) == {0.0}
 
 
 def test_ray_store_matches_dense_layout(tmp_path):
@@ -208,23 +238,37 @@ def test_ray_flags_raise():
         _alifmm.check_ray_flags(np.array([4, 0], dtype=np.int32))
 
 
-def test_model_key_cache_tracks_content():
-    """Module-level calls reuse the model digest by array identity (no 1 GB re-hash per call),
-    but an in-place edit of the array (sampled elements, first/last row) or a new array changes
-    the key."""
+def test_model_key_tracks_every_cell():
+    """ADVICE r2 / VERDICT r2: the resident-model key is a digest of the full content, so an
+    in-place edit of ANY cell of a C4-size array (interior, unsampled) changes it, as does new
+    data at a recycled address; trust_model_identity=True opts into the identity cache (which then
+    keeps the key, by contract)."""
     import Anis_TTF_rays as A
 
-    rng = np.random.default_rng(3)
-    veln = rng.uniform(0, 180, (64, 80))
-    velpn = np.zeros((64, 80), dtype=np.int64)
-    vm = np.ones((64, 80))
-    vt = np.ones((361, 2))
-    args = [veln, velpn, vm, None, vt, vt]
+    n = 4096
+    veln = np.zeros((n, n))
+    velpn = np.zeros((n, n), dtype=np.int64)
+    vm = np.ones((n, n))
+    sd = W.stif_field(n, n)
+    vt = W.default_table()
+    args = [veln, velpn, vm, sd, vt, vt]
     k0 = A._model_digest(args)
     assert A._model_digest(args) == k0
-    veln[0, 0] += 1.0  # first row
+    veln[100, 100] += 5.0
     k1 = A._model_digest(args)
     assert k1 != k0
-    veln[-1, -1] += 1.0  # last row
-    assert A._model_digest(args) != k1
-    assert A._model_digest([veln.copy(), velpn, vm, None, vt, vt]) == A._model_digest(args)
+    sd[2001, 3003, 2] += 1
+    k2 = A._model_digest(args)
+    assert k2 not in (k0, k1)
+    vm[4095, 17] *= 1.5
+    assert A._model_digest(args) not in (k0, k1, k2)
+    assert A._model_digest([veln.copy(), velpn, vm, sd.copy(), vt, vt]) == A._model_digest(args)
+    try:
+        A.trust_model_identity = True
+        k3 = A._model_digest(args)
+        veln[7, 7] += 1.0
+        assert A._model_digest(args) == k3  # identity cache: the caller promised no in-place edits
+    finally:
+        A.trust_model_identity = False
+        A._identity_cache.clear()
+    assert A._model_digest(args) != k3

@@ -135,6 +135,18 @@ def test_c4_weldlike_fields_and_rays(golden):
         rx, ry, t = O.find_ray(dnx, vt, [x, 0.0], [2056.0, 4095.0], TR, veln, velpn, vm, sd, 1)
         assert np.array_equal(rx, g["ray_x_%d" % x]) and np.array_equal(ry, g["ray_y_%d" % x])
         assert t == float(g["time_%d" % x])
+    # the corridor fixture of the GPU ray pin (test_gpu_c5.py): the reference's own field values,
+    # and the rays traced on the corridor alone are the reference's
+    gc = golden("c4_ray_corridor")
+    idx = gc["corridor_idx"]
+    assert np.array_equal(TR.reshape(-1)[idx], gc["corridor_val"])
+    TC = np.full(TR.size, np.nan)
+    TC[idx] = gc["corridor_val"]
+    TC = TC.reshape(TR.shape)
+    for x in (8, 4088):
+        rx, ry, t = O.find_ray(dnx, vt, [x, 0.0], [2056.0, 4095.0], TC, veln, velpn, vm, sd, 1)
+        assert np.array_equal(rx, gc["ray_x_%d" % x]) and np.array_equal(ry, gc["ray_y_%d" % x])
+        assert t == float(gc["time_%d" % x])
 
 
 def _kat_rays(veln, velpn, vm, sd, vt, ph, scx, scz, pairs, sg, dnx=1e-3):

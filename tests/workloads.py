@@ -115,6 +115,20 @@ def c4_sources(nsrc=128, n=4096, dnx=None, offset=0):
     return scx, scz
 
 
+def c5_transducers(n=4096, per_side=256, dnx=None):
+    """C5 (two-array variant, the pattern of Weld_rays.py:52-55): per_side transducers on the top
+    surface (z = 0) and per_side on the bottom (z = n-1), x = 8 + 16 k; every top element i sends to
+    every bottom element j: trans_pairs[i, per_side + j] = 1 -> per_side receiver fields and
+    per_side^2 rays.  Returns (scx, scz, trans_pairs) in metres."""
+    dnx = weldlike_dnx() if dnx is None else dnx
+    x = (8 + 16 * np.arange(per_side)).astype(np.float64)
+    scx = dnx * np.concatenate([x, x])
+    scz = dnx * np.concatenate([np.zeros(per_side), np.full(per_side, float(n - 1))])
+    tp = np.zeros((2 * per_side, 2 * per_side))
+    tp[:per_side, per_side:] = 1
+    return scx, scz, tp
+
+
 def voronoi_small(n, seed=99, nseeds=None):
     nseeds = max(4, n // 16) if nseeds is None else nseeds
     return voronoi_orientations(n, nseeds, seed)
