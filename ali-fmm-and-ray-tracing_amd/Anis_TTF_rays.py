@@ -667,7 +667,7 @@ class ALI_FMM:
                     print(_EARLY_MSG)
                 times[ii, jj] = t
                 if save_rays:
-                    store.add(ii, jj, lens, pts / sg)
+                    store.add(ii, jj, lens, pts if sg == 1 else pts / sg)  # (x / 1 == x: no pass over the points)
             except Exception as e:
                 errors.append(e)
 

@@ -28,6 +28,13 @@ static void free_ray_bufs(alifmm_ctx* c) {
     if (p) (void)hipFree(p);
   b = alifmm_ctx::RayBufs();
 }
+// points kept by alifmm_find_rays(..., ALIFMM_KEEP_RAYS) for alifmm_take_rays
+static void release_kept_rays(alifmm_ctx* c) {
+  for (auto& k : c->kept_dev) dfree(k.d);
+  c->kept_dev.clear();
+  std::vector<std::vector<double>>().swap(c->kept_rays);
+  c->kept_pts = 0;
+}
 static void free_arena(Arena& a) {
   dfree(a.S); dfree(a.own); dfree(a.lists); dfree(a.dlists); dfree(a.Ts); dfree(a.Ss); dfree(a.srcs); dfree(a.ho); dfree(a.jobs);
   dfree(a.rimc); dfree(a.rimt); dfree(a.kx);
@@ -118,6 +125,7 @@ int alifmm_release_fields(alifmm_ctx* ctx) {
   for (auto& f : ctx->fields) dfree(f.d);
   ctx->fields.clear();
   free_ray_bufs(ctx);  // the ray tracer's point buffers (chunk x max_pts per coordinate) go with the fields
+  release_kept_rays(ctx);
   return ALIFMM_OK;
 }
 
@@ -150,8 +158,11 @@ int alifmm_set_option(alifmm_ctx* ctx, const char* name, double value) {
   if (!ctx || !name) return ALIFMM_E_ARG;
   if (!strcmp(name, "cdelta") && value > 0) ctx->cdelta = value;
   else if (!strcmp(name, "r0") && value >= 0) ctx->r0 = value;
+  else if (!strcmp(name, "cdelta_far") && value >= 0) ctx->cdelta_far = value;
+  else if (!strcmp(name, "r_far") && value >= 0) ctx->r_far = value;
   else if (!strcmp(name, "batch") && value >= 1) ctx->batch = (int)value;
   else if (!strcmp(name, "prof")) ctx->prof = value != 0;
+  else if (!strcmp(name, "coop")) ctx->coop = value != 0;
   else if (!strcmp(name, "exact_r") && value >= 0 && value <= 48) ctx->exact_r = (int)value;
   else if (!strcmp(name, "members") && (value == 0 || value == 1 || value == 2 || value == 4 || value == 8 || value == 16))
     ctx->members = (int)value;
@@ -164,9 +175,12 @@ int alifmm_get_option(alifmm_ctx* ctx, const char* name, double* value) {
   if (!ctx || !name || !value) return ALIFMM_E_ARG;
   if (!strcmp(name, "cdelta")) *value = ctx->cdelta;
   else if (!strcmp(name, "r0")) *value = ctx->r0;
+  else if (!strcmp(name, "cdelta_far")) *value = ctx->cdelta_far;
+  else if (!strcmp(name, "r_far")) *value = ctx->r_far;
   else if (!strcmp(name, "batch")) *value = ctx->batch;
   else if (!strcmp(name, "exact_r")) *value = ctx->exact_r;
   else if (!strcmp(name, "prof")) *value = ctx->prof;
+  else if (!strcmp(name, "coop")) *value = ctx->coop;
   else if (!strcmp(name, "members")) *value = ctx->members;
   else if (!strcmp(name, "stripe_log")) *value = ctx->stripe_log;
   else if (!strcmp(name, "last_k")) *value = ctx->last_k;
@@ -410,7 +424,7 @@ int af_ensure_field(alifmm_ctx* ctx, int slot, int sg, int fz, int fx, long extr
 // to 8, times K workgroups, one per CU) is co-resident, with >= 2 stripes per member (option
 // "members" forces a value, still capped by residency)
 static int choose_members(const alifmm_ctx* ctx, int n, int fx) {
-  const int by_cu = std::max(1, ctx->n_cu / (8 * ((n + 7) / 8)));
+  const int by_cu = std::max(1, ctx->n_cu * af_band_wgs_per_cu() / (8 * ((n + 7) / 8)));
   int K = 1;
   if (ctx->members > 0) {
     while (K * 2 <= ctx->members && K * 2 <= by_cu) K *= 2;
@@ -510,6 +524,8 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
   P.cdelta = ctx->cdelta;
   P.vmax = ctx->vmax;
   P.r0 = ctx->r0;
+  P.cdelta_far = ctx->cdelta_far;
+  P.r_far = ctx->r_far;
   P.capL = (int)capL;
   P.capC = (int)capC;
   P.capS = (int)capS;
@@ -517,6 +533,7 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
   P.gox = ctx->gox;
   P.goz = ctx->goz;
   P.prof = ctx->prof;
+  P.coop = ctx->coop;
   P.K = K;
   P.wlog = wlog;
   P.capR = (int)capR;
@@ -670,6 +687,39 @@ static void team_memcpy(char* dst, const char* src, size_t n, int nthreads) {
   for (auto& th : team) th.join();
 }
 
+// Device -> pageable host copy of a list of segments: pieces of kPinBytes through kPinBufs pinned
+// buffers; the DMA of the next pieces runs while a thread team copies the current one out of its
+// buffer (alifmm_copy_fields, alifmm_take_rays)
+struct D2HSeg {
+  const char* src;
+  char* dst;
+  size_t bytes;
+};
+static int d2h_pageable(alifmm_ctx* ctx, const std::vector<D2HSeg>& segs) {
+  const int nb = alifmm_ctx::kPinBufs;
+  const size_t pb = alifmm_ctx::kPinBytes;
+  for (int b = 0; b < nb; b++) {
+    if (!ctx->pin[b]) HIPCHK(hipHostMalloc(&ctx->pin[b], pb, hipHostMallocDefault));
+    if (!ctx->pin_ev[b]) HIPCHK(hipEventCreateWithFlags(&ctx->pin_ev[b], hipEventDisableTiming));
+  }
+  std::vector<D2HSeg> pieces;
+  for (const auto& g : segs)
+    for (size_t o = 0; o < g.bytes; o += pb) pieces.push_back({g.src + o, g.dst + o, std::min(pb, g.bytes - o)});
+  const long np = (long)pieces.size();
+  auto issue = [&](long i) -> hipError_t {
+    hipError_t e = hipMemcpyAsync(ctx->pin[i % nb], pieces[i].src, pieces[i].bytes, hipMemcpyDeviceToHost, ctx->stream);
+    return e == hipSuccess ? hipEventRecord(ctx->pin_ev[i % nb], ctx->stream) : e;
+  };
+  const int team = (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+  for (long i = 0; i < std::min<long>(nb, np); i++) HIPCHK(issue(i));
+  for (long i = 0; i < np; i++) {
+    HIPCHK(hipEventSynchronize(ctx->pin_ev[i % nb]));
+    team_memcpy(pieces[i].dst, (const char*)ctx->pin[i % nb], pieces[i].bytes, team);
+    if (i + nb < np) HIPCHK(issue(i + nb));
+  }
+  return ALIFMM_OK;
+}
+
 int alifmm_copy_fields(alifmm_ctx* ctx, int first_slot, int n, double* dst, int dst_kind, double* gbps) {
   if (!ctx || n < 0 || first_slot < 0 || (n > 0 && !dst) || dst_kind < 0 || dst_kind > 3)
     return fail(ctx, ALIFMM_E_ARG, "copy_fields: bad args");
@@ -698,42 +748,10 @@ int alifmm_copy_fields(alifmm_ctx* ctx, int first_slot, int n, double* dst, int 
     if (e != hipSuccess || es != hipSuccess)
       return fail(ctx, ALIFMM_E_HIP, "copy_fields: %s", hipGetErrorString(e != hipSuccess ? e : es));
   } else {
-    // pageable: pieces of kPinBytes through kPinBufs pinned buffers; the DMA of the next pieces
-    // runs while a thread team copies the current one out of its buffer
-    const int nb = alifmm_ctx::kPinBufs;
-    const size_t pb = alifmm_ctx::kPinBytes;
-    for (int b = 0; b < nb; b++) {
-      if (!ctx->pin[b]) HIPCHK(hipHostMalloc(&ctx->pin[b], pb, hipHostMallocDefault));
-      if (!ctx->pin_ev[b]) HIPCHK(hipEventCreateWithFlags(&ctx->pin_ev[b], hipEventDisableTiming));
-    }
-    const size_t per = (fb + pb - 1) / pb;  // pieces per field
-    const long np = (long)per * n;
-    auto piece = [&](long i, const char*& src, char*& d, size_t& len) {
-      const int f = (int)(i / per);
-      const size_t o = (size_t)(i % per) * pb;
-      src = (const char*)ctx->fields[first_slot + f].d + o;
-      d = out + (size_t)f * fb + o;
-      len = std::min(pb, fb - o);
-    };
-    auto issue = [&](long i) -> hipError_t {
-      const char* s;
-      char* d;
-      size_t len;
-      piece(i, s, d, len);
-      hipError_t e = hipMemcpyAsync(ctx->pin[i % nb], s, len, hipMemcpyDeviceToHost, ctx->stream);
-      return e == hipSuccess ? hipEventRecord(ctx->pin_ev[i % nb], ctx->stream) : e;
-    };
-    const int team = (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
-    for (long i = 0; i < std::min<long>(nb, np); i++) HIPCHK(issue(i));
-    for (long i = 0; i < np; i++) {
-      HIPCHK(hipEventSynchronize(ctx->pin_ev[i % nb]));
-      const char* s;
-      char* d;
-      size_t len;
-      piece(i, s, d, len);
-      team_memcpy(d, (const char*)ctx->pin[i % nb], len, team);
-      if (i + nb < np) HIPCHK(issue(i + nb));
-    }
+    std::vector<D2HSeg> segs(n);
+    for (int i = 0; i < n; i++) segs[i] = {(const char*)ctx->fields[first_slot + i].d, out + (size_t)i * fb, fb};
+    const int rc = d2h_pageable(ctx, segs);
+    if (rc) return rc;
   }
   const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   if (gbps) *gbps = dt > 0 ? (double)fb * n / dt / 1e9 : 0.0;
@@ -833,9 +851,11 @@ int alifmm_find_rays(alifmm_ctx* ctx, int npairs, const int32_t* field_slot, con
   // offsets follow the caller's ray order; we first trace everything (times/lengths), packing each
   // chunk into a host staging area keyed by ray id.
   const bool keep = !ray_xy && ray_xy_cap == ALIFMM_KEEP_RAYS;
-  ctx->kept_rays.clear();
-  ctx->kept_pts = 0;
-  std::vector<std::vector<double>> staged((ray_xy || keep) ? npairs : 0);
+  // one subgrid (the usual case): the rays are traced in the caller's order, so the kept points
+  // stay on the device, chunk after chunk, and alifmm_take_rays copies them out once
+  const bool dev_keep = keep && groups.size() == 1;
+  release_kept_rays(ctx);
+  std::vector<std::vector<double>> staged(((ray_xy || keep) && !dev_keep) ? npairs : 0);
   for (auto& g : groups) {
     const int sg = g.first;
     const auto& ids = g.second;
@@ -893,6 +913,12 @@ int alifmm_find_rays(alifmm_ctx* ctx, int npairs, const int32_t* field_slot, con
         RCHK(dalloc(&d_packed, (size_t)2 * std::max<long long>(off[n], 1)));
         RCHK(hipMemcpyAsync(d_off, off.data(), 8 * n, hipMemcpyHostToDevice, ctx->stream));
         RCHK(af_launch_pack_rays(d_rx, d_ry, d_len, d_off, n, max_pts, d_packed, ctx->stream));
+        if (dev_keep) {  // the chunk's packed points stay on the device (the context owns them now)
+          ctx->kept_dev.push_back({d_packed, (int64_t)off[n]});
+          ctx->kept_pts += off[n];
+          d_packed = nullptr;
+          continue;
+        }
         std::vector<double> packed(2 * off[n]);
         RCHK(hipMemcpyAsync(packed.data(), d_packed, 16 * off[n], hipMemcpyDeviceToHost, ctx->stream));
         RCHK(hipStreamSynchronize(ctx->stream));
@@ -911,10 +937,14 @@ int alifmm_find_rays(alifmm_ctx* ctx, int npairs, const int32_t* field_slot, con
       if (flags) flags[k] = flg[k];
       if (ray_xy) std::copy(staged[k].begin(), staged[k].end(), ray_xy + 2 * offsets[k]);
     }
-    if (keep) {
+    if (keep && !dev_keep) {
       ctx->kept_rays.swap(staged);
       ctx->kept_pts = offsets[npairs];
     }
+  }
+  if (rc || (dev_keep && ctx->kept_pts != offsets[npairs])) {
+    release_kept_rays(ctx);
+    if (!rc) rc = fail(ctx, ALIFMM_E_KERNEL, "find_rays: kept points do not add up to the ray lengths");
   }
   cleanup();
   return rc;
@@ -928,12 +958,22 @@ int alifmm_take_rays(alifmm_ctx* ctx, double* ray_xy, int64_t ray_xy_cap, int64_
     return fail(ctx, ALIFMM_E_ARG, "take_rays: ray_xy capacity %lld < %lld", (long long)ray_xy_cap,
                 (long long)ctx->kept_pts);
   int64_t off = 0;
+  if (!ctx->kept_dev.empty()) {  // device-resident chunks: one pass through the pinned ring
+    std::vector<D2HSeg> segs;
+    for (auto& k : ctx->kept_dev) {
+      segs.push_back({(const char*)k.d, (char*)(ray_xy + 2 * off), (size_t)k.npts * 16});
+      off += k.npts;
+    }
+    HIPCHK(hipSetDevice(ctx->device));
+    const int rc = d2h_pageable(ctx, segs);
+    release_kept_rays(ctx);
+    return rc;
+  }
   for (auto& r : ctx->kept_rays) {
     std::copy(r.begin(), r.end(), ray_xy + 2 * off);
     off += (int64_t)r.size() / 2;
   }
-  std::vector<std::vector<double>>().swap(ctx->kept_rays);
-  ctx->kept_pts = 0;
+  release_kept_rays(ctx);
   return ALIFMM_OK;
 }
 

@@ -142,6 +142,7 @@ struct RunCfg {
   double dnx, dnz;  // update() spacing and fouds18 dnz
   MatView mv;
   double delta, t0;
+  double delta_far, tfar;  // band width far from the source (tfar 0: off)
 };
 
 // material of main-grid cell (z, x): LDSMAT = one id load + the LDS record; else four arrays

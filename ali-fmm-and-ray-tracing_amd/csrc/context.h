@@ -71,9 +71,11 @@ struct alifmm_ctx {
   double* d_ptab = nullptr;
   // options
   double cdelta = 0.5, r0 = 40.0;
+  double cdelta_far = 0.0, r_far = 0.0;  // band width beyond r_far nodes (0: off)
   int exact_r = 20;
   int batch = 256;
   int prof = 0;
+  int coop = 0;  // band kernel: cooperative launch (1) or plain launch after a residency check (0)
   int members = 0;     // band kernel: workgroups per source (0: as many as the device fits, <= 16)
   int stripe_log = 0;  // band kernel: stripe width log2 (0: 6 for K <= 4, 4 for K >= 8)
   int last_k = 0;      // members per source of the last band launch
@@ -85,7 +87,12 @@ struct alifmm_ctx {
   double t_init = 0, t_band = 0, t_total = 0;
   // packed points of the last alifmm_find_rays(ray_xy = NULL, ray_xy_cap = ALIFMM_KEEP_RAYS) call,
   // per ray in the caller's order, until alifmm_take_rays() copies them out
-  std::vector<std::vector<double>> kept_rays;
+  std::vector<std::vector<double>> kept_rays;  // host-staged (several subgrids in one call)
+  struct KeptChunk {
+    double* d;  // packed (x, z) points of a chunk of rays, device memory
+    int64_t npts;
+  };
+  std::vector<KeptChunk> kept_dev;  // device-resident (one subgrid: the caller's order)
   int64_t kept_pts = 0;
   // ray-tracer work buffers, kept across alifmm_find_rays calls (sized for the largest chunk seen)
   struct RayBufs {

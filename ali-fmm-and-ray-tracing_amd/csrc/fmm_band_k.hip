@@ -47,10 +47,17 @@
 namespace af {
 namespace kb {
 
+// Workgroups per CU (AF_WG_PER_CU): 1 = one 768-thread member per CU with the whole LDS; 2 = two
+// 384-thread members per CU (of any sources), each with half the LDS, so that one member's
+// barrier waits and memory round trips are covered by the other's work (the host then runs
+// twice the members per source, choose_members / af_band_wgs_per_cu).
+#ifndef AF_WG_PER_CU
+#define AF_WG_PER_CU 1
+#endif
 // 768 threads: 12 waves, 3 per SIMD (the kernel fits 168 VGPRs): the claim and accept passes
 // hide more latency (C4 128 sources: 456 -> 437 ms with 512 -> 768, tools/kbench.py)
 #ifndef AF_THREADS
-#define AF_THREADS 768
+#define AF_THREADS (768 / AF_WG_PER_CU)
 #endif
 constexpr int kThreads = AF_THREADS;
 constexpr int kWaves = kThreads / 64;
@@ -58,17 +65,30 @@ constexpr int kWaves = kThreads / 64;
 // (157 KB of 160), the close set to the C4 peak (3 295 live slots of one member at K = 2): 2560 / 1536
 // -> 3328 / 1792 took the C4 band from 416 to 405 ms, the accepted list 1024 -> 1536 (the claim
 // then stays in LDS and tile-sorted in the widest steps) to 388 ms; 161 KB of LDS in all
+// (two members per CU: half of it each, 77.7 KB, the claim hash a quarter)
+#if AF_WG_PER_CU == 2
+#define AF_LCAP_D 1664
+#define AF_ECAP_D 896
+#define AF_ACAP_D 768
+#define AF_HASHLOG_D 11
+#else
+#define AF_LCAP_D 3328
+#define AF_ECAP_D 1792
+#define AF_ACAP_D 1536
+#define AF_HASHLOG_D 13
+#endif
 #ifndef AF_LCAP
-#define AF_LCAP 3328
+#define AF_LCAP AF_LCAP_D
 #endif
 #ifndef AF_ECAP
-#define AF_ECAP 1792
+#define AF_ECAP AF_ECAP_D
 #endif
 #ifndef AF_ACAP
-#define AF_ACAP 1536
+#define AF_ACAP AF_ACAP_D
 #endif
-constexpr int kLcap = AF_LCAP, kAcap = AF_ACAP, kEcap = AF_ECAP, kBcap = 512, kDcap = 512, kRcap = 1024;
-constexpr int kHashLog = 13;
+constexpr int kLcap = AF_LCAP, kAcap = AF_ACAP, kEcap = AF_ECAP;
+constexpr int kBcap = 512 / AF_WG_PER_CU, kDcap = 512 / AF_WG_PER_CU, kRcap = 1024 / AF_WG_PER_CU;
+constexpr int kHashLog = AF_HASHLOG_D;
 constexpr int kHash = 1 << kHashLog;
 #ifndef AF_CLAIM_U
 #define AF_CLAIM_U 2
@@ -104,20 +124,20 @@ constexpr int kHash = 1 << kHashLog;
 #ifndef AF_SORT_ACC
 #define AF_SORT_ACC 256
 #endif
-constexpr int kSortB = 512;
-AF_DEV int tile_bucket(int c) { return ((pkz(c) >> 3) & 15) << 5 | ((pkx(c) >> 3) & 31); }
+constexpr int kSortB = 512 / AF_WG_PER_CU;
+AF_DEV int tile_bucket(int c) { return ((pkz(c) >> 3) & (kSortB / 32 - 1)) << 5 | ((pkx(c) >> 3) & 31); }
 constexpr int kClaimU = AF_CLAIM_U;  // claim items per lane per pass
 #ifndef AF_ACC_U
 #define AF_ACC_U 1
 #endif
 constexpr int kAccU = AF_ACC_U;  // close-set entries per lane per accept pass (2 and 4 measured slower)
 #ifndef AF_HASH_ITEMS
-#define AF_HASH_ITEMS 6144
+#define AF_HASH_ITEMS (6144 >> (13 - AF_HASHLOG_D))
 #endif
 constexpr int kHashItems = AF_HASH_ITEMS;  // claim items deduplicated in the LDS hash (more: global stamps)
 // model tables staged in LDS (more materials / stiffness rows: the model arrays are read instead)
 #ifndef AF_MATLDS
-#define AF_MATLDS 256
+#define AF_MATLDS (256 / AF_WG_PER_CU)
 #endif
 #ifndef AF_STABLDS
 #define AF_STABLDS 64
@@ -214,7 +234,7 @@ AF_DEV void load_nb(NbFieldT& nb, const double* T, int eprv, int total, const KG
 // another member's: known in the previous edge buffer, or close with T <= thr) — then one lane per
 // cell runs fouds18_A() on the staged window (few registers: the accessor is two LDS reads).
 #ifndef AF_FB_ROUND
-#define AF_FB_ROUND 128
+#define AF_FB_ROUND (128 >> (13 - AF_HASHLOG_D))
 #endif
 constexpr int kFbRound = AF_FB_ROUND;  // cells per staging round (25 doubles each in the claim-hash space)
 static_assert(kFbRound * 25 * sizeof(double) <= kHash * sizeof(int), "staging windows fit the claim hash");
@@ -288,7 +308,17 @@ AF_DEV bool x1_poll(KX* X, int K, int par, unsigned tag, Lds* sh, int me) {
 }
 
 template <int MODE, bool LDSMAT, bool PROF>
-__global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
+// 3 waves per SIMD (<= 168 VGPRs) in both layouts: 12 waves per CU = one 768-thread or two
+// 384-thread members
+#ifndef AF_WPE
+#define AF_WPE 1
+#endif
+#if AF_WPE
+#define AF_WPE_ATTR __attribute__((amdgpu_waves_per_eu(3)))
+#else
+#define AF_WPE_ATTR
+#endif
+__global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandParams P) {
   __shared__ Lds sh_;
   Lds* sh = &sh_;
   const int K = P.K;
@@ -429,6 +459,8 @@ __global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
     R.mv = MatView{P.sg, (P.sg - 1) / 2, 0, P.sg, (P.sg - 1) / 2, 0, 1, 0, 0, 0, 1};
   R.delta = launder_u(P.cdelta * P.dnx / P.vmax);
   R.t0 = launder_u(P.r0 * P.dnx / P.vmax);
+  R.delta_far = P.cdelta_far * P.dnx / P.vmax;
+  R.tfar = P.r_far > 0 && P.cdelta_far > 0 ? P.r_far * P.dnx / P.vmax : 0.0;
   long long steps = 0, myupd = 0;
   // profile (P.prof): thread 0 of member 0; phases [P1 + X1, accept + rim read, claim,
   // evaluate, fallback, commit], sub [X1 wait, rim read, claim dedupe, drain before X1]
@@ -532,6 +564,13 @@ __global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
     tmin = sh->tmin_g;
     double dl = delta;
     if (t0 > 0 && tmin < t0) dl = delta * (tmin / t0);
+#ifndef AF_FAR
+#define AF_FAR 1
+#endif
+    if (AF_FAR) {  // optional wider band far from the source (option cdelta_far / r_far; off by default)
+      const double tfar = launder_u(R.tfar);
+      if (tfar > 0 && tmin > tfar) dl = delta + (launder_u(R.delta_far) - delta) * fmin(1.0, (tmin - tfar) / tfar);
+    }
     const double thr = tmin + dl;
     if (tid == 0) {
       sh->thr = thr;
@@ -1025,7 +1064,10 @@ __global__ __launch_bounds__(kThreads) void fmm_band_k_kernel(BandParams P) {
 }  // namespace kb
 }  // namespace af
 
-// cooperative launch: nsrc (padded to a multiple of 8) x K workgroups, one per CU, all resident
+// band-kernel workgroups one CU holds at once (the host sizes K so that every member is resident)
+extern "C" int af_band_wgs_per_cu() { return AF_WG_PER_CU; }
+
+// nsrc (padded to a multiple of 8) x K workgroups, AF_WG_PER_CU per CU, all resident
 extern "C" hipError_t af_launch_band_k(const af::BandParams* P, hipStream_t stream) {
   const bool lds = P->M.mid && P->M.mslo && P->M.nmat <= af::kb::kMatLds && P->M.nstab <= af::kb::kStabLds &&
                    361 * P->M.ncol <= af::kb::kPtabLds;
@@ -1044,5 +1086,18 @@ extern "C" hipError_t af_launch_band_k(const af::BandParams* P, hipStream_t stre
              : (P->prof ? (const void*)af::kb::fmm_band_k_kernel<1, false, true>
                         : (const void*)af::kb::fmm_band_k_kernel<1, false, false>);
   }
-  return hipLaunchCooperativeKernel(fn, g, b, args, 0, stream);
+  if (P->coop) return hipLaunchCooperativeKernel(fn, g, b, args, 0, stream);
+  // Plain launch: the members of a source wait for each other every step, so every workgroup must
+  // be resident at once — checked here against the occupancy of this kernel (the grid is sized to
+  // it: K from af_band_wgs_per_cu and the CU count).  A cooperative launch checks the same and
+  // gang-schedules on a dedicated queue; the plain launch avoids that queue, whose teardown at
+  // process exit crashed every rocprofv3-traced run (the profiler's queue interception is gone by
+  // then).  A member that still never sees its peers stops at the X1 spin limit (error 7).
+  int dev = 0, ncu = 0, per_cu = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, af::kb::kThreads, 0);
+  if (e != hipSuccess) return e;
+  if ((long)per_cu * ncu < (long)g.x) return hipErrorCooperativeLaunchTooLarge;
+  return hipLaunchKernel(fn, g, b, args, 0, stream);
 }

@@ -61,6 +61,7 @@ struct BandParams {
   int nz, nx;    // main grid (fine grid in mode 1)
   double dnx, dnz;
   double cdelta, vmax, r0;
+  double cdelta_far, r_far;  // band width beyond r_far nodes (0: off), ramped in over r_far .. 2 r_far
   double tstop;  // mode 1: the exact main-loop prefix stops when the heap root reaches it (fmm_exact_kernel)
   int capL, capC, capS;  // list capacities, stage-grid capacity (cells)
   BandSrc* src;
@@ -69,6 +70,7 @@ struct BandParams {
   const double* scz;
   double gox, goz;
   int prof;  // record BandSrc::ph / lsum (thread 0 reads the wall clock after each barrier)
+  int coop;  // 1: hipLaunchCooperativeKernel; 0: plain launch after a residency check (default)
   int K;     // fmm_band_k: members per source (power of two <= kMaxK)
   int wlog;  // fmm_band_k: stripe width log2
   int capR;  // fmm_band_k: rim-list capacity per member and parity
@@ -130,6 +132,7 @@ extern "C" {
 hipError_t af_launch_init(const af::DevModel* M, af::InitJob* jobs, int njobs, af::HandoverOut* out, hipStream_t stream);
 hipError_t af_launch_exact(const af::BandParams* P, hipStream_t stream);
 hipError_t af_launch_band_k(const af::BandParams* P, hipStream_t stream);
+int af_band_wgs_per_cu(void);  // band-kernel workgroups resident per CU (fmm_band_k.hip AF_WG_PER_CU)
 hipError_t af_launch_scale(double* T, long n, double sg, hipStream_t stream);
 hipError_t af_launch_rays(const af::RayParams* P, hipStream_t stream);
 hipError_t af_launch_pack_rays(const double* rx, const double* ry, const int* len, const long long* off, int nrays,
