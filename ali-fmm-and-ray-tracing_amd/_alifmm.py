@@ -76,6 +76,7 @@ def _load():
             "alifmm_source_stats": (_i, [_p, _i, _p, _p]),
             "alifmm_last_timing": (_i, [_p, _p, _p, _p]),
             "alifmm_band_profile": (_i, [_p, _i, _p]),
+            "alifmm_band_span": (_i, [_p, _i, _p]),
             "alifmm_init_profile": (_i, [_p, _i, _p]),
             "alifmm_put_field": (_i, [_p, _i, _i, _p]),
             "alifmm_time_between_points": (_i, [_p, _i, _p, _p, _p, _p, _i, _p]),
@@ -365,6 +366,12 @@ class Context:
         out = np.zeros(14, dtype=np.int64)
         self._chk(lib().alifmm_band_profile(self._h, int(slot), _ptr(out)), "band_profile")
         return out
+
+    def band_span(self, slot):
+        """(start, end) wall clock [100 MHz ticks] of the band kernel's member 0 for a slot's source."""
+        out = np.zeros(2, dtype=np.int64)
+        self._chk(lib().alifmm_band_span(self._h, int(slot), _ptr(out)), "band_span")
+        return int(out[0]), int(out[1])
 
     def init_profile(self, i):
         """Source-init profile of source i of the last chunk: ticks (100 MHz) of stage 1/2/3 and the

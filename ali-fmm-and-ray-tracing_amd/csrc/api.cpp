@@ -164,7 +164,7 @@ int alifmm_set_option(alifmm_ctx* ctx, const char* name, double value) {
   else if (!strcmp(name, "prof")) ctx->prof = value != 0;
   else if (!strcmp(name, "coop")) ctx->coop = value != 0;
   else if (!strcmp(name, "exact_r") && value >= 0 && value <= 48) ctx->exact_r = (int)value;
-  else if (!strcmp(name, "members") && (value == 0 || value == 1 || value == 2 || value == 4 || value == 8 || value == 16))
+  else if (!strcmp(name, "members") && value >= 0 && value <= af::kMaxK && value == (int)value)
     ctx->members = (int)value;
   else if (!strcmp(name, "stripe_log") && (value == 0 || (value >= 3 && value <= 12))) ctx->stripe_log = (int)value;
   else return fail(ctx, ALIFMM_E_ARG, "unknown option or bad value: %s=%g", name, value);
@@ -420,19 +420,16 @@ int af_ensure_field(alifmm_ctx* ctx, int slot, int sg, int fz, int fx, long extr
   return ALIFMM_OK;
 }
 
-// members per source of the band kernel: the largest power of two <= kMaxK whose grid (nsrc padded
-// to 8, times K workgroups, one per CU) is co-resident, with >= 2 stripes per member (option
-// "members" forces a value, still capped by residency)
+// members per source of the band kernel: the largest K <= kMaxK whose grid (nsrc padded to 8, times
+// K workgroups, af_band_wgs_per_cu() of them per CU) is co-resident, with >= 2 stripes per member
+// (option "members" forces a value, still capped by residency)
 static int choose_members(const alifmm_ctx* ctx, int n, int fx) {
   const int by_cu = std::max(1, ctx->n_cu * af_band_wgs_per_cu() / (8 * ((n + 7) / 8)));
-  int K = 1;
-  if (ctx->members > 0) {
-    while (K * 2 <= ctx->members && K * 2 <= by_cu) K *= 2;
-    return K;
-  }
+  if (ctx->members > 0) return std::max(1, std::min(ctx->members, by_cu));
   // >= 2 stripes per member at the stripe width the member count selects
   auto stripes = [&](int k) { return (long)(fx + (1 << (k >= 8 ? 4 : 6)) - 1) >> (k >= 8 ? 4 : 6); };
-  while (K * 2 <= af::kMaxK && K * 2 <= by_cu && 2L * K * 2 <= stripes(K * 2)) K *= 2;
+  int K = std::min(af::kMaxK, by_cu);
+  while (K > 1 && 2L * K > stripes(K)) K--;
   return K;
 }
 
@@ -599,6 +596,8 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
     for (int k = 0; k < 6; k++) f.prof[k] = hs[i].ph[k];
     for (int k = 0; k < 3; k++) f.prof[6 + k] = hs[i].lsum[k];
     f.prof[9] = hs[i].lmax;
+    f.span[0] = hs[i].t_begin;
+    f.span[1] = hs[i].t_end;
     for (int k = 0; k < 4; k++) f.prof[10 + k] = hs[i].sub[k];
     if (hs[i].err == 2) cap_err = 1;
     else if (hs[i].err == 3) return fail(ctx, ALIFMM_E_KERNEL, "source %d: init heap overflow", i);
@@ -769,6 +768,13 @@ int alifmm_source_stats(alifmm_ctx* ctx, int slot, int64_t* steps4, int64_t* cel
 int alifmm_band_profile(alifmm_ctx* ctx, int slot, int64_t* out14) {
   if (!ctx || slot < 0 || slot >= (int)ctx->fields.size() || !out14) return fail(ctx, ALIFMM_E_ARG, "band_profile: bad slot");
   for (int k = 0; k < 14; k++) out14[k] = ctx->fields[slot].prof[k];
+  return ALIFMM_OK;
+}
+
+int alifmm_band_span(alifmm_ctx* ctx, int slot, int64_t* out2) {
+  if (!ctx || slot < 0 || slot >= (int)ctx->fields.size() || !out2) return fail(ctx, ALIFMM_E_ARG, "band_span: bad slot");
+  out2[0] = ctx->fields[slot].span[0];
+  out2[1] = ctx->fields[slot].span[1];
   return ALIFMM_OK;
 }
 

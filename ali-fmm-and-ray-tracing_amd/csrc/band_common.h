@@ -109,13 +109,17 @@ AF_DEV int wave_excl_scan(int v, int& total) {
 }
 
 // Column-stripe ownership of the K-member band kernel (fmm_band_k.hip): stripe s = x >> wlog
-// (W = 2^wlog columns, W >= 8) belongs to member s mod K (K a power of two).  EDGE cells lie
+// (W = 2^wlog columns, W >= 8) belongs to member s mod K (K = 1..16; the modulo by a multiply with
+// kmagic = ceil(2^16 / K), exact for every stripe index below 4096).  EDGE cells lie
 // within 2 columns of a stripe boundary (another member's 12-point / 5x5 stencils read them; they
 // are mirrored in the edge buffers: 4 columns per stripe, column-major, eidx), RIM cells next to
 // one (their 4-neighbour across the boundary belongs to another member).  K = 1: no edges, no rims.
 struct KGeom {
-  int K, wlog, nz, nx;
-  AF_DEV int owner(int x) const { return (x >> wlog) & (K - 1); }
+  int K, wlog, nz, nx, kmagic;
+  AF_DEV int owner(int x) const {
+    const int st = x >> wlog;
+    return st - K * ((st * kmagic) >> 16);
+  }
   AF_DEV bool edge(int x) const {
     const int r = x & ((1 << wlog) - 1);
     return K > 1 && (r < 2 || r >= (1 << wlog) - 2);

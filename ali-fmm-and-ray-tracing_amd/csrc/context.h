@@ -20,7 +20,8 @@ struct Field {
   int sg = 0, nz = 0, nx = 0;
   int64_t steps[4] = {0, 0, 0, 0};
   int64_t sweeps = 0;
-  int64_t prof[14] = {};  // band profile: 6 phase ticks, 3 list sums, max close, 4 sub-phase ticks
+  int64_t prof[14] = {};
+  int64_t span[2] = {0, 0};  // band kernel: member 0's entry / exit wall clock (100 MHz ticks)  // band profile: 6 phase ticks, 3 list sums, max close, 4 sub-phase ticks
 };
 
 struct Arena {  // per-chunk scratch, reused across calls

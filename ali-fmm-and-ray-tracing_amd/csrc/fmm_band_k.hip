@@ -55,7 +55,11 @@ namespace kb {
 #define AF_WG_PER_CU 1
 #endif
 // 768 threads: 12 waves, 3 per SIMD (the kernel fits 168 VGPRs): the claim and accept passes
-// hide more latency (C4 128 sources: 456 -> 437 ms with 512 -> 768, tools/kbench.py)
+// hide more latency (C4 128 sources: 456 -> 437 ms with 512 -> 768, tools/kbench.py).  Several
+// members per CU need workgroups the wave placement can pack: at 3 waves per SIMD two 384-thread
+// workgroups (2 + 2 + 1 + 1 waves each) do not fit together (measured: the second wave of
+// workgroups waits for the first, tools/micro/residency.hip), three 256-thread ones (one wave per
+// SIMD each) do.
 #ifndef AF_THREADS
 #define AF_THREADS (768 / AF_WG_PER_CU)
 #endif
@@ -66,16 +70,24 @@ constexpr int kWaves = kThreads / 64;
 // -> 3328 / 1792 took the C4 band from 416 to 405 ms, the accepted list 1024 -> 1536 (the claim
 // then stays in LDS and tile-sorted in the widest steps) to 388 ms; 161 KB of LDS in all
 // (two members per CU: half of it each, 77.7 KB, the claim hash a quarter)
-#if AF_WG_PER_CU == 2
+#if AF_WG_PER_CU == 3
+#define AF_LCAP_D 960
+#define AF_ECAP_D 512
+#define AF_ACAP_D 384
+#define AF_HASHLOG_D 11
+#define AF_SORTB_D 128
+#elif AF_WG_PER_CU == 2
 #define AF_LCAP_D 1664
 #define AF_ECAP_D 896
 #define AF_ACAP_D 768
 #define AF_HASHLOG_D 11
+#define AF_SORTB_D 256
 #else
 #define AF_LCAP_D 3328
 #define AF_ECAP_D 1792
 #define AF_ACAP_D 1536
 #define AF_HASHLOG_D 13
+#define AF_SORTB_D 512
 #endif
 #ifndef AF_LCAP
 #define AF_LCAP AF_LCAP_D
@@ -124,7 +136,7 @@ constexpr int kHash = 1 << kHashLog;
 #ifndef AF_SORT_ACC
 #define AF_SORT_ACC 256
 #endif
-constexpr int kSortB = 512 / AF_WG_PER_CU;
+constexpr int kSortB = AF_SORTB_D;
 AF_DEV int tile_bucket(int c) { return ((pkz(c) >> 3) & (kSortB / 32 - 1)) << 5 | ((pkx(c) >> 3) & 31); }
 constexpr int kClaimU = AF_CLAIM_U;  // claim items per lane per pass
 #ifndef AF_ACC_U
@@ -267,7 +279,7 @@ __device__ AF_F18_ATTR double fouds18_w5(const Win5& F, const DevModel& M, const
 // word per lane) until every member's words carry this step's tag, then the wave reduces them:
 // global Tmin, live close cells (sum), error (or), and the neighbour members' rim-list lengths.
 // false on timeout (a member is not resident)
-AF_DEV bool x1_poll(KX* X, int K, int par, unsigned tag, Lds* sh, int me) {
+AF_DEV bool x1_poll(KX* X, int K, int par, unsigned tag, Lds* sh, int mprev, int mnext) {
   const int lane = threadIdx.x & 63;
   const int nw = 4 * K;
   unsigned long long v = 0;
@@ -291,8 +303,8 @@ AF_DEV bool x1_poll(KX* X, int K, int par, unsigned tag, Lds* sh, int me) {
     tmin = __longlong_as_double((long long)(((unsigned long long)w1 << 32) | w));
     live = (int)w2;
     err = (int)(w3 >> 24);
-    if (q == ((me - 1) & (K - 1))) sh->nrim[0] = (int)(w3 & 0xffffffu);
-    if (K > 2 && q == ((me + 1) & (K - 1))) sh->nrim[1] = (int)(w3 & 0xffffffu);
+    if (q == mprev) sh->nrim[0] = (int)(w3 & 0xffffffu);
+    if (K > 2 && q == mnext) sh->nrim[1] = (int)(w3 & 0xffffffu);
   }
   tmin = wave_min(tmin);
   for (int o = 32; o > 0; o >>= 1) {
@@ -328,11 +340,14 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
   const int src = (j / K) * 8 + xq, me = j % K;
   if (src >= P.nsrc) return;  // all members of a padding source exit together
   BandSrc* B = P.src + src;
+  if (me == 0 && threadIdx.x == 0) B->t_begin = wall_clock64();
   KX* X = B->kx;
   const int tid0 = threadIdx.x;
   const int tid = tid0, lane = tid & 63, wv = tid >> 6;
   const int nz = P.nz, nx = P.nx;
-  const KGeom g{K, P.wlog, nz, nx};
+  const KGeom g{K, P.wlog, nz, nx, (65536 + K - 1) / K};
+  // the neighbour members (stripes s - 1 and s + 1 of an own stripe s belong to them)
+  const int mprev = me == 0 ? K - 1 : me - 1, mnext = me == K - 1 ? 0 : me + 1;
   double* T = B->T;
   int* S = B->S;
   int* own = B->own;
@@ -538,7 +553,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
         gst_sc1(&X->x1[me][par][2], gtag | (unsigned)(hi - sh->nF));
         gst_sc1(&X->x1[me][par][3], gtag | ((unsigned)min(sh->err, 255) << 24) | (unsigned)min(sh->nR, 0xffffff));
       }
-      if (wv == 0 && !x1_poll(X, K, par, (unsigned)(steps + 1), sh, me)) {
+      if (wv == 0 && !x1_poll(X, K, par, (unsigned)(steps + 1), sh, mprev, mnext)) {
         if (lane == 0) sh->err = 7;
       }
     } else if (tid == 0) {
@@ -585,7 +600,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
     const int nr1 = nq > 1 ? min(sh->nrim[1], P.capR) : 0;
     if (tid < nr0 + nr1) {
       const int side = tid < nr0 ? 0 : 1, e = tid < nr0 ? tid : tid - nr0;
-      const int q = (me + (side == 0 ? -1 : 1)) & (K - 1);
+      const int q = side == 0 ? mprev : mnext;
       rpc = gld_sc1(rimc + ((long)q * 2 + par) * P.capR + e);
       rpt = gld_sc1(rimt + ((long)q * 2 + par) * P.capR + e);
     }
@@ -681,7 +696,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
         double pt = INFINITY;
         if (e < nr0 + nr1) {
           const int side = e < nr0 ? 0 : 1, i = e < nr0 ? e : e - nr0;
-          const int q = (me + (side == 0 ? -1 : 1)) & (K - 1);
+          const int q = side == 0 ? mprev : mnext;
           pc = gld_sc1(rimc + ((long)q * 2 + par) * P.capR + i);
           pt = gld_sc1(rimt + ((long)q * 2 + par) * P.capR + i);
         }
@@ -1055,7 +1070,10 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
   for (int o = 32; o > 0; o >>= 1) myupd += __shfl_xor(myupd, o);
   if (lane == 0 && myupd) atomicAdd((unsigned long long*)&B->nupd, (unsigned long long)myupd);
   if (tid == 0) {
-    if (me == 0) B->steps[3] = steps;
+    if (me == 0) {
+      B->steps[3] = steps;
+      B->t_end = wall_clock64();
+    }
     const int e = sh->err ? sh->err : sh->err_g;
     if (e) atomicMax(&B->err, e);
   }

@@ -42,6 +42,7 @@ struct BandSrc {
   int bbox[4];    // mode 1: rows / columns [z0, z1, x0, x1] of the main grid fmm_exact_kernel wrote
   long long steps[4];
   long long nupd;  // relax evaluations (cell-sweeps) in the main run
+  long long t_begin, t_end;  // wall clock (100 MHz) when member 0 entered / left the band kernel
   int err;
   int nl0;
   // band profile (BandParams::prof): wall-clock ticks (100 MHz) of thread 0 of member 0 per phase

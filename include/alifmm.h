@@ -47,7 +47,7 @@ int alifmm_set_model(alifmm_ctx* ctx, int nnz, int nnx, const double* veln, cons
                      const double* phase_tab, int ncol, double dnx, double dnz, double gox, double goz);
 
 /* Tuning: "members" (workgroups per source of the band kernel: 0 = as many as the device holds
- * for the batch, else 1, 2, 4, 8 or 16; results are bit-identical for every value), "stripe_log"
+ * for the batch, else 1 .. 16; results are bit-identical for every value), "stripe_log"
  * (column-stripe width log2 of the band kernel's ownership, 0 = automatic), "prof" (1: record the
  * band profile, alifmm_band_profile), "cdelta" (band width in units of dnx/vmax, default 0.5),
  * "r0" (near-source band schedule radius in cells, default 40), "exact_r" (radius in cells of the
@@ -117,6 +117,9 @@ int alifmm_last_timing(alifmm_ctx* ctx, double* init_ms, double* band_ms, double
  * evaluated list sizes; out14[9] the largest close set; out14[10..13] thread 0's ticks inside
  * phases: claim [neighbour + dedupe, nsts loads, list pushes], evaluate [neighbourhood loads]. */
 int alifmm_band_profile(alifmm_ctx* ctx, int slot, int64_t* out14);
+/* Wall clock (100 MHz ticks) at which the band kernel's first member of the slot's source started
+ * and finished in the last alifmm_travel(): out2[0], out2[1] (dispatch and load-balance diagnostic). */
+int alifmm_band_span(alifmm_ctx* ctx, int slot, int64_t* out2);
 /* Source-init profile of source i of the last travel chunk (subgrid 1): wall-clock ticks
  * (100 MHz) of stage 1, 2, 3 and the exact main-loop prefix, their heap pops, the ticks the
  * relaxation role was busy in each, and their relaxations | fouds18_A() fallbacks << 32. */

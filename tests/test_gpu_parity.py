@@ -323,7 +323,7 @@ def test_c4_full_128_source_batch(golden, ctx, envelope):
 
 
 def test_members_bit_identical(ctx, envelope):
-    """One source over K = 2, 4, 16 workgroups (column stripes, one exchange per band step) gives
+    """One source over K = 2, 3, 4, 6, 16 workgroups (column stripes, one exchange per band step) gives
     the same bits as K = 1: C4 sources on stripe boundaries, the grid corners and the interior;
     the weld model at subgrid 3 (stage grids + fine-grid main loop)."""
     vt = W.default_table()
@@ -335,7 +335,7 @@ def test_members_bit_identical(ctx, envelope):
         ctx.set_option("members", 1)
         ref = ctx.travel(xs, zs)
         assert ctx.get_option("last_k") == 1.0
-        for K in (2, 4, 16):
+        for K in (2, 3, 4, 6, 16):
             ctx.set_option("members", K)
             F = ctx.travel(xs, zs)
             assert ctx.get_option("last_k") == K
@@ -346,7 +346,7 @@ def test_members_bit_identical(ctx, envelope):
         scx, scz = W.weld_transducers()
         ctx.set_option("members", 1)
         ref = ctx.travel(scx[[0, 46]], scz[[0, 46]], subgrid=3)
-        for K in (2, 8):
+        for K in (2, 5, 8):
             ctx.set_option("members", K)
             assert np.array_equal(ctx.travel(scx[[0, 46]], scz[[0, 46]], subgrid=3), ref), K
     finally:

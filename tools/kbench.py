@@ -34,6 +34,11 @@ def main():
             ctx.travel(sx[:ns], sz[:ns], copy_out=False)
             ti, tb, tt = ctx.last_timing()
             best = tb if best is None else min(best, tb)
+        sp = np.array([ctx.band_span(i) for i in range(ns)], dtype=np.float64) / 100.0  # us
+        span = {"start_spread_us": round(float(sp[:, 0].max() - sp[:, 0].min()), 1),
+                "end_spread_us": round(float(sp[:, 1].max() - sp[:, 1].min()), 1),
+                "member0_ms_min": round(float((sp[:, 1] - sp[:, 0]).min()) / 1e3, 1),
+                "member0_ms_max": round(float((sp[:, 1] - sp[:, 0]).max()) / 1e3, 1)}
         h = hashlib.sha256()
         for i in (0, ns // 2, ns - 1):
             h.update(ctx.get_field(i, 1).tobytes())
@@ -48,7 +53,7 @@ def main():
         prof.update({"live_mean": round(p[6] / st, 1), "acc_mean": round(p[7] / st, 1), "claimed_mean": round(p[8] / st, 1),
                      "close_hi_max": int(p[9]), "sub3_raw": int(p[13]), "steps": st})
         out[str(ns)] = {"k": int(ctx.get_option("last_k")), "band_ms": round(best, 1), "init_ms": round(ti, 1),
-                        "fields": h.hexdigest()[:16], "us_per_step": prof}
+                        "fields": h.hexdigest()[:16], "span": span, "us_per_step": prof}
     print(json.dumps(out), flush=True)
     ctx.close()
 
