@@ -44,8 +44,14 @@ static inline void push_close(bstate_t *b, long idx) {
     if (b->f.nsts[idx] != S_CLOSE) { b->f.nsts[idx] = S_CLOSE; b->L[b->nL++] = (int32_t)idx; }
 }
 
+/* optional wider band far from the source on the main grid (the device option cdelta_far / r_far,
+   fmm_band_k.hip): past tfar the width ramps from delta to delta_far over tfar .. 2 tfar */
+static double g_cdelta_far = 0.0, g_r_far = 0.0;
+void oband_set_far(double cdelta_far, double r_far) { g_cdelta_far = cdelta_far; g_r_far = r_far; }
+
 /* one band run on a grid until the close list drains (main) or the window edge is hit (stages) */
-static long band_run(bstate_t *b, const mat_t *m, const loopcfg_t *c, double delta, int sweeps, double t0) {
+static long band_run(bstate_t *b, const mat_t *m, const loopcfg_t *c, double delta, int sweeps, double t0,
+                     double delta_far, double tfar) {
     fstate_t *f = &b->f;
     long nx = f->nnx, nz = f->nnz;
     long steps = 0;
@@ -56,6 +62,7 @@ static long band_run(bstate_t *b, const mat_t *m, const loopcfg_t *c, double del
         /* near-source schedule: the band narrows in proportion to Tmin while Tmin < t0 */
         double dl = delta;
         if (t0 > 0 && tmin < t0) dl = delta * (tmin / t0);
+        if (tfar > 0 && tmin > tfar) dl = delta + (delta_far - delta) * fmin(1.0, (tmin - tfar) / tfar);
         double thr = tmin + dl;
         long nA = 0, nL2 = 0;
         for (long e = 0; e < b->nL; e++) {
@@ -207,7 +214,7 @@ int oband_travel(double scx, double scz, int nnz, int nnx, const double *veln, c
                 /* map band status back to heap-style codes for the hand-over test (close > 0) */
                 bstate_free(&bprev, 1);
             }
-            steps[st] = band_run(&b, &views[st].m, &c, cdelta * dn / vmax, sweeps, r0 * dnx / vmax);
+            steps[st] = band_run(&b, &views[st].m, &c, cdelta * dn / vmax, sweeps, r0 * dnx / vmax, 0.0, 0.0);
             bprev = b;
             have_b = 1;
         }
@@ -240,7 +247,8 @@ int oband_travel(double scx, double scz, int nnz, int nnx, const double *veln, c
         fstate_free(&h, 0);
         fstate_free(&hprev_keep, 1);
     }
-    steps[3] = band_run(&bm, base, &c, cdelta * dnx / vmax, sweeps, r0 * dnx / vmax);
+    steps[3] = band_run(&bm, base, &c, cdelta * dnx / vmax, sweeps, r0 * dnx / vmax, g_cdelta_far * dnx / vmax,
+                        g_r_far > 0 && g_cdelta_far > 0 ? g_r_far * dnx / vmax : 0.0);
     bstate_free(&bm, 0);
     for (int st = 0; st < 3; st++) free_view(&views[st]);
     free_base(&bb);

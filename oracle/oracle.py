@@ -177,13 +177,16 @@ def group_vel(angle, c_22, c_23, c_33, c_44, sigma, vel_scale=1):
 
 
 def band_travel(scx, scz, veln, velpn, vel_map, stif_den, avlist2, phase_vel, vmax, cdelta=0.25, exact_init=False,
-                sweeps=1, r0=0.0, exact_r=0.0, gox=0.0, goz=0.0, dnx=1e-3, dnz=None):
-    """CPU model of the MI355X band-synchronous formulation (oracle/band_model.c). Returns (T, steps[4])."""
+                sweeps=1, r0=0.0, exact_r=0.0, gox=0.0, goz=0.0, dnx=1e-3, dnz=None, cdelta_far=0.0, r_far=0.0):
+    """CPU model of the MI355X band-synchronous formulation (oracle/band_model.c). Returns (T, steps[4]).
+    cdelta_far / r_far: the device's optional wider band far from the source (0: off)."""
     m = _Model(veln, velpn, vel_map, stif_den, avlist2, phase_vel)
     dnz = dnx if dnz is None else dnz
     out = np.zeros((m.nnz, m.nnx))
     steps = np.zeros(4, dtype=np.int64)
     L = lib()
+    L.oband_set_far.argtypes = [_d, _d]
+    L.oband_set_far(float(cdelta_far), float(r_far))
     L.oband_travel.restype = _i
     L.oband_travel.argtypes = [_d, _d, _i, _i, _p, _p, _p, _p, _p, _p, _i, _d, _d, _d, _d, _d, _d, _i, _i, _d, _d, _p, _p]
     rc = L.oband_travel(scx, scz, m.nnz, m.nnx, _ptr(m.veln), _ptr(m.velpn), _ptr(m.vel_map), _ptr(m.stif),

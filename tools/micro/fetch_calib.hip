@@ -18,6 +18,14 @@ __global__ void gather8(const double* __restrict__ a, long lines, double* out) {
   if (v == 12345.678) out[0] = v;
 }
 
+// two lanes per line: offsets 0 and 64 of the same 128-byte line (one request or two sectors?)
+__global__ void gather8x2(const double* __restrict__ a, long lines, double* out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long l = ((i >> 1) * 40503L) & (lines - 1);
+  double v = (i >> 1) < lines ? a[l * 16 + (i & 1) * 8] : 0.0;
+  if (v == 12345.678) out[0] = v;
+}
+
 __global__ void stream16(const double4* __restrict__ a, long n4, double* out) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   double s = 0.0;
@@ -37,6 +45,7 @@ int main() {
   (void)hipMemset(a, 0, bytes);
   (void)hipDeviceSynchronize();
   hipLaunchKernelGGL(gather8, dim3((unsigned)(lines / 256)), dim3(256), 0, 0, a, lines, out);
+  hipLaunchKernelGGL(gather8x2, dim3((unsigned)(2 * lines / 256)), dim3(256), 0, 0, a, lines, out);
   hipLaunchKernelGGL(stream16, dim3(1024 * 8), dim3(256), 0, 0, (const double4*)a, bytes / 32, out);
   if (hipDeviceSynchronize() != hipSuccess) return 2;
   printf("{\"gather8_lines\": %ld, \"gather8_line_bytes\": %ld, \"stream16_bytes\": %ld}\n", lines, lines * 128,
