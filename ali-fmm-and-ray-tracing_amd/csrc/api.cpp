@@ -37,7 +37,7 @@ static void release_kept_rays(alifmm_ctx* c) {
 }
 static void free_arena(Arena& a) {
   dfree(a.S); dfree(a.own); dfree(a.lists); dfree(a.dlists); dfree(a.Ts); dfree(a.Ss); dfree(a.srcs); dfree(a.ho); dfree(a.jobs);
-  dfree(a.rimc); dfree(a.rimt); dfree(a.kx);
+  dfree(a.rimc); dfree(a.rimt); dfree(a.kx); dfree(a.Tb); dfree(a.Sb);
   dfree(a.dscx); dfree(a.dscz);
   a = Arena();
 }
@@ -366,10 +366,10 @@ static af::DevModel dev_model(const alifmm_ctx* c) {
 }
 
 static int ensure_arena(alifmm_ctx* ctx, int nsrc, long cells, long capL, long capC, long capS, int K, long capR,
-                        long ecells) {
+                        long ecells, long tbc, long sbc) {
   Arena& a = ctx->arena;
   if (a.nsrc >= nsrc && a.cells >= cells && a.capL >= capL && a.capC >= capC && a.capS >= capS && a.K >= K &&
-      a.capR >= capR && a.ecells >= ecells)
+      a.capR >= capR && a.ecells >= ecells && a.tbc >= tbc && a.sbc >= sbc)
     return ALIFMM_OK;
   free_arena(a);
   a.nsrc = nsrc;
@@ -380,6 +380,10 @@ static int ensure_arena(alifmm_ctx* ctx, int nsrc, long cells, long capL, long c
   a.K = K;
   a.capR = capR;
   a.ecells = ecells;
+  a.tbc = tbc;
+  a.sbc = sbc;
+  HIPCHK(dalloc(&a.Tb, (size_t)nsrc * tbc));
+  HIPCHK(dalloc(&a.Sb, (size_t)nsrc * sbc));
   HIPCHK(dalloc(&a.S, (size_t)nsrc * cells));
   HIPCHK(dalloc(&a.own, (size_t)nsrc * cells));
   HIPCHK(dalloc(&a.lists, (size_t)nsrc * (4 * capL + 6 * capC)));
@@ -453,8 +457,10 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
   const long nstripes = (fx + W - 1) / W;
   const long capR = K > 1 ? 2L * fz * ((nstripes + K - 1) / K) + 64 : 0;
   const long ecells = K > 1 ? nstripes * 4L * fz : 0;  // per edge buffer (4 columns per stripe)
+  // the band kernel's working field (af_band_tb_cells: its layout) and its edge buffers
+  const long tb_cells = af_band_tb_cells(fz, fx), tbc = tb_cells + 2 * ecells, sbc = af_band_sb_cells(fz, fx);
   // the arena is sized for this chunk (reused while later chunks fit in it)
-  int rc = ensure_arena(ctx, n, cells, capL, capC, capS, K, capR, ecells);
+  int rc = ensure_arena(ctx, n, cells, capL, capC, capS, K, capR, ecells, tbc, sbc);
   if (rc) return rc;
   Arena& a = ctx->arena;
   // subgrid 1: the fields are first written by the band kernel, so their initialisation runs on
@@ -468,7 +474,7 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
   std::vector<af::BandSrc> hs(n);
   for (int i = 0; i < n; i++) {
     int slot = first_slot + i;
-    if ((rc = af_ensure_field(ctx, slot, sg, fz, fx, 2 * ecells))) return rc;  // + the edge buffers
+    if ((rc = af_ensure_field(ctx, slot, sg, fz, fx))) return rc;
     af::BandSrc& b = hs[i];
     memset(&b, 0, sizeof b);
     b.T = ctx->fields[slot].d;
@@ -490,11 +496,14 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
     b.V = dbase + a.capL;
     b.Dv = b.V + a.capC;
     b.kx = a.kx + i;
+    b.Tb = a.Tb + (size_t)i * a.tbc;
+    HIPCHK(hipMemsetAsync(b.Tb, 0xFF, (size_t)tbc * 8, fs));  // far: NaN (working field + edge buffers)
+    b.Sb = a.Sb + (size_t)i * a.sbc;
+    HIPCHK(hipMemsetAsync(b.Sb, 0xFF, (size_t)sbc * 4, fs));  // kFar = -1
     if (K > 1) {
       b.rimc = a.rimc + (size_t)i * K * 2 * capR;
       b.rimt = a.rimt + (size_t)i * K * 2 * capR;
-      b.E = b.T + cells;  // edge buffers after the field (fmm_band_k.hip indexes both from T)
-      HIPCHK(hipMemsetAsync(b.E, 0xFF, (size_t)2 * ecells * 8, fs));  // far: NaN
+      b.E = b.Tb + tb_cells;  // edge buffers after the working field (fmm_band_k.hip indexes both from Tb)
     }
     if (capS > 0) {
       b.Ts[0] = a.Ts + (size_t)i * 2 * a.capS;
@@ -502,8 +511,10 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
       b.Ss[0] = a.Ss + (size_t)i * 2 * a.capS;
       b.Ss[1] = b.Ss[0] + a.capS;
     }
-    HIPCHK(hipMemsetAsync(b.T, 0xFF, (size_t)cells * 8, fs));  // far: NaN (fields.h)
-    HIPCHK(hipMemsetAsync(b.S, 0xFF, (size_t)cells * 4, fs));    // kFar = -1
+    // subgrid > 1: fmm_exact_kernel writes the exact region into the result field, which must
+    // start far (NaN, fields.h); subgrid 1: the band kernel's copy-out writes every cell
+    if (sg > 1) HIPCHK(hipMemsetAsync(b.T, 0xFF, (size_t)cells * 8, fs));
+    if (sg > 1) HIPCHK(hipMemsetAsync(b.S, 0xFF, (size_t)cells * 4, fs));  // the exact kernel's status: kFar
     HIPCHK(hipMemsetAsync(b.own, 0xFF, (size_t)cells * 4, fs));  // claim stamps -1
   }
   if (fs != ctx->stream) HIPCHK(hipEventRecord(ctx->ev_fill, fs));
@@ -535,6 +546,9 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
   P.wlog = wlog;
   P.capR = (int)capR;
   P.ecells = ecells;
+  P.tb_pitch = af_band_tb_pitch(fx);
+  P.tb_cells = tb_cells;
+  P.sb_pitch = af_band_sb_pitch(fx);
   P.max_steps = 200L * (fz + fx) + 100000;
   HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
   if (sg == 1) {
@@ -579,6 +593,7 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
   HIPCHK(af_launch_band_k(&P, ctx->stream));
   ctx->last_k = K;
   HIPCHK(hipEventRecord(ctx->ev[2], ctx->stream));
+  HIPCHK(af_launch_band_copy_out(&P, ctx->stream));  // working fields -> the row-major result fields
   if (sg > 1)
     for (int i = 0; i < n; i++) HIPCHK(af_launch_scale(hs[i].T, cells, (double)sg, ctx->stream));
   HIPCHK(hipMemcpyAsync(hs.data(), a.srcs, sizeof(af::BandSrc) * n, hipMemcpyDeviceToHost, ctx->stream));

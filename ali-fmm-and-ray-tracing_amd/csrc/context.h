@@ -36,6 +36,10 @@ struct Arena {  // per-chunk scratch, reused across calls
   int* rimc = nullptr;       // K-member kernel: rim lists [src][K][2][capR]
   double* rimt = nullptr;
   af::KX* kx = nullptr;      // K-member kernel: exchange blocks
+  double* Tb = nullptr;      // band kernel: working fields + their edge buffers, tbc doubles per source
+  long tbc = 0;
+  int* Sb = nullptr;         // band kernel: status arrays, sbc per source
+  long sbc = 0;
   double* Ts = nullptr;  // stage grids (travel_finer_grid), 2 per source
   int* Ss = nullptr;
   af::BandSrc* srcs = nullptr;

@@ -38,6 +38,7 @@
 // every wave before the flag, and read with sc1 loads after the flag (MI355X_MICROARCH.md
 // "inter-workgroup visibility", Valid forms).  Flags and rim lists are double-buffered by parity.
 #define CR_LDS_TABLES  // cr_math.h tables in LDS (crm::lds_init at kernel start)
+#include <algorithm>
 #include <type_traits>
 #include "kernels.h"
 #include "local_ops.h"
@@ -190,28 +191,83 @@ struct Lds {
 AF_DEV unsigned hslot(int key) { return ((unsigned)key * 2654435761u) >> (32 - kHashLog); }
 AF_DEV unsigned hstep(int key) { return (((unsigned)key * 0x85ebca6bu) >> (32 - kHashLog)) | 1u; }
 
+// The band kernel's working field Tb (per source, in the arena; its two edge buffers follow it):
+// AF_BRICK = 1 stores 4 x 4 bricks of doubles, one 128-byte line each, so the 12-point stencils
+// of a wavefront's cells touch fewer lines whatever the direction of the front (modelled on the
+// C4 front in the kernel's claim order: 0.87 instead of 1.26 lines per evaluated cell); 0 is
+// row-major.  af_launch_band_copy_out writes the row-major result after the band.
+#ifndef AF_BRICK
+#define AF_BRICK 1
+#endif
+struct TbLayout {
+  int pitch;  // bricks per brick row (AF_BRICK) or the row pitch
+  AF_DEV int at(int z, int x) const {
+#if AF_BRICK
+    return (((z >> 2) * pitch + (x >> 2)) << 4) | ((z & 3) << 2) | (x & 3);
+#else
+    return z * pitch + x;
+#endif
+  }
+};
+
+// The band kernel's status array Sb (far -1, known 0, close 1 + close-set slot; per source, in
+// the arena): AF_BRICK stores 4 x 8 bricks of int32, one 128-byte line each (claim items — the
+// 4-neighbours of tile-ordered accepted cells — then touch 0.17 instead of 0.31 lines per item on
+// the C4 front); 0 is row-major.
+struct SbLayout {
+  int pitch;  // bricks per brick row (AF_BRICK) or the row pitch
+  AF_DEV int at(int z, int x) const {
+#if AF_BRICK
+    return (((z >> 2) * pitch + (x >> 3)) << 5) | ((z & 3) << 3) | (x & 7);
+#else
+    return z * pitch + x;
+#endif
+  }
+};
+
+// 12-point neighbourhood of an interior cell (no other member's columns in reach) from Tb; same
+// values and validity as NbFieldT::load (rows past the grid invalid; other out-of-grid positions
+// read a clamped address and are never used: update() bounds-checks them)
+AF_DEV void load_tb(NbFieldT& nb, const double* Tb, const TbLayout& L, int nz, int nx, int z, int x) {
+  const int dz[12] = {0, 0, 0, 0, -2, -1, 1, 2, -1, -1, 1, 1};
+  const int dx[12] = {-2, -1, 1, 2, 0, 0, 0, 0, -1, 1, -1, 1};
+  nb.iz = z;
+  nb.ix = x;
+  double t[12];
+#pragma unroll
+  for (int k = 0; k < 12; k++) {
+    const int zz = min(max(z + dz[k], 0), nz - 1), xx = min(max(x + dx[k], 0), nx - 1);
+    t[k] = gld(Tb + L.at(zz, xx));
+  }
+  unsigned m = 0;
+#pragma unroll
+  for (int k = 0; k < 12; k++)
+    if (z + dz[k] < nz && t[k] == t[k]) m |= 1u << k;
+  nb.vm = m;
+  nb.t0 = t[0]; nb.t1 = t[1]; nb.t2 = t[2]; nb.t3 = t[3]; nb.t4 = t[4]; nb.t5 = t[5];
+  nb.t6 = t[6]; nb.t7 = t[7]; nb.t8 = t[8]; nb.t9 = t[9]; nb.t10 = t[10]; nb.t11 = t[11];
+}
+
 // Stencil neighbourhood (NbFieldT) at the state of the end of the previous step: own columns from
 // T, other members' columns from the previous step's edge buffer (the known sign dropped).  The
 // edge buffers follow T in the field's allocation, so every point is T[idx] with a 32-bit index
 // from one base (the loads keep the scalar-base + 32-bit-offset form): 12 independent loads in one
 // form (sc1: the edge buffer needs it), issued together.  Out-of-grid positions read a clamped
 // index (update() never uses them: it bounds-checks).
-AF_DEV void load_nb(NbFieldT& nb, const double* T, int eprv, int total, const KGeom& g, int z, int x) {
+AF_DEV void load_nb(NbFieldT& nb, const double* T, const TbLayout& L, int eprv, int total, const KGeom& g, int z,
+                    int x) {
   const int dz[12] = {0, 0, 0, 0, -2, -1, 1, 2, -1, -1, 1, 1};
   const int dx[12] = {-2, -1, 1, 2, 0, 0, 0, 0, -1, 1, -1, 1};
   nb.iz = z;
   nb.ix = x;
-  int zc[5], ro[5], cb[5];
+  int zc[5], cb[5];
   bool ot[5];
 #pragma unroll
-  for (int r = 0; r < 5; r++) {  // rows z-2 .. z+2 (clamped)
-    zc[r] = min(max(z + r - 2, 0), g.nz - 1);
-    ro[r] = zc[r] * g.nx;
-  }
+  for (int r = 0; r < 5; r++) zc[r] = min(max(z + r - 2, 0), g.nz - 1);  // rows z-2 .. z+2 (clamped)
 #pragma unroll
-  for (int c = 0; c < 5; c++) {  // columns x-2 .. x+2: own (row-major T) or edge buffer (column-major)
+  for (int c = 0; c < 5; c++) {  // columns x-2 .. x+2: own (working field) or edge buffer (column-major)
     ot[c] = g.other(x, c - 2);
-    cb[c] = ot[c] ? eprv + g.ecol(x + c - 2) * g.nz : x + c - 2;
+    cb[c] = ot[c] ? eprv + g.ecol(x + c - 2) * g.nz : min(max(x + c - 2, 0), g.nx - 1);
   }
   double t[12];
   // 32-bit byte offsets (scalar base + vector offset form) while field + edge buffers stay below
@@ -221,7 +277,7 @@ AF_DEV void load_nb(NbFieldT& nb, const double* T, int eprv, int total, const KG
 #pragma unroll
   for (int k = 0; k < 12; k++) {
     const int r = dz[k] + 2, c = dx[k] + 2;
-    const int i = cb[c] + (ot[c] ? zc[r] : ro[r]);
+    const int i = ot[c] ? cb[c] + zc[r] : L.at(zc[r], cb[c]);
     idx[k] = i < 0 ? 0 : i >= total ? total - 1 : i;
   }
   if (off32) {
@@ -349,7 +405,11 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
   // the neighbour members (stripes s - 1 and s + 1 of an own stripe s belong to them)
   const int mprev = me == 0 ? K - 1 : me - 1, mnext = me == K - 1 ? 0 : me + 1;
   double* T = B->T;
-  int* S = B->S;
+  double* const Tb = B->Tb;
+  const TbLayout TL{P.tb_pitch};
+  const SbLayout SL{P.sb_pitch};
+  int* const S = B->S;    // row-major status of fmm_exact_kernel's region (mode 1 hand-over only)
+  int* const Sb = B->Sb;  // the band's status
   int* own = B->own;
   DevModel M = P.M;
   crm::lds_init();
@@ -378,9 +438,9 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
   // step parity: no dynamically indexed private arrays, which would live in scratch)
   int* const rimc = B->rimc;
   double* const rimt = B->rimt;
-  // edge buffer of parity p: T + cells + p * ecells, compact (KGeom::eidx)
-  const int cells = nz * nx, ecells = (int)P.ecells;
-  double* const E0 = T + cells;
+  // edge buffer of parity p: Tb + tb_cells + p * ecells, compact (KGeom::eidx)
+  const int cells = nz * nx, ecells = (int)P.ecells, tbc = (int)P.tb_cells;
+  double* const E0 = Tb + tbc;
   if (tid == 0) {
     sh->hi = 0;
     sh->nF = 0;
@@ -407,12 +467,12 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
         if (g.owner(x) == me) {
           t = H->ttn[k];
           const bool known = H->cls[k] == 1;
-          gst(T + c, t);
+          gst(Tb + TL.at(z, x), t);
           if (g.edge(x)) {
             gst_sc1(E0 + g.eidx(z, x), known ? -t : t);
             gst_sc1(E0 + ecells + g.eidx(z, x), known ? -t : t);
           }
-          if (known) gst(S + c, (int)kKnown);
+          if (known) gst(Sb + SL.at(z, x), (int)kKnown);
           else push = true;
         }
       }
@@ -420,26 +480,32 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
       if (s >= 0) {
         L.put(s, pk(z, x));
         Lt.put(s, t);
-        gst(S + c, 1 + s);
+        gst(Sb + SL.at(z, x), 1 + s);
       }
     }
   } else {
     // travel_finer_grid(): fmm_exact_kernel wrote T / S of the exact region and its close cells in
     // Lin; the edge buffers get the region's edge cells (T is NaN outside what it touched)
+    // (and every member copies its own columns of the region into the working field)
     if (tid == 0 && B->err) sh->err = B->err;
-    if (K > 1) {
+    {
       const int z0 = max(0, B->bbox[0]), z1 = min(nz - 1, B->bbox[1]);
       const int x0 = max(0, B->bbox[2]), x1 = min(nx - 1, B->bbox[3]);
       const int w = x1 - x0 + 1;
       const long nb = (z1 >= z0 && w > 0) ? (long)(z1 - z0 + 1) * w : 0;
       for (long k = tid; k < nb; k += kThreads) {
         const int z = z0 + (int)(k / w), x = x0 + (int)(k % w);
-        if (g.owner(x) == me && g.edge(x)) {
+        if (g.owner(x) == me) {
           const long f = (long)z * nx + x;
           const double t = gld(T + f);
-          const double e = gld(S + f) == kKnown ? -t : t;
-          gst_sc1(E0 + g.eidx(z, x), e);
-          gst_sc1(E0 + ecells + g.eidx(z, x), e);
+          gst(Tb + TL.at(z, x), t);
+          const bool kn = gld(S + f) == kKnown;
+          if (kn) gst(Sb + SL.at(z, x), (int)kKnown);
+          if (g.edge(x)) {
+            const double e = kn ? -t : t;
+            gst_sc1(E0 + g.eidx(z, x), e);
+            gst_sc1(E0 + ecells + g.eidx(z, x), e);
+          }
         }
       }
     }
@@ -458,7 +524,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
       if (s >= 0) {
         L.put(s, pk(z, x));
         Lt.put(s, gld(T + c));
-        gst(S + c, 1 + s);
+        gst(Sb + SL.at(z, x), 1 + s);
       }
     }
   }
@@ -499,7 +565,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
     const int par = (int)(steps & 1), prv = par ^ 1;
     double* const Epar = E0 + par * ecells;
     const double* const Eprv = E0 + prv * ecells;
-    const int eprv = cells + prv * ecells;  // Eprv as an index from T
+    const int eprv = tbc + prv * ecells;  // Eprv as an index from Tb
     const int hi = sh->hi;
     // ---- P1: local Tmin over the close set (LDS); publish every own close RIM cell (cell, T) for
     // the neighbour members, which keep those with T <= thr; clear the claim hash ----
@@ -659,7 +725,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
               sh->err = 2;
             } else {
               AL.put(sa, c[u]);
-              gst(S + pk_flat(c[u], nx), (int)kKnown);
+              gst(Sb + SL.at(pkz(c[u]), pkx(c[u])), (int)kKnown);
               if (LO) {
                 Lt.put_lds(e, INFINITY);
                 FS.put_lds(sf, e);
@@ -760,7 +826,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
       // dedupe, whose LDS round trips then cover their latency (a duplicate's load is wasted)
 #pragma unroll
       for (int u = 0; u < kClaimU; u++)
-        s[u] = r[u] >= 0 ? gld(S + ((long)pkz(r[u]) * nx + pkx(r[u]))) : (int)kKnown;
+        s[u] = r[u] >= 0 ? gld(Sb + SL.at(pkz(r[u]), pkx(r[u]))) : (int)kKnown;
       if (use_hash) {
 #pragma unroll
         for (int u = 0; u < kClaimU; u++) pv[u] = r[u] >= 0 ? atomicCAS(&sh->H[hh[u]], 0, r[u] + 1) : 0;
@@ -889,8 +955,8 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
       const int r = lds_e ? EL.lds(e) : EL.get(e);
       const int z = pkz(r), x = pkx(r);
       NbFieldT nb;
-      if (interior) nb.load(T, nz, nx, z, x);
-      else load_nb(nb, T, eprv, cells + 2 * ecells, g, z, x);
+      if (interior) load_tb(nb, Tb, TL, nz, nx, z, x);
+      else load_nb(nb, Tb, TL, eprv, tbc + 2 * ecells, g, z, x);
       const CellMat cm = band_mat<LDSMAT>(M, sh->mat, sh->stab, R.mv, z, x);
 #if AF_DIAG_DBL  // diagnostic: a second, opaque update() per cell (its marginal cost), same results
       NbFieldT nb2 = nb;
@@ -933,8 +999,8 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
           if (zz >= 0 && zz < nz && xx >= 0 && xx < nx) {
             const long f = (long)zz * nx + xx;
             if (g.owner(xx) == me) {
-              t = far0(gld(T + f));
-              kn = gld(S + f) == kKnown;
+              t = far0(gld(Tb + TL.at(zz, xx)));
+              kn = gld(Sb + SL.at(zz, xx)) == kKnown;
             } else {  // known at the end of the last step (sign), or accepted now (close, T <= thr)
               const double ev = gld_sc1(Eprv + g.eidx(zz, xx));
               t = far0(fabs(ev));
@@ -1002,8 +1068,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
           r = LO ? EL.lds(e) : EL.get(e);
           v = LO ? VL.lds(e) : VL.get(e);
           const int p = LO ? EP.lds(e) : EP.get(e);
-          const long f = (long)pkz(r) * nx + pkx(r);
-          gst(T + f, v);
+          gst(Tb + TL.at(pkz(r), pkx(r)), v);
           ed = g.edge(pkx(r));
           if (ed) gst_sc1(Epar + g.eidx(pkz(r), pkx(r)), v);
           if (p >= 0) {
@@ -1031,7 +1096,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
               L.put(slot, ed ? (r | kDirty) : r);
               Lt.put(slot, v);
             }
-            gst(S + (long)pkz(r) * nx + pkx(r), 1 + slot);
+            gst(Sb + SL.at(pkz(r), pkx(r)), 1 + slot);
           }
         }
       }
@@ -1084,6 +1149,44 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
 
 // band-kernel workgroups one CU holds at once (the host sizes K so that every member is resident)
 extern "C" int af_band_wgs_per_cu() { return AF_WG_PER_CU; }
+
+extern "C" int af_band_tb_pitch(int nx) { return AF_BRICK ? (nx + 3) / 4 : nx; }
+extern "C" int af_band_sb_pitch(int nx) { return AF_BRICK ? (nx + 7) / 8 : nx; }
+extern "C" long af_band_sb_cells(int nz, int nx) {
+  return AF_BRICK ? 32L * ((nz + 3) / 4) * ((nx + 7) / 8) : (long)nz * nx;
+}
+extern "C" long af_band_tb_cells(int nz, int nx) {
+  return AF_BRICK ? 16L * ((nz + 3) / 4) * ((nx + 3) / 4) : (long)nz * nx;
+}
+
+namespace af {
+namespace kb {
+// working field -> row-major result: thread = 4 consecutive cells of a row (one brick row: 32
+// contiguous bytes read, 32 written), blockIdx.y = source
+__global__ __launch_bounds__(256) void band_copy_out_kernel(const BandSrc* src, int nz, int nx, int pitch) {
+  const BandSrc* B = src + blockIdx.y;
+  const double* __restrict__ Tb = B->Tb;
+  double* __restrict__ T = B->T;
+  const TbLayout L{pitch};
+  const int qx = (nx + 3) / 4;
+  const long nq = (long)nz * qx;
+  for (long q = (long)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += (long)gridDim.x * blockDim.x) {
+    const int z = (int)(q / qx), x0 = 4 * (int)(q - (long)z * qx);
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+      if (x0 + i < nx) T[(long)z * nx + x0 + i] = Tb[L.at(z, x0 + i)];
+  }
+}
+}  // namespace kb
+}  // namespace af
+
+extern "C" hipError_t af_launch_band_copy_out(const af::BandParams* P, hipStream_t stream) {
+  const long nq = (long)P->nz * ((P->nx + 3) / 4);
+  const unsigned bx = (unsigned)std::min<long>((nq + 255) / 256, 2048);
+  hipLaunchKernelGGL(af::kb::band_copy_out_kernel, dim3(bx, P->nsrc), dim3(256), 0, stream, P->src, P->nz, P->nx,
+                     P->tb_pitch);
+  return hipGetLastError();
+}
 
 // nsrc (padded to a multiple of 8) x K workgroups, AF_WG_PER_CU per CU, all resident
 extern "C" hipError_t af_launch_band_k(const af::BandParams* P, hipStream_t stream) {

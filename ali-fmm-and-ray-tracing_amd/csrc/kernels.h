@@ -17,8 +17,12 @@ struct KX {
 // one source of a band launch (fmm_exact_kernel / fmm_band_k_kernel); lists are split into K
 // per-member slices (capL / K, capC / K) that spill the LDS lists of the band kernel
 struct BandSrc {
-  double* T;      // field (main grid); the band kernel's edge buffers follow it (E)
-  int* S;         // status: far -1, known 0, close 1 + close-set slot
+  double* T;      // field (main grid, row-major): the result (fmm_band_k's copy-out writes it)
+  double* Tb;     // the band kernel's working field (layout fmm_band_k.hip TbLayout), its two edge
+                  // buffers after it
+  int* S;         // status, row-major: fmm_exact_kernel's (mode 1), read by the band's hand-over
+  int* Sb;        // the band kernel's status (layout fmm_band_k.hip SbLayout): far -1, known 0,
+                  // close 1 + close-set slot
   int* own;       // claim stamps (steps with more claim items than the LDS hash holds)
   int* Lin;       // mode 1: close cells handed over by fmm_exact_kernel (nl0 of them)
   int* L;         // close set: cells
@@ -76,6 +80,9 @@ struct BandParams {
   int wlog;  // fmm_band_k: stripe width log2
   int capR;  // fmm_band_k: rim-list capacity per member and parity
   long ecells;  // fmm_band_k: cells per edge buffer
+  int tb_pitch;   // fmm_band_k: working-field pitch (bricks per brick row, or row pitch)
+  long tb_cells;  // fmm_band_k: working-field size in doubles (the edge buffers follow)
+  int sb_pitch;   // fmm_band_k: status-array pitch
   long max_steps;  // fmm_band_k: a band still running after this many steps stops with error 8
 };
 
@@ -134,6 +141,13 @@ hipError_t af_launch_init(const af::DevModel* M, af::InitJob* jobs, int njobs, a
 hipError_t af_launch_exact(const af::BandParams* P, hipStream_t stream);
 hipError_t af_launch_band_k(const af::BandParams* P, hipStream_t stream);
 int af_band_wgs_per_cu(void);  // band-kernel workgroups resident per CU (fmm_band_k.hip AF_WG_PER_CU)
+// the band kernel's working-field layout: pitch and size (doubles) for an nz x nx main grid
+int af_band_tb_pitch(int nx);
+long af_band_tb_cells(int nz, int nx);
+int af_band_sb_pitch(int nx);
+long af_band_sb_cells(int nz, int nx);
+// working fields -> the row-major result fields of every source of the launch
+hipError_t af_launch_band_copy_out(const af::BandParams* P, hipStream_t stream);
 hipError_t af_launch_scale(double* T, long n, double sg, hipStream_t stream);
 hipError_t af_launch_rays(const af::RayParams* P, hipStream_t stream);
 hipError_t af_launch_pack_rays(const double* rx, const double* ry, const int* len, const long long* off, int nrays,
