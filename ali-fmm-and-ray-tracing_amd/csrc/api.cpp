@@ -108,9 +108,10 @@ int alifmm_ctx_create(int device, alifmm_ctx** out) {
 
 static void free_model(alifmm_ctx* c) {
   dfree(c->d_veln); dfree(c->d_vm); dfree(c->d_velpn); dfree(c->d_sidx); dfree(c->d_stab); dfree(c->d_gtab);
-  dfree(c->d_ptab); dfree(c->d_mid); dfree(c->d_mid8); dfree(c->d_mtab); dfree(c->d_mslo);
+  dfree(c->d_ptab); dfree(c->d_mid); dfree(c->d_mid8); dfree(c->d_mid8b); dfree(c->d_mtab); dfree(c->d_mslo);
   c->d_mid = nullptr;
   c->d_mid8 = nullptr;
+  c->d_mid8b = nullptr;
   c->d_mtab = nullptr;
   c->d_mslo = nullptr;
   c->nmat = 0;
@@ -312,6 +313,15 @@ int alifmm_set_model(alifmm_ctx* ctx, int nnz, int nnx, const double* veln, cons
         std::vector<unsigned char> m8(mid.begin(), mid.end());
         HIPCHK(dalloc(&ctx->d_mid8, n));
         HIPCHK(hipMemcpy(ctx->d_mid8, m8.data(), n, hipMemcpyHostToDevice));
+        // the same ids in 8 x 16 bricks (one 128-byte line each) for the band kernel's subgrid-1 view
+        const int bp = (nnx + 15) / 16, bz = (nnz + 7) / 8;
+        std::vector<unsigned char> mb((size_t)128 * bp * bz, 0);
+        for (int z = 0; z < nnz; z++)
+          for (int x = 0; x < nnx; x++)
+            mb[(((size_t)(z >> 3) * bp + (x >> 4)) << 7) | ((z & 7) << 4) | (x & 15)] = m8[(size_t)z * nnx + x];
+        HIPCHK(dalloc(&ctx->d_mid8b, mb.size()));
+        HIPCHK(hipMemcpy(ctx->d_mid8b, mb.data(), mb.size(), hipMemcpyHostToDevice));
+        ctx->mid8b_pitch = bp;
       }
       HIPCHK(hipMemcpy(ctx->d_mtab, recs.data(), recs.size() * sizeof(af::MatRec), hipMemcpyHostToDevice));
       ctx->nmat = (int)recs.size();
@@ -356,6 +366,8 @@ static af::DevModel dev_model(const alifmm_ctx* c) {
   M.nstab = c->nstab;
   M.mid = c->d_mid;
   M.mid8 = c->d_mid8;
+  M.mid8b = c->d_mid8b;
+  M.mid8b_pitch = c->mid8b_pitch;
   M.mtab = c->d_mtab;
   M.nmat = c->nmat;
   M.mslo = c->d_mslo;

@@ -149,12 +149,20 @@ struct RunCfg {
   double delta_far, tfar;  // band width far from the source (tfar 0: off)
 };
 
-// material of main-grid cell (z, x): LDSMAT = one id load + the LDS record; else four arrays
-template <bool LDSMAT>
+// material of main-grid cell (z, x): LDSMAT = one id load + the LDS record; else four arrays.
+// IDENT: the main grid is the model grid (subgrid 1): no view arithmetic (its four integer
+// divisions), and the ids from the bricked copy when there is one
+template <bool LDSMAT, bool IDENT = false>
 AF_DEV CellMat band_mat(const DevModel& M, const MatRec* mat, const double* stab, const MatView& v, int z, int x) {
   if (!LDSMAT) return cell_mat(M, v, z, x);
-  const long i = mv_cell(M, v, z, x);
-  const MatRec m = mat[M.mid8 ? (int)gld(M.mid8 + i) : gld(M.mid + i)];
+  int id;
+  if (IDENT && M.mid8b) {
+    id = (int)gld(M.mid8b + ((((long)(z >> 3) * M.mid8b_pitch + (x >> 4)) << 7) | ((z & 7) << 4) | (x & 15)));
+  } else {
+    const long i = IDENT ? (long)z * M.nx0 + x : mv_cell(M, v, z, x);
+    id = M.mid8 ? (int)gld(M.mid8 + i) : gld(M.mid + i);
+  }
+  const MatRec m = mat[id];
   CellMat r;
   r.velpn = m.velpn;
   r.veln = v.quant ? (double)(int)m.veln : m.veln;

@@ -69,6 +69,8 @@ struct alifmm_ctx {
   int nstab = 0;
   int* d_mid = nullptr;
   unsigned char* d_mid8 = nullptr;  // the same ids as bytes when there are <= 256 materials
+  unsigned char* d_mid8b = nullptr; // ... in 8 x 16 bricks (DevModel::mid8b)
+  int mid8b_pitch = 0;
   af::MatRec* d_mtab = nullptr;
   double* d_mslo = nullptr;  // fouds18_A() slownesses per material (DevModel::mslo)
   int nmat = 0;

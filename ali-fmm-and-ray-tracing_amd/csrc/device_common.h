@@ -111,6 +111,8 @@ struct DevModel {
   int ncol;
   const int* mid;        // material id per cell (into mtab), or nullptr when there are too many
   const unsigned char* mid8;  // the same ids as bytes when nmat <= 256, else nullptr
+  const unsigned char* mid8b; // mid8 in 8 x 16 bricks (one 128-byte line each; pitch mid8b_pitch
+  int mid8b_pitch;            // bricks per brick row), or nullptr: the band kernel's subgrid-1 view
   const MatRec* mtab;
   int nmat;
   const double* mslo;     // per material and MatView::quant: fouds18_A()'s 4 slownesses [nmat][2][4], or nullptr

@@ -957,7 +957,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
       NbFieldT nb;
       if (interior) load_tb(nb, Tb, TL, nz, nx, z, x);
       else load_nb(nb, Tb, TL, eprv, tbc + 2 * ecells, g, z, x);
-      const CellMat cm = band_mat<LDSMAT>(M, sh->mat, sh->stab, R.mv, z, x);
+      const CellMat cm = band_mat<LDSMAT, MODE == 0>(M, sh->mat, sh->stab, R.mv, z, x);
 #if AF_DIAG_DBL  // diagnostic: a second, opaque update() per cell (its marginal cost), same results
       NbFieldT nb2 = nb;
       double d0 = nb.t0;
@@ -1022,7 +1022,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
               const int c = EL.get(e);
               const int z = pkz(c), x = pkx(c);
               const Win5 F{win + 25 * ci, wmask[ci], z, x};
-              const CellMat cm = band_mat<LDSMAT>(M, sh->mat, sh->stab, R.mv, z, x);
+              const CellMat cm = band_mat<LDSMAT, MODE == 0>(M, sh->mat, sh->stab, R.mv, z, x);
               const double dnx_f = launder_u(R.dnx), dnz_f = launder_u(R.dnz);
               F18Part fp = fouds18_part<LDSMAT>(F, M, cm, z, x, dnx_f, dnz_f, nx, nz, mat_slo(M, R.mv, z, x), part);
 #pragma unroll
@@ -1042,7 +1042,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
             const int c = EL.get(e);
             const int z = pkz(c), x = pkx(c);
             const Win5 F{win + 25 * tid, wmask[tid], z, x};
-            const CellMat cm = band_mat<LDSMAT>(M, sh->mat, sh->stab, R.mv, z, x);
+            const CellMat cm = band_mat<LDSMAT, MODE == 0>(M, sh->mat, sh->stab, R.mv, z, x);
             const double dnx_f = launder_u(R.dnx), dnz_f = launder_u(R.dnz);
             double v;
             v = fouds18_w5<LDSMAT>(F, M, cm, z, x, dnx_f, dnz_f, nx, nz, mat_slo(M, R.mv, z, x));
