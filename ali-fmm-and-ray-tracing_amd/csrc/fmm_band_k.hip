@@ -104,7 +104,7 @@ constexpr int kBcap = 512 / AF_WG_PER_CU, kDcap = 512 / AF_WG_PER_CU, kRcap = 10
 constexpr int kHashLog = AF_HASHLOG_D;
 constexpr int kHash = 1 << kHashLog;
 #ifndef AF_CLAIM_U
-#define AF_CLAIM_U 2
+#define AF_CLAIM_U 1
 #endif
 #ifndef AF_X1_SLEEP
 #define AF_X1_SLEEP 1
