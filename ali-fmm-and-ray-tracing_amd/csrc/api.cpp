@@ -605,7 +605,6 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
   HIPCHK(af_launch_band_k(&P, ctx->stream));
   ctx->last_k = K;
   HIPCHK(hipEventRecord(ctx->ev[2], ctx->stream));
-  HIPCHK(af_launch_band_copy_out(&P, ctx->stream));  // working fields -> the row-major result fields
   if (sg > 1)
     for (int i = 0; i < n; i++) HIPCHK(af_launch_scale(hs[i].T, cells, (double)sg, ctx->stream));
   HIPCHK(hipMemcpyAsync(hs.data(), a.srcs, sizeof(af::BandSrc) * n, hipMemcpyDeviceToHost, ctx->stream));

@@ -195,7 +195,7 @@ AF_DEV unsigned hstep(int key) { return (((unsigned)key * 0x85ebca6bu) >> (32 - 
 // AF_BRICK = 1 stores 4 x 4 bricks of doubles, one 128-byte line each, so the 12-point stencils
 // of a wavefront's cells touch fewer lines whatever the direction of the front (modelled on the
 // C4 front in the kernel's claim order: 0.87 instead of 1.26 lines per evaluated cell); 0 is
-// row-major.  af_launch_band_copy_out writes the row-major result after the band.
+// row-major.  Each member writes the row-major result of its stripes at the end (copy_out_own).
 #ifndef AF_BRICK
 #define AF_BRICK 1
 #endif
@@ -209,6 +209,41 @@ struct TbLayout {
 #endif
   }
 };
+
+// Working field -> row-major result for the stripes member `me` owns (s = me, me + K, ...; stripe
+// widths are multiples of 4, so bricks never straddle two owners).  Item = one 4 x 4 brick: one
+// contiguous 128-B line read, four 32-B row pieces written; consecutive lanes take consecutive
+// bricks of a stripe row, so a wave reads contiguous lines and writes 512-B row segments.
+AF_DEV void copy_out_own(double* __restrict__ T, const double* __restrict__ Tb, const TbLayout& L, const KGeom& g,
+                         int me, int nz, int nx, int tid) {
+  const int nstr = (nx + (1 << g.wlog) - 1) >> g.wlog;
+  const int nown = (nstr - me + g.K - 1) / g.K;
+  const int qlog = g.wlog - 2;  // bricks per stripe row: 1 << qlog
+  const long nq = (long)((nz + 3) >> 2) * nown << qlog;
+  const bool vec = AF_BRICK && (nx & 3) == 0;
+  for (long q = tid; q < nq; q += kThreads) {
+    const int c = (int)(q & ((1 << qlog) - 1));
+    const long r = q >> qlog;
+    const int zb = (int)(r / nown), js = (int)(r - (long)zb * nown);
+    const int x0 = ((me + js * g.K) << g.wlog) + 4 * c, z0 = 4 * zb;
+    if (x0 >= nx) continue;
+    if (vec && z0 + 4 <= nz) {
+      const double2* s = reinterpret_cast<const double2*>(Tb + L.at(z0, x0));
+      double2 v[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) v[k] = s[k];
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        double2* d = reinterpret_cast<double2*>(T + (long)(z0 + i) * nx + x0);
+        d[0] = v[2 * i];
+        d[1] = v[2 * i + 1];
+      }
+    } else {
+      for (int i = 0; i < 4 && z0 + i < nz; i++)
+        for (int k = 0; k < 4 && x0 + k < nx; k++) T[(long)(z0 + i) * nx + x0 + k] = Tb[L.at(z0 + i, x0 + k)];
+    }
+  }
+}
 
 // The band kernel's status array Sb (far -1, known 0, close 1 + close-set slot; per source, in
 // the arena): AF_BRICK stores 4 x 8 bricks of int32, one 128-byte line each (claim items — the
@@ -1126,6 +1161,10 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
   }
 #undef AF_TICK
 #undef AF_SUBT
+  // the row-major result: each member writes its own stripes' cells as soon as its source is
+  // done, so the copy-out of early sources overlaps the band of the late ones
+  __syncthreads();
+  copy_out_own(T, Tb, TL, g, me, nz, nx, tid);
   if (prof) {
     for (int k = 0; k < 6; k++) B->ph[k] += ph[k];
     for (int k = 0; k < 4; k++) B->sub[k] += sub[k];
@@ -1157,35 +1196,6 @@ extern "C" long af_band_sb_cells(int nz, int nx) {
 }
 extern "C" long af_band_tb_cells(int nz, int nx) {
   return AF_BRICK ? 16L * ((nz + 3) / 4) * ((nx + 3) / 4) : (long)nz * nx;
-}
-
-namespace af {
-namespace kb {
-// working field -> row-major result: thread = 4 consecutive cells of a row (one brick row: 32
-// contiguous bytes read, 32 written), blockIdx.y = source
-__global__ __launch_bounds__(256) void band_copy_out_kernel(const BandSrc* src, int nz, int nx, int pitch) {
-  const BandSrc* B = src + blockIdx.y;
-  const double* __restrict__ Tb = B->Tb;
-  double* __restrict__ T = B->T;
-  const TbLayout L{pitch};
-  const int qx = (nx + 3) / 4;
-  const long nq = (long)nz * qx;
-  for (long q = (long)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += (long)gridDim.x * blockDim.x) {
-    const int z = (int)(q / qx), x0 = 4 * (int)(q - (long)z * qx);
-#pragma unroll
-    for (int i = 0; i < 4; i++)
-      if (x0 + i < nx) T[(long)z * nx + x0 + i] = Tb[L.at(z, x0 + i)];
-  }
-}
-}  // namespace kb
-}  // namespace af
-
-extern "C" hipError_t af_launch_band_copy_out(const af::BandParams* P, hipStream_t stream) {
-  const long nq = (long)P->nz * ((P->nx + 3) / 4);
-  const unsigned bx = (unsigned)std::min<long>((nq + 255) / 256, 2048);
-  hipLaunchKernelGGL(af::kb::band_copy_out_kernel, dim3(bx, P->nsrc), dim3(256), 0, stream, P->src, P->nz, P->nx,
-                     P->tb_pitch);
-  return hipGetLastError();
 }
 
 // nsrc (padded to a multiple of 8) x K workgroups, AF_WG_PER_CU per CU, all resident

@@ -147,7 +147,6 @@ long af_band_tb_cells(int nz, int nx);
 int af_band_sb_pitch(int nx);
 long af_band_sb_cells(int nz, int nx);
 // working fields -> the row-major result fields of every source of the launch
-hipError_t af_launch_band_copy_out(const af::BandParams* P, hipStream_t stream);
 hipError_t af_launch_scale(double* T, long n, double sg, hipStream_t stream);
 hipError_t af_launch_rays(const af::RayParams* P, hipStream_t stream);
 hipError_t af_launch_pack_rays(const double* rx, const double* ry, const int* len, const long long* off, int nrays,
