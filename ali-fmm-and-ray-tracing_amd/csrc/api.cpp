@@ -71,6 +71,8 @@ static double christoffel_group_host(const double* s, double eff, double vm) {
 static const int kMaxMatIds = 4096;
 // plane-search candidates per ray the ray kernel holds (rays.hip kMaxCand)
 static const int kMaxRayCand = 256;
+// ray point buffers larger than this are freed at the end of each alifmm_find_rays call
+static const size_t kRayBufKeepBytes = (size_t)1 << 30;
 
 extern "C" {
 
@@ -979,6 +981,9 @@ int alifmm_find_rays(alifmm_ctx* ctx, int npairs, const int32_t* field_slot, con
     if (!rc) rc = fail(ctx, ALIFMM_E_KERNEL, "find_rays: kept points do not add up to the ray lengths");
   }
   cleanup();
+  // point buffers above kRayBufKeepBytes (C4: 8192 rays x 40 960 points x 16 B = 5.4 GB) are not kept
+  // between calls, so they do not hold device memory that later travel / arena allocations need
+  if (rb.pts * 2 * sizeof(double) > kRayBufKeepBytes) free_ray_bufs(ctx);
   return rc;
 }
 
