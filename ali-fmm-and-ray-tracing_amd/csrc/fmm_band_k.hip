@@ -137,7 +137,10 @@ constexpr int kHash = 1 << kHashLog;
 #ifndef AF_SORT_ACC
 #define AF_SORT_ACC 256
 #endif
-constexpr int kSortB = AF_SORTB_D;
+#ifndef AF_SORTB
+#define AF_SORTB AF_SORTB_D
+#endif
+constexpr int kSortB = AF_SORTB;
 AF_DEV int tile_bucket(int c) { return ((pkz(c) >> 3) & (kSortB / 32 - 1)) << 5 | ((pkx(c) >> 3) & 31); }
 constexpr int kClaimU = AF_CLAIM_U;  // claim items per lane per pass
 #ifndef AF_ACC_U

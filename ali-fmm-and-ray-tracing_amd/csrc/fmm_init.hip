@@ -25,6 +25,19 @@ constexpr int kInitDec = 37 * 37;     // decimated stage-1/2 grid
 constexpr int kInitWin = 53 * 53;     // coarse cells under a stage grid / the prefix window
 constexpr int kInitStab = 64;         // stiffness rows staged in LDS
 constexpr int kSpec = 64;             // speculative relaxations kept by the relax role (one per lane)
+// diagnostic build (AF_INIT_DIAG=1): shader-clock cycles of the walk's activities, summed over the
+// stages into prof[8..15] (heap: wait for relaxations, downtree, add/upd, classify; relax: wait
+// for a pop, verification passes, evaluation passes, verification-pass count)
+#ifndef AF_INIT_DIAG
+#define AF_INIT_DIAG 0
+#endif
+#if AF_INIT_DIAG
+#define AF_DG_T0(v) const long long v = clock64();
+#define AF_DG_ADD(L, k, v) (L)->dg[k] += clock64() - (v);
+#else
+#define AF_DG_T0(v)
+#define AF_DG_ADD(L, k, v)
+#endif
 
 // a relaxation evaluated ahead of its turn: the node (z << 8 | x, -1: empty), update()'s stencil
 // stage on the state it saw, and the value
@@ -54,6 +67,9 @@ struct InitLds {
   SpecEnt spec[kSpec];              // speculative relaxations (relax_role)
   long long rbusy;                  // profile: relax-role ticks of the current walk
   long long rjobs;                  // profile: relaxations | fouds18_A() fallbacks << 32
+#if AF_INIT_DIAG
+  long long dg[8];                  // diagnostic build: shader-clock cycles per activity (AF_DG)
+#endif
 };
 
 struct LdsField {
@@ -294,12 +310,18 @@ AF_DEV bool pop_two_role(Heap& h, int& seq, int& jobs, int n) {
   }
   L->njob = n;
   post(&L->cmd, ++seq);
+  AF_DG_T0(td)
   h.down();
+  AF_DG_ADD(L, 1, td)
   for (int k = 0; k < n; k++) {
+    AF_DG_T0(tw)
     if (!await_at_least(&L->done, jobs + k + 1)) return false;
+    AF_DG_ADD(L, 0, tw)
+    AF_DG_T0(ta)
     if (L->jkind[k] & kJobAdd) h.add(L->jz[k], L->jx[k], true);
     else h.upd(L->jz[k], L->jx[k]);
     if (h.ndup) h.sync(L->jz[k], L->jx[k]);
+    AF_DG_ADD(L, 2, ta)
   }
   jobs += n;
   return true;
@@ -334,7 +356,9 @@ AF_DEV void relax_role(InitLds* L, const DevModel& M, const MatView& mv, const M
   L->spec[lane].cell = -1;
   while (true) {
     int cmd = 0;
+    AF_DG_T0(tcw)
     if (lane == 0) cmd = await_change(&L->cmd, last);
+    if (lane == 0) { AF_DG_ADD(L, 4, tcw) }
     cmd = __shfl(cmd, 0);
     if (cmd < 0) break;  // stop (or timeout: the heap role is gone)
     last = cmd;
@@ -342,6 +366,7 @@ AF_DEV void relax_role(InitLds* L, const DevModel& M, const MatView& mv, const M
     const int nj = L->njob;  // read once: the heap role refills the jobs after the last one is done
     int k0 = 0;
     while (k0 < nj) {
+      AF_DG_T0(tv)
       // the entries of jobs k0.. (one ballot each), then one pass in which lane k - k0 re-runs job k's
       // stencil stage on the current state with jobs k0..k-1 set to their entries' values
       int src[4] = {-1, -1, -1, -1};
@@ -386,7 +411,12 @@ AF_DEV void relax_role(InitLds* L, const DevModel& M, const MatView& mv, const M
       }
       njobs += hk;
       k0 += hk;
+      if (lane == 0) { AF_DG_ADD(L, 5, tv) }
+#if AF_INIT_DIAG
+      if (lane == 0) L->dg[7]++;
+#endif
       if (k0 >= nj) break;
+      AF_DG_T0(tf)
       // job k0 in turn: one pass, this job on lane 0, guesses of the next pops' jobs on the others
       const int lz = L->jz[k0], lx = L->jx[k0], kind = L->jkind[k0];
       const int iz = lz + R.oz, ix = lx + R.ox;
@@ -432,6 +462,7 @@ AF_DEV void relax_role(InitLds* L, const DevModel& M, const MatView& mv, const M
         L->T[lz * R.w + lx] = v;
         if (kind & kJobAdd) L->S[lz * R.w + lx] = 1;  // valid for the next relaxations (addtree sets the index)
         post(&L->done, (int)(njobs + 1));
+        AF_DG_ADD(L, 6, tf)
       }
       njobs++;
       k0++;
@@ -453,6 +484,7 @@ AF_DEV void stage_loop(Heap& h, const DevModel& M, const StageCfg& c, int tid) {
     int seq = 0, jobs = 0;
     bool finished = false;
     while (h.ntr > 0 && !finished && !h.err) {
+      AF_DG_T0(tc)
       const int ix = h.bx(1), iz = h.bz(1);
       L->S[iz * nx + ix] = 0;
       int n = 0;
@@ -484,6 +516,7 @@ AF_DEV void stage_loop(Heap& h, const DevModel& M, const StageCfg& c, int tid) {
           finished = true;
         }
       }
+      AF_DG_ADD(L, 3, tc)
       if (!pop_two_role(h, seq, jobs, n)) h.err = 1;
     }
     post(&L->cmd, -1);
@@ -594,6 +627,9 @@ __global__ __launch_bounds__(128) void fmm_init_kernel(DevModel M0, InitJob* job
   }
   if (src >= njobs) return;
   const int lane = threadIdx.x, nl = blockDim.x;
+#if AF_INIT_DIAG
+  if (lane < 8) L->dg[lane] = 0;
+#endif
   InitJob J = jobs[src];
   const int nnz = M.nz0, nnx = M.nx0;
   const long isx = J.isx, isz = J.isz;
@@ -744,6 +780,9 @@ __global__ __launch_bounds__(128) void fmm_init_kernel(DevModel M0, InitJob* job
           O->cls[n] = st == 0 ? 1 : 3;
           n++;
         }
+#if AF_INIT_DIAG
+        for (int k = 0; k < 8; k++) O->prof[8 + k] = L->dg[k];
+#endif
         O->n = n;
         O->err = err;
       }
@@ -764,6 +803,9 @@ __global__ __launch_bounds__(128) void fmm_init_kernel(DevModel M0, InitJob* job
       O->cls[n] = cls;
       n++;
     }
+#if AF_INIT_DIAG
+    for (int k = 0; k < 8; k++) O->prof[8 + k] = L->dg[k];
+#endif
     O->n = n;
     O->err = err;
   }

@@ -1,0 +1,32 @@
+"""Init-kernel activity breakdown (diagnostic build AF_INIT_DIAG=1, GPU box): mean shader-clock
+cycles per pop of the heap role (wait for relaxations, downtree, add/upd, classify) and of the relax
+role (wait for a pop, verification passes, evaluation passes), C4 grid -> one JSON line.
+ALIFMM_LIB=variants/idiag/libalifmm.so python tools/init_diag.py [sources]"""
+import json
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "ali-fmm-and-ray-tracing_amd"), os.path.join(REPO, "tests")]
+import _alifmm  # noqa: E402
+import workloads as W  # noqa: E402
+
+ctx = _alifmm.Context(0)
+vt = W.default_table()
+ctx.set_model(*W.weldlike_model(), vt, vt, W.weldlike_dnx())
+sx, sz = W.c4_sources(128)
+ns = int(sys.argv[1]) if len(sys.argv) > 1 else 128
+ctx.travel(sx[:ns], sz[:ns], copy_out=False)
+ctx.travel(sx[:ns], sz[:ns], copy_out=False)
+ti, tb, _ = ctx.last_timing()
+P = np.array([ctx.init_profile(i) for i in range(ns)], dtype=np.float64)
+m = P.mean(axis=0)
+pops = float(m[4:8].sum())
+walk_ticks = float(m[0:4].sum())
+names = ["heap_wait_relax", "heap_down", "heap_addupd", "heap_classify", "relax_wait_pop", "relax_verify",
+         "relax_eval", "verify_passes"]
+out = {"sources": ns, "init_ms": ti, "pops": pops, "walk_us_per_pop": walk_ticks / 100 / pops,
+       "cycles_per_pop": {n: round(m[8 + k] / pops, 1) for k, n in enumerate(names)}}
+print(json.dumps(out))
