@@ -843,7 +843,26 @@ int alifmm_find_rays(alifmm_ctx* ctx, int npairs, const int32_t* field_slot, con
                   6 * g.first + 3, kMaxRayCand);
   // chunk of rays per launch; the point buffers (chunk x max_pts per coordinate) are sized to the
   // request and kept in the context for the next call
-  const int chunk = std::min(8192, npairs);
+  // Rays per launch: wavefronts for every SIMD at the ray kernel's occupancy (af_ray_waves_per_simd;
+  // 8 192 rays at 16 lanes per ray and 2 wavefronts per SIMD), balanced over the launches, with the
+  // point buffers within a quarter of the free device memory.
+  int chunk = 8192;
+  {
+    int rays_per_wave = 64;
+    for (auto& g : by_sg) {
+      const int nc = 6 * g.first + 3;
+      rays_per_wave = std::min(rays_per_wave, nc <= 16 ? 4 : nc <= 32 ? 2 : 1);
+    }
+    const long target = (long)std::max(ctx->n_cu, 1) * 4 * af_ray_waves_per_simd() * rays_per_wave;
+    size_t free_b = 0, total_b = 0;
+    long by_mem = target;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess)
+      by_mem = (long)(free_b / 4 / ((size_t)max_pts * 2 * sizeof(double) + 64));
+    const long cmax = std::max(1024L, std::min(target, by_mem));
+    const long nlaunch = (npairs + cmax - 1) / cmax;
+    chunk = (int)((npairs + nlaunch - 1) / nlaunch);
+  }
+  chunk = std::min(chunk, npairs);
   auto& rb = ctx->rb;
   if (rb.rays < chunk || rb.pts < (size_t)chunk * max_pts) {
     free_ray_bufs(ctx);

@@ -24,7 +24,6 @@ constexpr int kInitMat = 256;         // material records staged in LDS (DevMode
 constexpr int kInitDec = 37 * 37;     // decimated stage-1/2 grid
 constexpr int kInitWin = 53 * 53;     // coarse cells under a stage grid / the prefix window
 constexpr int kInitStab = 64;         // stiffness rows staged in LDS
-constexpr int kSpec = 64;             // speculative relaxations kept by the relax role (one per lane)
 // diagnostic build (AF_INIT_DIAG=1): shader-clock cycles of the walk's activities, summed over the
 // stages into prof[8..15] (heap: wait for relaxations, downtree, add/upd, classify; relax: wait
 // for a pop, verification passes, evaluation passes, verification-pass count)
@@ -38,14 +37,6 @@ constexpr int kSpec = 64;             // speculative relaxations kept by the rel
 #define AF_DG_T0(v)
 #define AF_DG_ADD(L, k, v)
 #endif
-
-// a relaxation evaluated ahead of its turn: the node (z << 8 | x, -1: empty), update()'s stencil
-// stage on the state it saw, and the value
-struct SpecEnt {
-  int cell;
-  double val;
-  UpdSel sel;
-};
 
 struct InitLds {
   double T[kInitMaxN];
@@ -63,8 +54,7 @@ struct InitLds {
   // heap role -> relax role hand-off of one pop's neighbours (two-wavefront heap walk)
   int cmd, done;                    // sequence numbers (cmd -1: stop)
   int njob;
-  int jz[4], jx[4], jkind[4];       // kind: 1 add (far), 2 upd (close), +4: stage-1 quirk nnz
-  SpecEnt spec[kSpec];              // speculative relaxations (relax_role)
+  alignas(16) int job[4];           // packed (job_pack): node, kind 1 add (far), 2 upd (close), +4: stage-1 quirk nnz
   long long rbusy;                  // profile: relax-role ticks of the current walk
   long long rjobs;                  // profile: relaxations | fouds18_A() fallbacks << 32
 #if AF_INIT_DIAG
@@ -268,6 +258,11 @@ AF_DEV double fouds18_win(const WinField& F, const DevModel& M, const CellMat& c
 // after its relaxation, as the reference's addtree would before the next neighbour is relaxed.
 // Same results as the one-lane walk, with downtree off the critical path.
 constexpr int kJobAdd = 1, kJobUpd = 2, kJobQuirk = 4;
+// packed relaxation job: LDS-local node z << 8 | x, kind << 16
+AF_DEV int job_z(int j) { return (j >> 8) & 255; }
+AF_DEV int job_x(int j) { return j & 255; }
+AF_DEV int job_kind(int j) { return j >> 16; }
+AF_DEV int job_pack(int z, int x, int kind) { return (z << 8) | x | (kind << 16); }
 AF_DEV void post(int* w, int v) { __hip_atomic_store(w, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP); }
 // the waiting role backs off between polls (s_sleep) so that it does not take issue slots and
 // LDS cycles from the working one
@@ -318,9 +313,10 @@ AF_DEV bool pop_two_role(Heap& h, int& seq, int& jobs, int n) {
     if (!await_at_least(&L->done, jobs + k + 1)) return false;
     AF_DG_ADD(L, 0, tw)
     AF_DG_T0(ta)
-    if (L->jkind[k] & kJobAdd) h.add(L->jz[k], L->jx[k], true);
-    else h.upd(L->jz[k], L->jx[k]);
-    if (h.ndup) h.sync(L->jz[k], L->jx[k]);
+    const int jk = L->job[k];
+    if (job_kind(jk) & kJobAdd) h.add(job_z(jk), job_x(jk), true);
+    else h.upd(job_z(jk), job_x(jk));
+    if (h.ndup) h.sync(job_z(jk), job_x(jk));
     AF_DG_ADD(L, 2, ta)
   }
   jobs += n;
@@ -331,7 +327,7 @@ AF_DEV bool pop_two_role(Heap& h, int& seq, int& jobs, int n) {
 // ones' new values (the reference's sequence).  Relaxations are evaluated ahead of their turn, 64 at
 // a time: when a job has no usable speculative value, the whole wavefront runs one pass in which
 // lane 0 evaluates that job and every other lane a neighbour of one of the heap's first 16 entries
-// (the next pops), against the current state; each lane keeps its result (SpecEnt).  A job whose
+// (the next pops), against the current state; each lane keeps its result in registers.  A job whose
 // node has an entry only re-runs update()'s cheap stencil stage on the state of its turn: equal
 // to the entry's (same stencil, same input values), the entry's value is the job's value —
 // update()'s value is a function of its stencil stage's outputs — so the results are the
@@ -347,13 +343,25 @@ struct RelaxWin {
   int has_quirk;          // this walk has quirk jobs (close x-neighbours in stage 1)
 };
 
+// v of lane l (l wave-uniform)
+AF_DEV double readlane_d(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)b, l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
 template <bool LDSMAT>
 AF_DEV void relax_role(InitLds* L, const DevModel& M, const MatView& mv, const MidWin& mw, const RelaxWin& R,
                        int lane) {
   int last = 0;
   long long busy = 0, njobs = 0, nf18 = 0, nburst = 0;
   const int wz = R.z1 - R.z0, wx = R.x1 - R.x0;  // local coordinate bounds (0..wz, 0..wx)
-  L->spec[lane].cell = -1;
+  // this lane's speculative relaxation, kept in registers: node (LDS-local z << 8 | x; -1: none),
+  // value, and update()'s stencil stage on the state it saw
+  int my_cell = -1;
+  double my_val = 0.0;
+  UpdSel my_sel{};
   while (true) {
     int cmd = 0;
     AF_DG_T0(tcw)
@@ -363,51 +371,64 @@ AF_DEV void relax_role(InitLds* L, const DevModel& M, const MatView& mv, const M
     if (cmd < 0) break;  // stop (or timeout: the heap role is gone)
     last = cmd;
     const long long t0 = wall_clock64();
-    const int nj = L->njob;  // read once: the heap role refills the jobs after the last one is done
+    // the pop's jobs (read once: the heap role refills them after the last one is done), in
+    // wave-uniform registers; job(i) selects without dynamic indexing
+    const int nj = L->njob;
+    const int4 jv = *reinterpret_cast<const int4*>(L->job);
+    auto job = [&](int i) { return i == 0 ? jv.x : i == 1 ? jv.y : i == 2 ? jv.z : jv.w; };
     int k0 = 0;
     while (k0 < nj) {
       AF_DG_T0(tv)
-      // the entries of jobs k0.. (one ballot each), then one pass in which lane k - k0 re-runs job k's
-      // stencil stage on the current state with jobs k0..k-1 set to their entries' values
+      // the entries of jobs k0.. (one ballot each: the lowest lane holding the job's node) and
+      // their values; then the lane holding job k's entry re-runs its stencil stage on the current
+      // state with jobs k0..k-1 set to their entries' values
       int src[4] = {-1, -1, -1, -1};
+      double sv[4] = {-1.0, -1.0, -1.0, -1.0};
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         if (k0 + k < nj) {
-          const int key = (L->jz[k0 + k] << 8) | L->jx[k0 + k];
-          const unsigned long long hm = __ballot(L->spec[lane].cell == key);
-          src[k] = hm ? __ffsll((long long)hm) - 1 : -1;
+          const unsigned long long hm = __ballot(my_cell == (job(k0 + k) & 0xffff));
+          if (hm) {
+            src[k] = __ffsll((long long)hm) - 1;
+            sv[k] = readlane_d(my_val, src[k]);
+          }
         }
       }
       bool ok = false;
       {
-        const int q = lane, k = k0 + lane;
-        int sq = -1;
+        int q = -1;  // the job whose entry this lane holds
 #pragma unroll
-        for (int u = 0; u < 4; u++) sq = u == q ? src[u] : sq;
-        bool prior = true;  // every job k0..k-1 has an entry with a usable value
+        for (int k = 0; k < 4; k++) q = src[k] == lane ? k : q;
+        bool prior = true;  // every job k0..k0+q-1 has an entry with a usable value
 #pragma unroll
-        for (int u = 0; u < 4; u++) prior = prior && (u >= q || (src[u] >= 0 && L->spec[src[u]].val != -1.0));
-        if (k < nj && sq >= 0 && prior && L->spec[sq].val != -1.0) {
-          const int lz = L->jz[k], lx = L->jx[k], kind = L->jkind[k];
+        for (int u = 0; u < 4; u++) prior = prior && (u >= q || (src[u] >= 0 && sv[u] != -1.0));
+        if (q >= 0 && prior && my_val != -1.0) {
+          const int jq = job(k0 + q);
+          const int lz = job_z(jq), lx = job_x(jq);
           const int iz = lz + R.oz, ix = lx + R.ox;
           NbFieldT nb;
           nb.load_lds(L->T, L->S, R.z0, R.x0, R.z1, R.x1, R.w, iz, ix);
 #pragma unroll
           for (int u = 0; u < 3; u++)
-            if (u < q) nb.patch(L->jz[k0 + u] - lz, L->jx[k0 + u] - lx, L->spec[src[u]].val);
-          ok = update_nb_select(nb, iz, ix, (kind & kJobQuirk) ? R.quirk_nnz : R.nnz, R.nnx).same(L->spec[sq].sel);
+            if (u < q) nb.patch(job_z(job(k0 + u)) - lz, job_x(job(k0 + u)) - lx, sv[u]);
+          ok = update_nb_select(nb, iz, ix, (job_kind(jq) & kJobQuirk) ? R.quirk_nnz : R.nnz, R.nnx).same(my_sel);
         }
       }
       const unsigned long long okm = __ballot(ok);
       int hk = 0;  // leading confirmed jobs
-      while (k0 + hk < nj && ((okm >> hk) & 1ull)) hk++;
-      if (lane == 0) {
-        for (int u = 0; u < hk; u++) {
-          const int k = k0 + u, lz = L->jz[k], lx = L->jx[k];
-          L->T[lz * R.w + lx] = L->spec[src[u]].val;
-          if (L->jkind[k] & kJobAdd) L->S[lz * R.w + lx] = 1;  // valid for the next relaxations
-          post(&L->done, (int)(njobs + u + 1));
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        if (hk == k && k0 + k < nj && src[k] >= 0 && ((okm >> src[k]) & 1ull)) hk = k + 1;
+      if (lane == 0 && hk > 0) {
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          if (u < hk) {
+            const int ju = job(k0 + u);
+            L->T[job_z(ju) * R.w + job_x(ju)] = sv[u];
+            if (job_kind(ju) & kJobAdd) L->S[job_z(ju) * R.w + job_x(ju)] = 1;  // valid for the next relaxations
+          }
         }
+        post(&L->done, (int)(njobs + hk));
       }
       njobs += hk;
       k0 += hk;
@@ -418,7 +439,8 @@ AF_DEV void relax_role(InitLds* L, const DevModel& M, const MatView& mv, const M
       if (k0 >= nj) break;
       AF_DG_T0(tf)
       // job k0 in turn: one pass, this job on lane 0, guesses of the next pops' jobs on the others
-      const int lz = L->jz[k0], lx = L->jx[k0], kind = L->jkind[k0];
+      const int jk = job(k0);
+      const int lz = job_z(jk), lx = job_x(jk), kind = job_kind(jk);
       const int iz = lz + R.oz, ix = lx + R.ox;
       double v = 0.0;
       {
@@ -440,14 +462,12 @@ AF_DEV void relax_role(InitLds* L, const DevModel& M, const MatView& mv, const M
           const CellMat cm = init_mat<LDSMAT>(M, L, mv, mw, gz, gx, &pre);
           NbFieldT nb;
           nb.load_lds(L->T, L->S, R.z0, R.x0, R.z1, R.x1, R.w, gz, gx);
-          const UpdSel sel = update_nb_select(nb, gz, gx, cnnz, R.nnx);
-          const double val = update_nb_finish(M, cm, gz, gx, R.dnx, sel);
-          L->spec[lane].cell = (cz << 8) | cx;
-          L->spec[lane].val = val;
-          L->spec[lane].sel = sel;
-          if (lane == 0) v = val;
+          my_sel = update_nb_select(nb, gz, gx, cnnz, R.nnx);
+          my_val = update_nb_finish(M, cm, gz, gx, R.dnx, my_sel);
+          my_cell = (cz << 8) | cx;
+          if (lane == 0) v = my_val;
         } else {
-          L->spec[lane].cell = -1;
+          my_cell = -1;
         }
         nburst++;
       }
@@ -493,9 +513,7 @@ AF_DEV void stage_loop(Heap& h, const DevModel& M, const StageCfg& c, int tid) {
         if (0 <= i && i <= nx - 1) {
           const int st = L->S[iz * nx + i];
           if (st == -1 || st > 0) {
-            L->jz[n] = iz;
-            L->jx[n] = i;
-            L->jkind[n] = st == -1 ? kJobAdd : (kJobUpd | (c.quirk ? kJobQuirk : 0));
+            L->job[n] = job_pack(iz, i, st == -1 ? kJobAdd : (kJobUpd | (c.quirk ? kJobQuirk : 0)));
             n++;
           }
         } else if (abs(c.isx - i) == c.max_dist + 1) {
@@ -507,9 +525,7 @@ AF_DEV void stage_loop(Heap& h, const DevModel& M, const StageCfg& c, int tid) {
         if (0 <= i && i <= nz - 1) {
           const int st = L->S[i * nx + ix];
           if (st == -1 || st > 0) {
-            L->jz[n] = i;
-            L->jx[n] = ix;
-            L->jkind[n] = st == -1 ? kJobAdd : kJobUpd;
+            L->job[n] = job_pack(i, ix, st == -1 ? kJobAdd : kJobUpd);
             n++;
           }
         } else if (abs(c.isz - i) == c.max_dist + 1) {
@@ -581,9 +597,7 @@ AF_DEV void main_prefix(Heap& h, const DevModel& M, const InitJob& J, int wz0, i
         if (0 <= i && i <= nnx - 1) {
           const int st = L->S[lz * ww + (i - wx0)];
           if (st == -1 || st > 0) {
-            L->jz[n] = lz;
-            L->jx[n] = i - wx0;
-            L->jkind[n] = st == -1 ? kJobAdd : kJobUpd;
+            L->job[n] = job_pack(lz, i - wx0, st == -1 ? kJobAdd : kJobUpd);
             n++;
           }
         }
@@ -593,9 +607,7 @@ AF_DEV void main_prefix(Heap& h, const DevModel& M, const InitJob& J, int wz0, i
         if (0 <= i && i <= nnz - 1) {
           const int st = L->S[(i - wz0) * ww + lx];
           if (st == -1 || st > 0) {
-            L->jz[n] = i - wz0;
-            L->jx[n] = lx;
-            L->jkind[n] = st == -1 ? kJobAdd : kJobUpd;
+            L->job[n] = job_pack(i - wz0, lx, st == -1 ? kJobAdd : kJobUpd);
             n++;
           }
         }

@@ -34,8 +34,13 @@ struct Key {
 };
 AF_DEV bool key_less(const Key& a, const Key& b) { return a.v < b.v || (a.v == b.v && a.order < b.order); }
 
+// wavefronts per SIMD the kernel is compiled for (232 VGPRs at 2; 3 or 4 force fewer registers)
+#ifndef AF_RAY_WPE
+#define AF_RAY_WPE 2
+#endif
 template <int G, bool LDSMAT>
-__global__ __launch_bounds__(64 * kRayWaves) void find_ray_kernel(RayParams P) {
+__global__ __launch_bounds__(64 * kRayWaves) __attribute__((amdgpu_waves_per_eu(AF_RAY_WPE))) void find_ray_kernel(
+    RayParams P) {
   constexpr int kGroups = 64 / G;             // rays per wavefront
   constexpr int kTT = kMaxCand / kGroups;      // candidate slots per ray
   __shared__ double TTs[kRayWaves][kMaxCand];
@@ -267,6 +272,8 @@ extern "C" hipError_t af_launch_pack_rays(const double* rx, const double* ry, co
   hipLaunchKernelGGL(af::pack_rays_kernel, dim3(nrays), dim3(256), 0, stream, rx, ry, len, off, max_pts, packed);
   return hipGetLastError();
 }
+
+extern "C" int af_ray_waves_per_simd() { return AF_RAY_WPE; }
 
 extern "C" hipError_t af_launch_rays(const af::RayParams* P, hipStream_t stream) {
   const int ncand = 6 * P->sg + 3;  // axis planes; diagonal planes have <= 5*sg+3
