@@ -258,6 +258,30 @@ def gen_c4():
     save("c4_weldlike", **res)
 
 
+C4_WIN = 48  # half-width (nodes) of the full-resolution windows kept around the C4 source and receiver
+
+
+def gen_c4_window():
+    """The reference's C4 fields at full resolution in a (2 C4_WIN + 1)^2 window around source 64
+    and around the F7 receiver (2056, 4095): pins the exact heap-ordered prefix cell by cell (the
+    decimated c4_weldlike fields hold only a dozen cells inside it)."""
+    veln, velpn, vm, sd = W.weldlike_model()
+    vt = W.default_table()
+    dnx = W.weldlike_dnx()
+    scx, scz = W.c4_sources(128)
+    res = {"half": np.array(C4_WIN)}
+    for name, (x, z) in (("src", (int(round(scx[64] / dnx)), int(round(scz[64] / dnx)))), ("rec", (2056, 4095))):
+        t0 = time.time()
+        T = tr(dnx * x, dnx * z, veln, velpn, vm, sd, vt, vt, dnx)
+        z0, z1 = max(0, z - C4_WIN), min(T.shape[0], z + C4_WIN + 1)
+        x0, x1 = max(0, x - C4_WIN), min(T.shape[1], x + C4_WIN + 1)
+        res[name + "_xz"] = np.array([x, z])
+        res[name + "_box"] = np.array([z0, z1, x0, x1])
+        res[name + "_win"] = T[z0:z1, x0:x1].copy()
+        print("C4 %s window %.1fs" % (name, time.time() - t0), flush=True)
+    save("c4_window", **res)
+
+
 CORRIDOR_R = 6  # Chebyshev radius (fine nodes) kept around each rounded ray point at subgrid 1
 
 
@@ -409,7 +433,7 @@ def gen_group_vel():
 
 
 GENS = {"fmm_small": gen_fmm_small, "c1": gen_c1, "kat": gen_kat, "weld1": lambda: gen_weld(1),
-        "weld9": lambda: gen_weld(9), "c3": gen_c3, "c4": gen_c4, "c4_corridor": gen_c4_corridor, "local_ops": gen_local_ops, "tbp": gen_tbp,
+        "weld9": lambda: gen_weld(9), "c3": gen_c3, "c4": gen_c4, "c4_corridor": gen_c4_corridor, "c4_window": gen_c4_window, "local_ops": gen_local_ops, "tbp": gen_tbp,
         "group_vel": gen_group_vel}
 
 if __name__ == "__main__":

@@ -276,6 +276,16 @@ def test_c4_4096_fields_rays_and_batch_consistency(golden, ctx, envelope):
     TR = ctx.travel([dnx * 2056], [dnx * 4095])[0]
     _check_field(envelope, "c4_rec_dec8", TR[::8, ::8], g["rec_field_dec8"], (2056 / 8, 4095 / 8), excl=1)
     _exact_pin(envelope, "exact_c4_rec", TR[::8, ::8], g["rec_field_dec8"], tstop, 3)
+    # the same fields at full resolution around the source and the receiver (c4_window: the
+    # reference's own values in a 97 x 97 window): every cell of the exact heap-ordered prefix
+    # cell by cell, the rest of the window within the field tolerance
+    w = golden("c4_window")
+    for name, F in (("src", T), ("rec", TR)):
+        z0, z1, x0, x1 = (int(v) for v in w[name + "_box"])
+        x, z = (int(v) for v in w[name + "_xz"])
+        Fw, Rw = F[z0:z1, x0:x1], w[name + "_win"]
+        _exact_pin(envelope, "exact_c4_%s_window" % name, Fw, Rw, tstop, 300)
+        _check_field(envelope, "c4_%s_window" % name, Fw, Rw, (x - x0, z - z0))
     # batch independence: sources 0..3 together == each alone (sources never share state)
     B = ctx.travel(sx[:4], sz[:4])
     for i in (0, 3):

@@ -131,6 +131,11 @@ def test_c4_weldlike_fields_and_rays(golden):
     assert np.array_equal(T[::8, ::8], g["field_dec8"]) and np.array_equal(T[0], g["row_top"])
     TR = O.travel(dnx * 2056, dnx * 4095, veln, velpn, vm, sd, vt, vt, dnx=dnx)
     assert np.array_equal(TR[::8, ::8], g["rec_field_dec8"])
+    # the full-resolution windows around the source and the receiver (the GPU exact-prefix pin)
+    w = golden("c4_window")
+    for name, F in (("src", T), ("rec", TR)):
+        z0, z1, x0, x1 = (int(v) for v in w[name + "_box"])
+        assert np.array_equal(F[z0:z1, x0:x1], w[name + "_win"]), name
     for x in (8, 1032, 2056, 3080, 4088):
         rx, ry, t = O.find_ray(dnx, vt, [x, 0.0], [2056.0, 4095.0], TR, veln, velpn, vm, sd, 1)
         assert np.array_equal(rx, g["ray_x_%d" % x]) and np.array_equal(ry, g["ray_y_%d" % x])
