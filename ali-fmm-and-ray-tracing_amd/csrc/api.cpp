@@ -473,6 +473,10 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
   const long ecells = K > 1 ? nstripes * 4L * fz : 0;  // per edge buffer (4 columns per stripe)
   // the band kernel's working field (af_band_tb_cells: its layout) and its edge buffers
   const long tb_cells = af_band_tb_cells(fz, fx), tbc = tb_cells + 2 * ecells, sbc = af_band_sb_cells(fz, fx);
+  // the band kernel indexes the working field and both edge buffers with 32-bit cell indices
+  if (tbc >= (1L << 31) - 1)
+    return fail(ctx, ALIFMM_E_ARG, "travel: %d x %d grid with %ld edge cells exceeds the band kernel's 32-bit indexing",
+                fz, fx, 2 * ecells);
   // the arena is sized for this chunk (reused while later chunks fit in it)
   int rc = ensure_arena(ctx, n, cells, capL, capC, capS, K, capR, ecells, tbc, sbc);
   if (rc) return rc;
