@@ -263,6 +263,10 @@ AF_DEV int job_z(int j) { return (j >> 8) & 255; }
 AF_DEV int job_x(int j) { return j & 255; }
 AF_DEV int job_kind(int j) { return j >> 16; }
 AF_DEV int job_pack(int z, int x, int kind) { return (z << 8) | x | (kind << 16); }
+// the relax wavefront verifies the predicted next pop's jobs while the heap wavefront sifts (1)
+#ifndef AF_INIT_PREDICT
+#define AF_INIT_PREDICT 1
+#endif
 AF_DEV void post(int* w, int v) { __hip_atomic_store(w, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP); }
 // the waiting role backs off between polls (s_sleep) so that it does not take issue slots and
 // LDS cycles from the working one
@@ -362,6 +366,57 @@ AF_DEV void relax_role(InitLds* L, const DevModel& M, const MatView& mv, const M
   int my_cell = -1;
   double my_val = 0.0;
   UpdSel my_sel{};
+  // Verification of jobs k0.. of the job list jw (n jobs): the entries of the jobs (one ballot
+  // each: the lowest lane holding the job's node) and their values (src / sv); then the lane
+  // holding job k's entry re-runs its stencil stage on the current state with jobs k0..k-1 set to
+  // their entries' values.  Returns the number of leading confirmed jobs.
+  auto verify = [&](const int4& jw, int n, int k0, int (&src)[4], double (&sv)[4]) -> int {
+    auto job = [&](int i) { return i == 0 ? jw.x : i == 1 ? jw.y : i == 2 ? jw.z : jw.w; };
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      src[k] = -1;
+      sv[k] = -1.0;
+      if (k0 + k < n) {
+        const unsigned long long hm = __ballot(my_cell == (job(k0 + k) & 0xffff));
+        if (hm) {
+          src[k] = __ffsll((long long)hm) - 1;
+          sv[k] = readlane_d(my_val, src[k]);
+        }
+      }
+    }
+    bool ok = false;
+    {
+      int q = -1;  // the job whose entry this lane holds
+#pragma unroll
+      for (int k = 0; k < 4; k++) q = src[k] == lane ? k : q;
+      bool prior = true;  // every job k0..k0+q-1 has an entry with a usable value
+#pragma unroll
+      for (int u = 0; u < 4; u++) prior = prior && (u >= q || (src[u] >= 0 && sv[u] != -1.0));
+      if (q >= 0 && prior && my_val != -1.0) {
+        const int jq = job(k0 + q);
+        const int lz = job_z(jq), lx = job_x(jq);
+        const int iz = lz + R.oz, ix = lx + R.ox;
+        NbFieldT nb;
+        nb.load_lds(L->T, L->S, R.z0, R.x0, R.z1, R.x1, R.w, iz, ix);
+#pragma unroll
+        for (int u = 0; u < 3; u++)
+          if (u < q) nb.patch(job_z(job(k0 + u)) - lz, job_x(job(k0 + u)) - lx, sv[u]);
+        ok = update_nb_select(nb, iz, ix, (job_kind(jq) & kJobQuirk) ? R.quirk_nnz : R.nnz, R.nnx).same(my_sel);
+      }
+    }
+    const unsigned long long okm = __ballot(ok);
+    int hk = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      if (hk == k && k0 + k < n && src[k] >= 0 && ((okm >> src[k]) & 1ull)) hk = k + 1;
+    return hk;
+  };
+  // the next pop's job list as predicted after the last pop (wave-uniform; pred_n -1: none), and
+  // its verification done ahead, while the heap wavefront sifts and classifies
+  int pred_n = -1, pred_hk = 0;
+  int4 pred_jv = make_int4(0, 0, 0, 0);
+  int pred_src[4] = {-1, -1, -1, -1};
+  double pred_sv[4] = {-1.0, -1.0, -1.0, -1.0};
   while (true) {
     int cmd = 0;
     AF_DG_T0(tcw)
@@ -376,49 +431,30 @@ AF_DEV void relax_role(InitLds* L, const DevModel& M, const MatView& mv, const M
     const int nj = L->njob;
     const int4 jv = *reinterpret_cast<const int4*>(L->job);
     auto job = [&](int i) { return i == 0 ? jv.x : i == 1 ? jv.y : i == 2 ? jv.z : jv.w; };
+    // the prediction holds when the job lists are equal: the verification read the same state
+    // (only relaxations write T; sift-ups and pops change no node's validity)
+    const bool hit = pred_n == nj && nj > 0 && pred_jv.x == jv.x && (nj < 2 || pred_jv.y == jv.y) &&
+                     (nj < 3 || pred_jv.z == jv.z) && (nj < 4 || pred_jv.w == jv.w);
+    double jval[4] = {0.0, 0.0, 0.0, 0.0};  // the values this pop's jobs receive (next prediction)
     int k0 = 0;
     while (k0 < nj) {
       AF_DG_T0(tv)
-      // the entries of jobs k0.. (one ballot each: the lowest lane holding the job's node) and
-      // their values; then the lane holding job k's entry re-runs its stencil stage on the current
-      // state with jobs k0..k-1 set to their entries' values
-      int src[4] = {-1, -1, -1, -1};
-      double sv[4] = {-1.0, -1.0, -1.0, -1.0};
+      int src[4];
+      double sv[4];
+      int hk;
+      if (hit && k0 == 0) {
 #pragma unroll
-      for (int k = 0; k < 4; k++) {
-        if (k0 + k < nj) {
-          const unsigned long long hm = __ballot(my_cell == (job(k0 + k) & 0xffff));
-          if (hm) {
-            src[k] = __ffsll((long long)hm) - 1;
-            sv[k] = readlane_d(my_val, src[k]);
-          }
+        for (int k = 0; k < 4; k++) {
+          src[k] = pred_src[k];
+          sv[k] = pred_sv[k];
         }
+        hk = pred_hk;
+#if AF_INIT_DIAG
+        if (lane == 0) L->dg[7]++;
+#endif
+      } else {
+        hk = verify(jv, nj, k0, src, sv);
       }
-      bool ok = false;
-      {
-        int q = -1;  // the job whose entry this lane holds
-#pragma unroll
-        for (int k = 0; k < 4; k++) q = src[k] == lane ? k : q;
-        bool prior = true;  // every job k0..k0+q-1 has an entry with a usable value
-#pragma unroll
-        for (int u = 0; u < 4; u++) prior = prior && (u >= q || (src[u] >= 0 && sv[u] != -1.0));
-        if (q >= 0 && prior && my_val != -1.0) {
-          const int jq = job(k0 + q);
-          const int lz = job_z(jq), lx = job_x(jq);
-          const int iz = lz + R.oz, ix = lx + R.ox;
-          NbFieldT nb;
-          nb.load_lds(L->T, L->S, R.z0, R.x0, R.z1, R.x1, R.w, iz, ix);
-#pragma unroll
-          for (int u = 0; u < 3; u++)
-            if (u < q) nb.patch(job_z(job(k0 + u)) - lz, job_x(job(k0 + u)) - lx, sv[u]);
-          ok = update_nb_select(nb, iz, ix, (job_kind(jq) & kJobQuirk) ? R.quirk_nnz : R.nnz, R.nnx).same(my_sel);
-        }
-      }
-      const unsigned long long okm = __ballot(ok);
-      int hk = 0;  // leading confirmed jobs
-#pragma unroll
-      for (int k = 0; k < 4; k++)
-        if (hk == k && k0 + k < nj && src[k] >= 0 && ((okm >> src[k]) & 1ull)) hk = k + 1;
       if (lane == 0 && hk > 0) {
 #pragma unroll
         for (int u = 0; u < 4; u++) {
@@ -430,12 +466,14 @@ AF_DEV void relax_role(InitLds* L, const DevModel& M, const MatView& mv, const M
         }
         post(&L->done, (int)(njobs + hk));
       }
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+          if (u < hk && i == k0 + u) jval[i] = sv[u];
       njobs += hk;
       k0 += hk;
       if (lane == 0) { AF_DG_ADD(L, 5, tv) }
-#if AF_INIT_DIAG
-      if (lane == 0) L->dg[7]++;
-#endif
       if (k0 >= nj) break;
       AF_DG_T0(tf)
       // job k0 in turn: one pass, this job on lane 0, guesses of the next pops' jobs on the others
@@ -484,9 +522,57 @@ AF_DEV void relax_role(InitLds* L, const DevModel& M, const MatView& mv, const M
         post(&L->done, (int)(njobs + 1));
         AF_DG_ADD(L, 6, tf)
       }
+      {
+        const double vj = readlane_d(v, 0);
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+          if (i == k0) jval[i] = vj;
+      }
       njobs++;
       k0++;
     }
+    // Predict the next pop — the heap's root after downtree (read while the heap wavefront may still
+    // be sifting: a guess) or, when smaller, this pop's smallest new value — classify its
+    // neighbours as the heap wavefront will (x-1, x+1, z-1, z+1; far -> add, close -> update, the
+    // stage-1 quirk on x-neighbour updates), and verify those jobs now.  Only an identical job list
+    // at the next command uses the result.
+    pred_n = -1;
+#if AF_INIT_PREDICT
+    if (nj > 0) {
+      int pc = __builtin_amdgcn_readfirstlane((int)L->hcell[1]);
+      double pk = readlane_d(L->hkey[1], 0);
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        if (k < nj && jval[k] < pk) {
+          pk = jval[k];
+          pc = job(k) & 0xffff;
+        }
+      const int pz = pc >> 8, px = pc & 255;
+      int o[4] = {0, 0, 0, 0}, pn = 0;
+#pragma unroll
+      for (int d = 0; d < 4; d++) {
+        const int zz = pz + (d == 2 ? -1 : d == 3 ? 1 : 0), xx = px + (d == 0 ? -1 : d == 1 ? 1 : 0);
+        const int gz = zz + R.oz, gx = xx + R.ox;
+        const bool inb = d < 2 ? (gx >= 0 && gx <= R.nnx - 1) : (gz >= 0 && gz <= R.nnz - 1);
+        if (inb && zz >= 0 && zz <= wz && xx >= 0 && xx <= wx) {
+          const int st = __builtin_amdgcn_readfirstlane((int)L->S[zz * R.w + xx]);
+          if (st == -1 || st > 0) {
+            const int kind = st == -1 ? kJobAdd : (kJobUpd | (d < 2 && R.has_quirk ? kJobQuirk : 0));
+            const int jp = job_pack(zz, xx, kind);
+#pragma unroll
+            for (int s2 = 0; s2 < 4; s2++)
+              if (s2 == pn) o[s2] = jp;
+            pn++;
+          }
+        }
+      }
+      if (pn > 0) {
+        pred_jv = make_int4(o[0], o[1], o[2], o[3]);
+        pred_hk = verify(pred_jv, pn, 0, pred_src, pred_sv);
+        pred_n = pn;
+      }
+    }
+#endif
     busy += wall_clock64() - t0;
   }
   if (lane == 0) {

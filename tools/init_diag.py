@@ -26,7 +26,7 @@ m = P.mean(axis=0)
 pops = float(m[4:8].sum())
 walk_ticks = float(m[0:4].sum())
 names = ["heap_wait_relax", "heap_down", "heap_addupd", "heap_classify", "relax_wait_pop", "relax_verify",
-         "relax_eval", "verify_passes"]
+         "relax_eval", "pred_hits"]
 out = {"sources": ns, "init_ms": ti, "pops": pops, "walk_us_per_pop": walk_ticks / 100 / pops,
        "cycles_per_pop": {n: round(m[8 + k] / pops, 1) for k, n in enumerate(names)}}
 print(json.dumps(out))
