@@ -2,7 +2,8 @@
 //
 // Owns the HBM-resident model, the per-source work arena (status grid + band work lists) and
 // the resident travel-time fields that the ray tracer reads without a host round trip.
-// Sources are processed in chunks of `batch` (one persistent workgroup per source).
+// Sources are processed in launches of at most `batch` (and at most half the CUs: >= 2 band
+// workgroups per source), all workgroups of a launch co-resident.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -656,9 +657,14 @@ int alifmm_travel(alifmm_ctx* ctx, int subgrid, int nsrc, const double* scx, con
   hipEvent_t t_begin;
   HIPCHK(hipEventCreate(&t_begin));
   HIPCHK(hipEventRecord(t_begin, ctx->stream));
-  // chunk: two workgroups per source need 2n CUs (pair mode), one per source otherwise
-  // at least one band workgroup per source (sources padded to 8), all co-resident
-  const int chunk = std::max(1, std::min(ctx->batch, ctx->n_cu / 8 * 8));
+  // Sources per launch: at most half the CUs, so that every source gets >= 2 band members (256
+  // C5 receivers on 256 CUs: one launch with one member each 927 ms, two launches of 128 with two
+  // members each 810 ms, profiles/r3w_batch.json), balanced over the launches (multiples of 8)
+  int chunk = std::max(1, std::min(ctx->batch, std::max(8, ctx->n_cu / 2 / 8 * 8)));
+  if (nsrc > chunk) {
+    const int nl = (nsrc + chunk - 1) / chunk;
+    chunk = std::min(chunk, ((nsrc + nl - 1) / nl + 7) / 8 * 8);
+  }
   for (int s0 = 0; s0 < nsrc; s0 += chunk) {
     int n = std::min(chunk, nsrc - s0);
     int rc;
