@@ -139,6 +139,11 @@ int alifmm_ctx_destroy(alifmm_ctx* ctx) {
   (void)hipStreamSynchronize(ctx->stream);
   alifmm_release_fields(ctx);
   free_arena(ctx->arena);
+  dfree(ctx->ho_all);
+  dfree(ctx->jobs_all);
+  ctx->ho_all = nullptr;
+  ctx->jobs_all = nullptr;
+  ctx->ho_last = nullptr;
   free_ray_bufs(ctx);
   for (int b = 0; b < alifmm_ctx::kPinBufs; b++) {
     if (ctx->pin[b]) (void)hipHostFree(ctx->pin[b]);
@@ -386,6 +391,10 @@ static int ensure_arena(alifmm_ctx* ctx, int nsrc, long cells, long capL, long c
   if (a.nsrc >= nsrc && a.cells >= cells && a.capL >= capL && a.capC >= capC && a.capS >= capS && a.K >= K &&
       a.capR >= capR && a.ecells >= ecells && a.tbc >= tbc && a.sbc >= sbc)
     return ALIFMM_OK;
+  if (ctx->ho_last == a.ho) {  // init profile of a chunk whose arena goes away
+    ctx->ho_last = nullptr;
+    ctx->n_ho_last = 0;
+  }
   free_arena(a);
   a.nsrc = nsrc;
   a.cells = cells;
@@ -452,9 +461,29 @@ static int choose_members(const alifmm_ctx* ctx, int n, int fx) {
   return K;
 }
 
+// subgrid-1 source init (fmm_init_kernel) of n sources into ho (jobs: device scratch of n InitJobs)
+static int launch_source_init(alifmm_ctx* ctx, int n, const double* scx, const double* scz, af::InitJob* djobs,
+                              af::HandoverOut* ho) {
+  std::vector<af::InitJob> jobs(n);
+  for (int i = 0; i < n; i++) {
+    jobs[i].isx = (long)std::nearbyint((scx[i] - ctx->gox) / ctx->dnx);
+    jobs[i].isz = (long)std::nearbyint((scz[i] - ctx->goz) / ctx->dnz);
+    jobs[i].dnx = ctx->dnx;
+    jobs[i].dnz = ctx->dnz;
+    jobs[i].exact_r = ctx->exact_r;
+    jobs[i].tstop = ctx->exact_r * ctx->dnx / ctx->vmax;
+    if (jobs[i].isx < 0 || jobs[i].isx >= ctx->nx0 || jobs[i].isz < 0 || jobs[i].isz >= ctx->nz0)
+      return fail(ctx, ALIFMM_E_ARG, "source %d (%g, %g) outside the grid", i, scx[i], scz[i]);
+  }
+  af::DevModel M = dev_model(ctx);
+  HIPCHK(hipMemcpyAsync(djobs, jobs.data(), sizeof(af::InitJob) * n, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(af_launch_init(&M, djobs, n, ho, ctx->stream));
+  return ALIFMM_OK;
+}
+
 // one chunk of sources; returns ALIFMM_E_CAPACITY when a work list overflowed
 static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const double* scz, int first_slot, int fz,
-                        int fx, float* ms_init, float* ms_band) {
+                        int fx, float* ms_init, float* ms_band, const af::HandoverOut* pre_ho = nullptr) {
   const long cells = (long)fz * fx;
   long capL = std::min(cells, std::max(65536L, cells / 8) * ctx->cap_scale);
   long capC = capL;
@@ -571,21 +600,15 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
   P.max_steps = 200L * (fz + fx) + 100000;
   HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
   if (sg == 1) {
-    std::vector<af::InitJob> jobs(n);
-    for (int i = 0; i < n; i++) {
-      jobs[i].isx = (long)std::nearbyint((scx[i] - ctx->gox) / ctx->dnx);
-      jobs[i].isz = (long)std::nearbyint((scz[i] - ctx->goz) / ctx->dnz);
-      jobs[i].dnx = ctx->dnx;
-      jobs[i].dnz = ctx->dnz;
-      jobs[i].exact_r = ctx->exact_r;
-      jobs[i].tstop = ctx->exact_r * ctx->dnx / ctx->vmax;
-      if (jobs[i].isx < 0 || jobs[i].isx >= ctx->nx0 || jobs[i].isz < 0 || jobs[i].isz >= ctx->nz0)
-        return fail(ctx, ALIFMM_E_ARG, "source %d (%g, %g) outside the grid", i, scx[i], scz[i]);
+    if (pre_ho) {  // initialised by the travel call for all its chunks (alifmm_travel)
+      P.ho = const_cast<af::HandoverOut*>(pre_ho);
+    } else {
+      if ((rc = launch_source_init(ctx, n, scx, scz, a.jobs, a.ho))) return rc;
+      P.ho = a.ho;
+      ctx->ho_last = a.ho;
+      ctx->n_ho_last = n;
     }
-    HIPCHK(hipMemcpyAsync(a.jobs, jobs.data(), sizeof(af::InitJob) * n, hipMemcpyHostToDevice, ctx->stream));
-    HIPCHK(af_launch_init(&M, a.jobs, n, a.ho, ctx->stream));
     P.mode = 0;
-    P.ho = a.ho;
   } else {
     for (int i = 0; i < n; i++) {
       long ix = (long)std::nearbyint((scx[i] - ctx->gox) / ctx->dnx), iz = (long)std::nearbyint((scz[i] - ctx->goz) / ctx->dnz);
@@ -665,11 +688,39 @@ int alifmm_travel(alifmm_ctx* ctx, int subgrid, int nsrc, const double* scx, con
     const int nl = (nsrc + chunk - 1) / chunk;
     chunk = std::min(chunk, ((nsrc + nl - 1) / nl + 7) / 8 * 8);
   }
+  // subgrid 1 over several launches: one source-init launch for every source of the call (the
+  // init uses one CU per source; chunk by chunk it would run alone before each band launch)
+  const af::HandoverOut* pre = nullptr;
+  if (subgrid == 1 && nsrc > chunk) {
+    if (ctx->n_all < nsrc) {
+      dfree(ctx->ho_all);
+      dfree(ctx->jobs_all);
+      ctx->n_all = 0;
+      HIPCHK(dalloc(&ctx->ho_all, nsrc));
+      HIPCHK(dalloc(&ctx->jobs_all, nsrc));
+      ctx->n_all = nsrc;
+    }
+    HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
+    int rc = launch_source_init(ctx, nsrc, scx, scz, ctx->jobs_all, ctx->ho_all);
+    if (rc) {
+      (void)hipEventDestroy(t_begin);
+      return rc;
+    }
+    HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
+    HIPCHK(hipEventSynchronize(ctx->ev[1]));
+    float t = 0;
+    (void)hipEventElapsedTime(&t, ctx->ev[0], ctx->ev[1]);
+    ms_init += t;
+    pre = ctx->ho_all;
+    ctx->ho_last = ctx->ho_all;
+    ctx->n_ho_last = nsrc;
+  }
   for (int s0 = 0; s0 < nsrc; s0 += chunk) {
     int n = std::min(chunk, nsrc - s0);
     int rc;
     for (;;) {
-      rc = travel_chunk(ctx, subgrid, n, scx + s0, scz + s0, first_slot + s0, fz, fx, &ms_init, &ms_band);
+      rc = travel_chunk(ctx, subgrid, n, scx + s0, scz + s0, first_slot + s0, fz, fx, &ms_init, &ms_band,
+                        pre ? pre + s0 : nullptr);
       if (rc != ALIFMM_E_CAPACITY || ctx->cap_scale * 4 > 64) break;
       ctx->cap_scale *= 4;  // retry the chunk with larger work lists
     }
@@ -817,10 +868,10 @@ int alifmm_band_span(alifmm_ctx* ctx, int slot, int64_t* out2) {
 }
 
 int alifmm_init_profile(alifmm_ctx* ctx, int i, int64_t* out16) {
-  if (!ctx || !out16 || i < 0 || i >= ctx->arena.nsrc || !ctx->arena.ho)
+  if (!ctx || !out16 || i < 0 || i >= ctx->n_ho_last || !ctx->ho_last)
     return fail(ctx, ALIFMM_E_ARG, "init_profile: bad index");
   HIPCHK(hipSetDevice(ctx->device));
-  HIPCHK(hipMemcpy(out16, &ctx->arena.ho[i].prof[0], 16 * sizeof(long long), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(out16, &ctx->ho_last[i].prof[0], 16 * sizeof(long long), hipMemcpyDeviceToHost));
   return ALIFMM_OK;
 }
 

@@ -81,6 +81,12 @@ struct alifmm_ctx {
   double cdelta_far = 0.0, r_far = 0.0;  // band width beyond r_far nodes (0: off)
   int exact_r = 20;
   int batch = 256;
+  // subgrid-1 source init of a whole multi-launch travel call (one init launch for every chunk)
+  af::HandoverOut* ho_all = nullptr;
+  af::InitJob* jobs_all = nullptr;
+  int n_all = 0;
+  const af::HandoverOut* ho_last = nullptr;  // what alifmm_init_profile reads (last travel call)
+  int n_ho_last = 0;
   int prof = 0;
   int coop = 0;  // band kernel: cooperative launch (1) or plain launch after a residency check (0)
   int members = 0;     // band kernel: workgroups per source (0: as many as the device fits, <= 16)
