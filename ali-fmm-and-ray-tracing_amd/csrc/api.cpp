@@ -910,10 +910,7 @@ int alifmm_find_rays(alifmm_ctx* ctx, int npairs, const int32_t* field_slot, con
   int chunk = 8192;
   {
     int rays_per_wave = 64;
-    for (auto& g : by_sg) {
-      const int nc = 6 * g.first + 3;
-      rays_per_wave = std::min(rays_per_wave, nc <= 16 ? 4 : nc <= 32 ? 2 : 1);
-    }
+    for (auto& g : by_sg) rays_per_wave = std::min(rays_per_wave, 64 / af_ray_group_lanes(g.first));
     const long target = (long)std::max(ctx->n_cu, 1) * 4 * af_ray_waves_per_simd() * rays_per_wave;
     size_t free_b = 0, total_b = 0;
     long by_mem = target;

@@ -150,6 +150,7 @@ long af_band_sb_cells(int nz, int nx);
 hipError_t af_launch_scale(double* T, long n, double sg, hipStream_t stream);
 hipError_t af_launch_rays(const af::RayParams* P, hipStream_t stream);
 int af_ray_waves_per_simd();
+int af_ray_group_lanes(int sg);
 hipError_t af_launch_pack_rays(const double* rx, const double* ry, const int* len, const long long* off, int nrays,
                                int max_pts, double* packed, hipStream_t stream);
 hipError_t af_launch_local_ops(const af::LocalOpsParams* P, hipStream_t stream);

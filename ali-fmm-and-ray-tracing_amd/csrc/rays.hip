@@ -275,16 +275,28 @@ extern "C" hipError_t af_launch_pack_rays(const double* rx, const double* ry, co
 
 extern "C" int af_ray_waves_per_simd() { return AF_RAY_WPE; }
 
+// lanes per ray (a power of two): candidates of one search plane across lanes; AF_RAY_GMIN 8 puts
+// 8 rays in a wavefront at subgrid 1 (9 axis-plane candidates then take two rounds)
+#ifndef AF_RAY_GMIN
+#define AF_RAY_GMIN 16
+#endif
+extern "C" int af_ray_group_lanes(int sg) {
+  const int ncand = 6 * sg + 3;  // axis planes; diagonal planes have <= 5*sg+3
+  return ncand <= AF_RAY_GMIN ? AF_RAY_GMIN : ncand <= 16 ? 16 : ncand <= 32 ? 32 : 64;
+}
+
 extern "C" hipError_t af_launch_rays(const af::RayParams* P, hipStream_t stream) {
-  const int ncand = 6 * P->sg + 3;  // axis planes; diagonal planes have <= 5*sg+3
-  const int G = ncand <= 16 ? 16 : ncand <= 32 ? 32 : 64;
+  const int G = af_ray_group_lanes(P->sg);
   const int per_block = af::kRayWaves * (64 / G);
   const dim3 grid((P->nrays + per_block - 1) / per_block), block(64 * af::kRayWaves);
   // material records, stiffness rows and the group table in LDS when they fit (the per-cell ids
   // index the records)
   const bool lds = P->M.mid && P->M.mtab && P->M.nmat <= af::kRayMatLds && P->M.nstab <= af::kRayStabLds &&
                    361 * P->M.ncol <= af::kRayGtabLds;
-  if (G == 16) {
+  if (G == 8) {
+    if (lds) hipLaunchKernelGGL((af::find_ray_kernel<8, true>), grid, block, 0, stream, *P);
+    else hipLaunchKernelGGL((af::find_ray_kernel<8, false>), grid, block, 0, stream, *P);
+  } else if (G == 16) {
     if (lds) hipLaunchKernelGGL((af::find_ray_kernel<16, true>), grid, block, 0, stream, *P);
     else hipLaunchKernelGGL((af::find_ray_kernel<16, false>), grid, block, 0, stream, *P);
   } else if (G == 32) {
