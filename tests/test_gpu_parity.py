@@ -572,3 +572,14 @@ def test_empty_and_degenerate_requests(A, ctx, envelope):
     # a source outside the grid is an argument error, not a fault
     with pytest.raises(_alifmm.AlifmmError):
         ctx.travel(np.array([1.0]), np.array([0.0]))
+    # maximum sizes: a field side of 32 768 nodes (subgrid 1, or a subgrid that refines past it)
+    # is refused up front (the kernels' packed 15-bit cell keys), not computed wrongly
+    tall = 32768
+    ctx.set_model(np.zeros((tall, 2)), np.ones((tall, 2), dtype=np.int64), np.full((tall, 2), 5790.0), None, vt, vt,
+                  1e-3)
+    with pytest.raises(_alifmm.AlifmmError, match="32768"):
+        ctx.travel(np.array([0.0]), np.array([0.0]))
+    ctx.set_model(np.zeros((3642, 2)), np.ones((3642, 2), dtype=np.int64), np.full((3642, 2), 5790.0), None, vt, vt,
+                  1e-3)
+    with pytest.raises(_alifmm.AlifmmError, match="32768"):
+        ctx.travel(np.array([0.0]), np.array([0.0]), subgrid=9)  # 9 * 3641 + 1 = 32 770 fine rows
