@@ -101,3 +101,20 @@ def test_rccl_gather_one_rank_paths():
         if comm is not None:
             comm.close()
         ctx.close()
+
+
+def test_option_environment_hook(monkeypatch):
+    """ALIFMM_OPT_<NAME>=value sets the option on every new context (README "Options"); an unknown
+    name or a non-numeric value is reported with a warning and ignored, never fatal."""
+    import _alifmm
+
+    monkeypatch.setenv("ALIFMM_OPT_R0", "30")
+    monkeypatch.setenv("ALIFMM_OPT_NO_SUCH_OPTION", "1")
+    monkeypatch.setenv("ALIFMM_OPT_CDELTA", "not-a-number")
+    with pytest.warns(UserWarning):
+        c = _alifmm.Context(0)
+    try:
+        assert c.get_option("r0") == 30.0
+        assert c.get_option("cdelta") == 0.5  # the bad value left the default
+    finally:
+        c.close()
