@@ -676,10 +676,6 @@ int alifmm_travel(alifmm_ctx* ctx, int subgrid, int nsrc, const double* scx, con
   alifmm_field_shape(ctx, subgrid, &fz, &fx);
   const long cells = (long)fz * fx;
   float ms_init = 0, ms_band = 0;
-  HIPCHK(hipEventRecord(ctx->ev[3], ctx->stream));
-  hipEvent_t t_begin;
-  HIPCHK(hipEventCreate(&t_begin));
-  HIPCHK(hipEventRecord(t_begin, ctx->stream));
   // Sources per launch: at most half the CUs, so that every source gets >= 2 band members (256
   // C5 receivers on 256 CUs: one launch with one member each 927 ms, two launches of 128 with two
   // members each 810 ms, profiles/r3w_batch.json), balanced over the launches (multiples of 8)
@@ -690,16 +686,27 @@ int alifmm_travel(alifmm_ctx* ctx, int subgrid, int nsrc, const double* scx, con
   }
   // subgrid 1 over several launches: one source-init launch for every source of the call (the
   // init uses one CU per source; chunk by chunk it would run alone before each band launch)
-  const af::HandoverOut* pre = nullptr;
-  if (subgrid == 1 && nsrc > chunk) {
-    if (ctx->n_all < nsrc) {
-      dfree(ctx->ho_all);
-      dfree(ctx->jobs_all);
-      ctx->n_all = 0;
-      HIPCHK(dalloc(&ctx->ho_all, nsrc));
-      HIPCHK(dalloc(&ctx->jobs_all, nsrc));
-      ctx->n_all = nsrc;
+  const bool pre_init = subgrid == 1 && nsrc > chunk;
+  if (pre_init && ctx->n_all < nsrc) {
+    if (ctx->ho_last == ctx->ho_all) {
+      ctx->ho_last = nullptr;
+      ctx->n_ho_last = 0;
     }
+    dfree(ctx->ho_all);
+    dfree(ctx->jobs_all);
+    ctx->ho_all = nullptr;
+    ctx->jobs_all = nullptr;
+    ctx->n_all = 0;
+    HIPCHK(dalloc(&ctx->ho_all, nsrc));
+    HIPCHK(dalloc(&ctx->jobs_all, nsrc));
+    ctx->n_all = nsrc;
+  }
+  HIPCHK(hipEventRecord(ctx->ev[3], ctx->stream));
+  hipEvent_t t_begin;
+  HIPCHK(hipEventCreate(&t_begin));
+  HIPCHK(hipEventRecord(t_begin, ctx->stream));
+  const af::HandoverOut* pre = nullptr;
+  if (pre_init) {
     HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
     int rc = launch_source_init(ctx, nsrc, scx, scz, ctx->jobs_all, ctx->ho_all);
     if (rc) {

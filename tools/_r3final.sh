@@ -1,3 +1,3 @@
 # final-build check: GPU tests, smoke, bench line, then the rocprofv3 passes (stats, FETCH, WRITE, SQ)
-bash tools/gpu_check.sh r3f tests smoke bench || exit $?
-bash tools/profile.sh r3f "stats fetch write sq" || exit $?
+bash tools/gpu_check.sh r3fin tests smoke bench || exit $?
+bash tools/profile.sh r3fin "stats fetch write sq" || exit $?
