@@ -102,17 +102,21 @@ def lib():
     return _load()
 
 
-def shutdown():
-    """Destroy every open context, then unload the library — at interpreter exit (atexit), while
-    the HIP runtime and anything attached to it (rocprofv3's tool) are still intact.
+def _profiler_attached():
+    """True under rocprofv3 (its tool library is configured through ROCPROF* / ROCP_* variables)."""
+    return any(k.startswith(("ROCPROF", "ROCP_")) for k in os.environ)
 
-    Why: the library's HIP module destructor (__hip_module_dtor -> __hipUnregisterFatBinary, which
-    hipcc registers with __cxa_atexit when the library is loaded) otherwise runs from exit() AFTER
-    handlers registered later — rocprofv3's finalisation is registered at the first HIP call, after
-    the library was loaded — and calls into a torn-down runtime (the SIGSEGV at exit of round 2's
-    profiled runs).  dlclose() runs the destructor now, and contexts destroyed here release their
-    streams, events, pinned buffers and device memory in order instead of leaving them to the
-    runtime's own static teardown."""
+
+def shutdown():
+    """Destroy every open context and communicator at interpreter exit (atexit), while the HIP
+    runtime is intact: their streams, events, pinned buffers and device memory are released in
+    order instead of by the runtime's own static teardown.
+
+    The library stays mapped (its path shows in the process maps to the end, as any loaded
+    extension's), except under a profiler: rocprofv3 registers its finalisation after the
+    library's HIP module destructor (__hip_module_dtor, registered with __cxa_atexit when the
+    library is loaded), so that destructor would run from exit() after the tool has torn down;
+    there the library is unloaded here, which runs the destructor now."""
     global _lib, _lib_closed
     live = list(_live)
     for c in [c for c in live if isinstance(c, Comm)] + [c for c in live if not isinstance(c, Comm)]:
@@ -121,6 +125,8 @@ def shutdown():
         except Exception:
             pass
     _default.clear()
+    if not _profiler_attached():
+        return
     with _lock:
         L, _lib, _lib_closed = _lib, None, True
     if L is not None:

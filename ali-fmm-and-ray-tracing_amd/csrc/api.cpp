@@ -23,6 +23,8 @@
 #include "context.h"
 #include "kernels.h"
 
+extern char** environ;
+
 static void free_ray_bufs(alifmm_ctx* c) {
   auto& b = c->rb;
   for (void* p : {(void*)b.rx, (void*)b.ry, (void*)b.t, (void*)b.len, (void*)b.flags, (void*)b.jobs, (void*)b.off})
@@ -105,6 +107,14 @@ int alifmm_ctx_create(int device, alifmm_ctx** out) {
   }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) ctx->n_cu = prop.multiProcessorCount;
+  // band kernel launch: cooperative (gang-scheduled: every member resident whatever else runs on
+  // the device) by default; under rocprofv3 a plain launch after a residency check, because the
+  // runtime's teardown of the cooperative queue at exit crashed after the profiler had finalised
+  // (the plain path assumes exclusive use of the device; a member that never sees its peers stops
+  // at the exchange's spin limit, error 7, and the chunk is re-run with a cooperative launch)
+  ctx->coop = 1;
+  for (char** e = environ; e && *e; e++)
+    if (!strncmp(*e, "ROCPROF", 7) || !strncmp(*e, "ROCP_", 5)) ctx->coop = 0;
   *out = ctx;
   return ALIFMM_OK;
 }
@@ -385,11 +395,13 @@ static af::DevModel dev_model(const alifmm_ctx* c) {
   return M;
 }
 
-static int ensure_arena(alifmm_ctx* ctx, int nsrc, long cells, long capL, long capC, long capS, int K, long capR,
-                        long ecells, long tbc, long sbc) {
+// scells: cells of the row-major status S (fmm_exact_kernel's region and the mode-1 hand-over:
+// subgrid > 1 only; 0 at subgrid 1, where the band kernel keeps its status in the bricked Sb)
+static int ensure_arena(alifmm_ctx* ctx, int nsrc, long cells, long scells, long capL, long capC, long capS, int K,
+                        long capR, long ecells, long tbc, long sbc) {
   Arena& a = ctx->arena;
-  if (a.nsrc >= nsrc && a.cells >= cells && a.capL >= capL && a.capC >= capC && a.capS >= capS && a.K >= K &&
-      a.capR >= capR && a.ecells >= ecells && a.tbc >= tbc && a.sbc >= sbc)
+  if (a.nsrc >= nsrc && a.cells >= cells && a.scells >= scells && a.capL >= capL && a.capC >= capC &&
+      a.capS >= capS && a.K >= K && a.capR >= capR && a.ecells >= ecells && a.tbc >= tbc && a.sbc >= sbc)
     return ALIFMM_OK;
   if (ctx->ho_last == a.ho) {  // init profile of a chunk whose arena goes away
     ctx->ho_last = nullptr;
@@ -398,6 +410,7 @@ static int ensure_arena(alifmm_ctx* ctx, int nsrc, long cells, long capL, long c
   free_arena(a);
   a.nsrc = nsrc;
   a.cells = cells;
+  a.scells = scells;
   a.capL = capL;
   a.capC = capC;
   a.capS = capS;
@@ -408,7 +421,7 @@ static int ensure_arena(alifmm_ctx* ctx, int nsrc, long cells, long capL, long c
   a.sbc = sbc;
   HIPCHK(dalloc(&a.Tb, (size_t)nsrc * tbc));
   HIPCHK(dalloc(&a.Sb, (size_t)nsrc * sbc));
-  HIPCHK(dalloc(&a.S, (size_t)nsrc * cells));
+  if (scells > 0) HIPCHK(dalloc(&a.S, (size_t)nsrc * scells));
   HIPCHK(dalloc(&a.own, (size_t)nsrc * cells));
   HIPCHK(dalloc(&a.lists, (size_t)nsrc * (4 * capL + 6 * capC)));
   HIPCHK(dalloc(&a.dlists, (size_t)nsrc * (capL + 2 * capC)));
@@ -481,6 +494,10 @@ static int launch_source_init(alifmm_ctx* ctx, int n, const double* scx, const d
   return ALIFMM_OK;
 }
 
+// travel_chunk: a plain band launch whose members were not all resident (another process held CUs);
+// alifmm_travel re-runs the chunk once with a cooperative launch
+static const int kRetryCoop = -100;
+
 // one chunk of sources; returns ALIFMM_E_CAPACITY when a work list overflowed
 static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const double* scz, int first_slot, int fz,
                         int fx, float* ms_init, float* ms_band, const af::HandoverOut* pre_ho = nullptr) {
@@ -508,7 +525,7 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
     return fail(ctx, ALIFMM_E_ARG, "travel: %d x %d grid with %ld edge cells exceeds the band kernel's 32-bit indexing",
                 fz, fx, 2 * ecells);
   // the arena is sized for this chunk (reused while later chunks fit in it)
-  int rc = ensure_arena(ctx, n, cells, capL, capC, capS, K, capR, ecells, tbc, sbc);
+  int rc = ensure_arena(ctx, n, cells, sg > 1 ? cells : 0, capL, capC, capS, K, capR, ecells, tbc, sbc);
   if (rc) return rc;
   Arena& a = ctx->arena;
   // subgrid 1: the fields are first written by the band kernel, so their initialisation runs on
@@ -526,7 +543,7 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
     af::BandSrc& b = hs[i];
     memset(&b, 0, sizeof b);
     b.T = ctx->fields[slot].d;
-    b.S = a.S + (size_t)i * a.cells;
+    b.S = sg > 1 ? a.S + (size_t)i * a.scells : nullptr;
     b.own = a.own + (size_t)i * a.cells;
     int* base = a.lists + (size_t)i * (4 * a.capL + 6 * a.capC);
     b.Lin = base;
@@ -658,6 +675,7 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
     if (hs[i].err == 2) cap_err = 1;
     else if (hs[i].err == 3) return fail(ctx, ALIFMM_E_KERNEL, "source %d: init heap overflow", i);
     else if (hs[i].err == 4) return fail(ctx, ALIFMM_E_KERNEL, "source %d: stage grid capacity", i);
+    else if (hs[i].err == 7 && !P.coop) return fail(ctx, kRetryCoop, "source %d: band members not co-resident", i);
     else if (hs[i].err) return fail(ctx, ALIFMM_E_KERNEL, "source %d: kernel error %d", i, hs[i].err);
   }
   if (cap_err) return fail(ctx, ALIFMM_E_CAPACITY, "work-list capacity %ld exceeded", capL);
@@ -702,17 +720,21 @@ int alifmm_travel(alifmm_ctx* ctx, int subgrid, int nsrc, const double* scx, con
     ctx->n_all = nsrc;
   }
   HIPCHK(hipEventRecord(ctx->ev[3], ctx->stream));
-  hipEvent_t t_begin;
-  HIPCHK(hipEventCreate(&t_begin));
-  HIPCHK(hipEventRecord(t_begin, ctx->stream));
+  // the call's timing events, destroyed on every return path
+  struct Ev {
+    hipEvent_t e = nullptr;
+    ~Ev() {
+      if (e) (void)hipEventDestroy(e);
+    }
+  } t_begin, t_end;
+  HIPCHK(hipEventCreate(&t_begin.e));
+  HIPCHK(hipEventCreate(&t_end.e));
+  HIPCHK(hipEventRecord(t_begin.e, ctx->stream));
   const af::HandoverOut* pre = nullptr;
   if (pre_init) {
     HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
     int rc = launch_source_init(ctx, nsrc, scx, scz, ctx->jobs_all, ctx->ho_all);
-    if (rc) {
-      (void)hipEventDestroy(t_begin);
-      return rc;
-    }
+    if (rc) return rc;
     HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
     HIPCHK(hipEventSynchronize(ctx->ev[1]));
     float t = 0;
@@ -728,29 +750,27 @@ int alifmm_travel(alifmm_ctx* ctx, int subgrid, int nsrc, const double* scx, con
     for (;;) {
       rc = travel_chunk(ctx, subgrid, n, scx + s0, scz + s0, first_slot + s0, fz, fx, &ms_init, &ms_band,
                         pre ? pre + s0 : nullptr);
+      if (rc == kRetryCoop) {  // once, gang-scheduled
+        const int c0 = ctx->coop;
+        ctx->coop = 1;
+        rc = travel_chunk(ctx, subgrid, n, scx + s0, scz + s0, first_slot + s0, fz, fx, &ms_init, &ms_band,
+                          pre ? pre + s0 : nullptr);
+        ctx->coop = c0;
+        if (rc == kRetryCoop) rc = ALIFMM_E_KERNEL;
+      }
       if (rc != ALIFMM_E_CAPACITY || ctx->cap_scale * 4 > 64) break;
       ctx->cap_scale *= 4;  // retry the chunk with larger work lists
     }
-    if (rc) {
-      (void)hipEventDestroy(t_begin);
-      return rc;
-    }
+    if (rc) return rc;
     if (out) {  // pageable host destination: through the pinned staging ring
       rc = alifmm_copy_fields(ctx, first_slot + s0, n, out + (size_t)s0 * cells, 0, nullptr);
-      if (rc) {
-        (void)hipEventDestroy(t_begin);
-        return rc;
-      }
+      if (rc) return rc;
     }
   }
-  hipEvent_t t_end;
-  HIPCHK(hipEventCreate(&t_end));
-  HIPCHK(hipEventRecord(t_end, ctx->stream));
+  HIPCHK(hipEventRecord(t_end.e, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
   float tot = 0;
-  (void)hipEventElapsedTime(&tot, t_begin, t_end);
-  (void)hipEventDestroy(t_begin);
-  (void)hipEventDestroy(t_end);
+  (void)hipEventElapsedTime(&tot, t_begin.e, t_end.e);
   ctx->t_init = ms_init;
   ctx->t_band = ms_band;
   ctx->t_total = tot;
@@ -915,14 +935,17 @@ int alifmm_find_rays(alifmm_ctx* ctx, int npairs, const int32_t* field_slot, con
   // 8 192 rays at 16 lanes per ray and 2 wavefronts per SIMD), balanced over the launches, with the
   // point buffers within a quarter of the free device memory.
   int chunk = 8192;
+  size_t keep_budget = SIZE_MAX;  // device bytes the kept points of this call may hold (a quarter of the free memory)
   {
     int rays_per_wave = 64;
     for (auto& g : by_sg) rays_per_wave = std::min(rays_per_wave, 64 / af_ray_group_lanes(g.first));
     const long target = (long)std::max(ctx->n_cu, 1) * 4 * af_ray_waves_per_simd() * rays_per_wave;
     size_t free_b = 0, total_b = 0;
     long by_mem = target;
-    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess)
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
       by_mem = (long)(free_b / 4 / ((size_t)max_pts * 2 * sizeof(double) + 64));
+      keep_budget = free_b / 4;
+    }
     const long cmax = std::max(1024L, std::min(target, by_mem));
     const long nlaunch = (npairs + cmax - 1) / cmax;
     chunk = (int)((npairs + nlaunch - 1) / nlaunch);
@@ -947,11 +970,13 @@ int alifmm_find_rays(alifmm_ctx* ctx, int npairs, const int32_t* field_slot, con
   long long* d_off = rb.off;
   int rc = ALIFMM_OK;
   auto cleanup = [&]() { dfree(d_packed); };
+  // an error return also drops the points kept so far (kept_pts then matches no ray list)
 #define RCHK(call)                                                                        \
   do {                                                                                    \
     hipError_t e_ = (call);                                                               \
     if (e_ != hipSuccess) {                                                               \
       cleanup();                                                                          \
+      release_kept_rays(ctx);                                                             \
       return fail(ctx, ALIFMM_E_HIP, "%s: %s", #call, hipGetErrorString(e_));             \
     }                                                                                     \
   } while (0)
@@ -971,9 +996,32 @@ int alifmm_find_rays(alifmm_ctx* ctx, int npairs, const int32_t* field_slot, con
   const bool keep = !ray_xy && ray_xy_cap == ALIFMM_KEEP_RAYS;
   // one subgrid (the usual case): the rays are traced in the caller's order, so the kept points
   // stay on the device, chunk after chunk, and alifmm_take_rays copies them out once
-  const bool dev_keep = keep && groups.size() == 1;
+  // (while the kept bytes stay within keep_budget; past it the kept chunks move to host staging)
+  bool dev_keep = keep && groups.size() == 1;
   release_kept_rays(ctx);
   std::vector<std::vector<double>> staged(((ray_xy || keep) && !dev_keep) ? npairs : 0);
+  size_t kept_bytes = 0;
+  // device-kept chunks -> per-ray host staging (rays ids[0 .. ndone-1] of the single group, in order)
+  auto spill_kept = [&](const std::vector<int>& ids) -> hipError_t {
+    staged.assign(npairs, {});
+    size_t r = 0;
+    for (auto& k : ctx->kept_dev) {
+      std::vector<double> h(2 * (size_t)k.npts);
+      hipError_t e = hipMemcpy(h.data(), k.d, 16 * (size_t)k.npts, hipMemcpyDeviceToHost);
+      if (e != hipSuccess) return e;
+      size_t o = 0;
+      while (o < (size_t)k.npts) {
+        const int id = ids[r++];
+        staged[id].assign(h.begin() + 2 * o, h.begin() + 2 * (o + lens[id]));
+        o += lens[id];
+      }
+    }
+    for (auto& k : ctx->kept_dev) dfree(k.d);
+    ctx->kept_dev.clear();
+    ctx->kept_pts = 0;
+    dev_keep = false;
+    return hipSuccess;
+  };
   for (auto& g : groups) {
     const int sg = g.first;
     const auto& ids = g.second;
@@ -991,6 +1039,7 @@ int alifmm_find_rays(alifmm_ctx* ctx, int npairs, const int32_t* field_slot, con
         jobs[i].ry = rec_xy[2 * k + 1];
         if (f.nz != f0.nz || f.nx != f0.nx) {
           cleanup();
+          release_kept_rays(ctx);
           return fail(ctx, ALIFMM_E_ARG, "find_rays: mixed field shapes for subgrid %d", sg);
         }
       }
@@ -1031,7 +1080,9 @@ int alifmm_find_rays(alifmm_ctx* ctx, int npairs, const int32_t* field_slot, con
         RCHK(dalloc(&d_packed, (size_t)2 * std::max<long long>(off[n], 1)));
         RCHK(hipMemcpyAsync(d_off, off.data(), 8 * n, hipMemcpyHostToDevice, ctx->stream));
         RCHK(af_launch_pack_rays(d_rx, d_ry, d_len, d_off, n, max_pts, d_packed, ctx->stream));
+        if (dev_keep && kept_bytes + 16 * (size_t)off[n] > keep_budget) RCHK(spill_kept(ids));
         if (dev_keep) {  // the chunk's packed points stay on the device (the context owns them now)
+          kept_bytes += 16 * (size_t)off[n];
           ctx->kept_dev.push_back({d_packed, (int64_t)off[n]});
           ctx->kept_pts += off[n];
           d_packed = nullptr;

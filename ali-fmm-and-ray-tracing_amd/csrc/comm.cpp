@@ -32,6 +32,7 @@ struct Rccl {
   decltype(&::ncclGroupEnd) GroupEnd = nullptr;
   decltype(&::ncclSend) Send = nullptr;
   decltype(&::ncclRecv) Recv = nullptr;
+  decltype(&::ncclAllReduce) AllReduce = nullptr;
   decltype(&::ncclGetErrorString) ErrorString = nullptr;
 };
 
@@ -58,6 +59,7 @@ Rccl& rccl() {
     sym(r.GroupEnd, "ncclGroupEnd");
     sym(r.Send, "ncclSend");
     sym(r.Recv, "ncclRecv");
+    sym(r.AllReduce, "ncclAllReduce");
     sym(r.ErrorString, "ncclGetErrorString");
     r.ok = all;
     if (!all) r.why = "librccl.so.1 lacks an expected symbol";
@@ -72,6 +74,7 @@ struct alifmm_comm {
   std::vector<alifmm_ctx*> ctx;  // local members (one per GPU driven by this process)
   std::vector<int> rank;         // their ranks
   std::vector<ncclComm_t> nc;
+  int* dflag = nullptr;  // one process per GPU: device word of the ranks' agreement on a gather's arguments
   std::string err;
 };
 
@@ -113,6 +116,11 @@ int alifmm_comm_init_rank(alifmm_ctx* ctx, int nranks, int rank, const char* id1
   m->ctx = {ctx};
   m->rank = {rank};
   m->nc = {c};
+  if (hipMalloc((void**)&m->dflag, sizeof(int)) != hipSuccess) {
+    (void)R.CommDestroy(c);
+    delete m;
+    return fail(ctx, ALIFMM_E_HIP, "comm_init_rank: out of device memory");
+  }
   *out = m;
   return ALIFMM_OK;
 }
@@ -151,25 +159,20 @@ int alifmm_comm_destroy(alifmm_comm* comm) {
     (void)hipSetDevice(comm->ctx[k]->device);
     if (comm->nc[k] && R.ok) (void)R.CommDestroy(comm->nc[k]);
   }
+  if (comm->dflag) (void)hipFree(comm->dflag);
   delete comm;
   return ALIFMM_OK;
 }
 
 const char* alifmm_comm_last_error(alifmm_comm* comm) { return comm ? comm->err.c_str() : "no communicator"; }
 
-int alifmm_gather_fields(alifmm_comm* comm, int root, int subgrid, const int* first_slot, const int* count,
-                         int dst_slot, double* ms) {
-  if (!comm || !first_slot || !count || root < 0 || root >= comm->nranks || dst_slot < 0)
-    return cfail(comm, ALIFMM_E_ARG, "gather_fields: bad arguments");
-  Rccl& R = rccl();
+// every check of one process's part of a gather (arguments, source slots, the root's destination
+// slots, allocated here); 0 or an error code with comm->err set
+static int gather_check(alifmm_comm* comm, int root, int subgrid, const int* first_slot, const int* count, int dst_slot,
+                        const std::vector<long>& off, size_t* cells_out) {
   const int G = comm->nranks;
-  std::vector<long> off(G + 1, 0);  // root slot of rank r's first field: dst_slot + off[r]
-  for (int r = 0; r < G; r++) {
-    if (count[r] < 0 || first_slot[r] < 0) return cfail(comm, ALIFMM_E_ARG, "gather_fields: rank %d count/slot", r);
-    off[r + 1] = off[r] + count[r];
-  }
-  // field shape from the model of each local member (all ranks hold one model and subgrid)
   size_t cells = 0;
+  // field shape from the model of each local member (all ranks hold one model and subgrid)
   for (size_t k = 0; k < comm->ctx.size(); k++) {
     alifmm_ctx* ctx = comm->ctx[k];
     int fz = 0, fx = 0;
@@ -195,23 +198,52 @@ int alifmm_gather_fields(alifmm_comm* comm, int root, int subgrid, const int* fi
         if (s >= first_slot[root] && s < first_slot[root] + count[root] && d0 != s0)
           return cfail(comm, ALIFMM_E_ARG, "gather_fields: destination slot %d holds one of the root's fields", s);
       }
+      // destination slots (allocated before the group and the clock: no allocation inside)
+      (void)hipSetDevice(ctx->device);
+      for (long i = 0; i < off[G]; i++) {
+        if (i >= off[root] && i < off[root + 1] && d0 == s0) continue;
+        const int rc = af_ensure_field(ctx, dst_slot + (int)i, subgrid, fz, fx);
+        if (rc) return cfail(comm, rc, "gather_fields: %s", ctx->err.c_str());
+      }
     }
   }
+  *cells_out = cells;
+  return ALIFMM_OK;
+}
+
+int alifmm_gather_fields(alifmm_comm* comm, int root, int subgrid, const int* first_slot, const int* count,
+                         int dst_slot, double* ms) {
+  if (!comm || !first_slot || !count || root < 0 || root >= comm->nranks || dst_slot < 0)
+    return cfail(comm, ALIFMM_E_ARG, "gather_fields: bad arguments");
+  Rccl& R = rccl();
   if (!R.ok) return cfail(comm, ALIFMM_E_HIP, "RCCL unavailable: %s", R.why.c_str());
-  // destination slots on the root (allocated before the group and the clock: no allocation inside)
-  for (size_t k = 0; k < comm->ctx.size(); k++) {
-    if (comm->rank[k] != root) continue;
-    alifmm_ctx* ctx = comm->ctx[k];
-    int fz = 0, fx = 0;
-    alifmm_field_shape(ctx, subgrid, &fz, &fx);
+  const int G = comm->nranks;
+  std::vector<long> off(G + 1, 0);  // root slot of rank r's first field: dst_slot + off[r]
+  int rc = ALIFMM_OK;
+  for (int r = 0; r < G && !rc; r++) {
+    if (count[r] < 0 || first_slot[r] < 0) rc = cfail(comm, ALIFMM_E_ARG, "gather_fields: rank %d count/slot", r);
+    off[r + 1] = off[r] + std::max(count[r], 0);
+  }
+  size_t cells = 0;
+  if (!rc) rc = gather_check(comm, root, subgrid, first_slot, count, dst_slot, off, &cells);
+  // one process per GPU: the ranks agree on the checks before anyone posts a send or receive (a
+  // rank that returned alone would leave its peers blocked in the group); min over the ranks' flags
+  if (comm->ctx.size() < (size_t)G) {
+    alifmm_ctx* ctx = comm->ctx[0];
     (void)hipSetDevice(ctx->device);
-    for (long i = 0; i < off[G]; i++) {
-      const int s = dst_slot + (int)i;
-      const bool own_in_place = i >= off[root] && i < off[root + 1] && dst_slot + off[root] == first_slot[root];
-      if (own_in_place) continue;
-      const int rc = af_ensure_field(ctx, s, subgrid, fz, fx);
-      if (rc) return cfail(comm, rc, "gather_fields: %s", ctx->err.c_str());
-    }
+    const int mine = rc ? 0 : 1;
+    int all = 0;
+    if (hipMemcpyAsync(comm->dflag, &mine, sizeof(int), hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
+      (void)hipMemsetAsync(comm->dflag, 0, sizeof(int), ctx->stream);  // still take part, with a failing flag
+    const ncclResult_t e = R.AllReduce(comm->dflag, comm->dflag, 1, ncclInt32, ncclMin, comm->nc[0], ctx->stream);
+    if (e != ncclSuccess) return cfail(comm, ALIFMM_E_HIP, "gather_fields: agreement: %s", R.ErrorString(e));
+    if (hipMemcpyAsync(&all, comm->dflag, sizeof(int), hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+        hipStreamSynchronize(ctx->stream) != hipSuccess)
+      return cfail(comm, ALIFMM_E_HIP, "gather_fields: agreement: copy");
+    if (rc) return rc;
+    if (!all) return cfail(comm, ALIFMM_E_ARG, "gather_fields: another rank rejected the gather");
+  } else if (rc) {
+    return rc;
   }
   const auto t0 = std::chrono::steady_clock::now();
   for (size_t k = 0; k < comm->ctx.size(); k++) {

@@ -26,8 +26,8 @@ struct Field {
 
 struct Arena {  // per-chunk scratch, reused across calls
   int nsrc = 0;
-  long cells = 0, capL = 0, capC = 0, capS = 0;
-  int* S = nullptr;
+  long cells = 0, scells = 0, capL = 0, capC = 0, capS = 0;
+  int* S = nullptr;  // row-major status, scells per source (subgrid > 1 only)
   int* own = nullptr;
   int* lists = nullptr;    // Lin | FS | A | L | C | Cp | D | Rx | Bl | Bp per source
   double* dlists = nullptr;  // Lt | V | Dv per source
@@ -88,7 +88,7 @@ struct alifmm_ctx {
   const af::HandoverOut* ho_last = nullptr;  // what alifmm_init_profile reads (last travel call)
   int n_ho_last = 0;
   int prof = 0;
-  int coop = 0;  // band kernel: cooperative launch (1) or plain launch after a residency check (0)
+  int coop = 1;  // band kernel: cooperative launch (1; 0 under rocprofv3) or plain launch after a residency check (0)
   int members = 0;     // band kernel: workgroups per source (0: as many as the device fits, <= 16)
   int stripe_log = 0;  // band kernel: stripe width log2 (0: 6 for K <= 4, 4 for K >= 8)
   int last_k = 0;      // members per source of the last band launch

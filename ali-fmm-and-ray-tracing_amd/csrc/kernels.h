@@ -75,7 +75,7 @@ struct BandParams {
   const double* scz;
   double gox, goz;
   int prof;  // record BandSrc::ph / lsum (thread 0 reads the wall clock after each barrier)
-  int coop;  // 1: hipLaunchCooperativeKernel; 0: plain launch after a residency check (default)
+  int coop;  // 1: hipLaunchCooperativeKernel (default); 0: plain launch after a residency check (under rocprofv3)
   int K;     // fmm_band_k: members per source (power of two <= kMaxK)
   int wlog;  // fmm_band_k: stripe width log2
   int capR;  // fmm_band_k: rim-list capacity per member and parity

@@ -39,45 +39,3 @@ def gather_plan(n_sources, world):
     for r, p in enumerate(parts):
         slot[p] = off[r] + np.arange(len(p))
     return counts, slot
-
-
-def gather_fields(ctx, n_local, subgrid, rank, world, first_slot=0):
-    """RCCL gather of every rank's resident fields to rank 0 through the library's C-ABI
-    (alifmm_comm_init_rank + alifmm_gather_fields: one ncclSend / ncclRecv per field over xGMI,
-    no padding), the result-return leg of bench.py for N > 1.  torch.distributed (gloo, CPU) only
-    carries the 128-byte RCCL id and the per-rank counts.  Returns the timings (max over ranks)."""
-    import time
-
-    import torch.distributed as dist
-
-    import _alifmm
-
-    uid = [_alifmm.Comm.unique_id() if rank == 0 else None]
-    dist.broadcast_object_list(uid, src=0)
-    counts = [None] * world
-    dist.all_gather_object(counts, int(n_local))
-    t0 = time.perf_counter()
-    comm = _alifmm.Comm.rank(ctx, world, rank, uid[0])
-    init_s = max_over_ranks(time.perf_counter() - t0, dist)
-    try:
-        dist.barrier()
-        ms = comm.gather(0, subgrid, [first_slot] * world, counts, dst_slot=first_slot)
-    finally:
-        comm.close()
-    gather_s = max_over_ranks(ms / 1e3, dist)
-    fz, fx = ctx.field_shape(subgrid)
-    remote = (sum(counts) - counts[0]) * fz * fx * 8
-    return {"rccl_init_ms": init_s * 1e3, "rccl_gather_ms": gather_s * 1e3, "rccl_gather_bytes_into_rank0": remote,
-            "rccl_gather_GBps_into_rank0": remote / gather_s / 1e9 if gather_s > 0 else None,
-            "rccl_gather": "alifmm_gather_fields (library C-ABI, librccl), one message per field"}
-
-
-def max_over_ranks(value, dist=None):
-    """Max of a float over all ranks of the default process group (identity without one)."""
-    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
-        return float(value)
-    import torch
-
-    t = torch.tensor([float(value)], dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())

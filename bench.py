@@ -63,6 +63,44 @@ def parse():
     return ap.parse_args()
 
 
+def max_over_ranks(value, dist=None):
+    """Max of a float over all ranks of the default process group (identity without one)."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return float(value)
+    import torch
+
+    t = torch.tensor([float(value)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def rccl_gather_fields(ctx, n_local, subgrid, rank, world, dist, first_slot=0):
+    """RCCL gather of every rank's resident fields to rank 0 through the library's C-ABI
+    (alifmm_comm_init_rank + alifmm_gather_fields: one ncclSend / ncclRecv per field over xGMI,
+    no padding), the result-return leg for N > 1.  torch.distributed (gloo, CPU) only carries the
+    128-byte RCCL id and the per-rank counts.  Returns the timings (max over ranks)."""
+    import _alifmm
+
+    uid = [_alifmm.Comm.unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(uid, src=0)
+    counts = [None] * world
+    dist.all_gather_object(counts, int(n_local))
+    t0 = time.perf_counter()
+    comm = _alifmm.Comm.rank(ctx, world, rank, uid[0])
+    init_s = max_over_ranks(time.perf_counter() - t0, dist)
+    try:
+        dist.barrier()
+        ms = comm.gather(0, subgrid, [first_slot] * world, counts, dst_slot=first_slot)
+    finally:
+        comm.close()
+    gather_s = max_over_ranks(ms / 1e3, dist)
+    fz, fx = ctx.field_shape(subgrid)
+    remote = (sum(counts) - counts[0]) * fz * fx * 8
+    return {"rccl_init_ms": init_s * 1e3, "rccl_gather_ms": gather_s * 1e3, "rccl_gather_bytes_into_rank0": remote,
+            "rccl_gather_GBps_into_rank0": remote / gather_s / 1e9 if gather_s > 0 else None,
+            "rccl_gather": "alifmm_gather_fields (library C-ABI, librccl), one message per field"}
+
+
 def rank_sources(args, rank, world, dnx):
     import sharding
 
@@ -154,7 +192,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
-        import torch  # noqa: F401  (before the library: one HIP runtime for both, see sharding.gather_fields)
+        import torch  # noqa: F401  (before the library: one HIP runtime for both, see rccl_gather_fields)
         import torch.distributed as dist
 
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -194,7 +232,7 @@ def main():
         init_ms += ti
         band_ms += tb
     barrier()
-    dt = sharding.max_over_ranks(time.perf_counter() - t0, dist)
+    dt = max_over_ranks(time.perf_counter() - t0, dist)
     sweeps = sum(ctx.source_stats(i)[1] for i in range(ns))
     steps_main = [int(ctx.source_stats(i)[0][3]) for i in range(ns)]
     members = int(ctx.get_option("last_k"))
@@ -233,7 +271,7 @@ def main():
         barrier()
         t1 = time.perf_counter()
         _, gbps = ctx.copy_fields(0, ns, 1)
-        d2h = sharding.max_over_ranks(time.perf_counter() - t1, dist)
+        d2h = max_over_ranks(time.perf_counter() - t1, dist)
         ret.update({"d2h_ms": d2h * 1e3, "d2h_GBps_per_gpu": gbps, "bytes_per_gpu": int(cells * 8 * ns),
                     "d2h": "pageable host memory through the library's pinned staging ring, every GPU at once"})
         # the same copy DMA'd straight into the pageable destination, registered for the copy
@@ -241,13 +279,13 @@ def main():
         barrier()
         t1 = time.perf_counter()
         ctx.copy_fields_into(0, dst, range(ns), 1, dst_kind=3)
-        d2h_reg = sharding.max_over_ranks(time.perf_counter() - t1, dist)
+        d2h_reg = max_over_ranks(time.perf_counter() - t1, dist)
         del dst
         ret.update({"d2h_registered_ms": d2h_reg * 1e3, "d2h_registered_GBps_per_gpu": cells * 8 * ns / d2h_reg / 1e9})
         if world > 1 and "ALIFMM_BENCH_DEVICE" in os.environ:
             ret["rccl_gather"] = "skipped: every rank on one device (RCCL needs one GPU per rank)"
         elif world > 1 and args.gather:
-            ret.update(sharding.gather_fields(ctx, ns, 1, rank, world))
+            ret.update(rccl_gather_fields(ctx, ns, 1, rank, world, dist))
     # end to end through the drop-in (N = 1): ALI_FMM.update() on the C4 sources — model digest,
     # fields, and their single copy into the caller's (nsrc, 4096, 4096) stack; the second call is
     # timed (the first uploads the model into the object's own context)

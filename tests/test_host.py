@@ -132,10 +132,10 @@ def _rank_main(rank, world, port, q):
         dist.all_gather_object(allx, np.round(scx / 2.5e-5).astype(np.int64))
         dist.all_gather_object(allid, np.asarray(ids, dtype=np.int64))
         out[weak] = (allx, allid, scz.tolist())
-    # the counts every rank passes to alifmm_gather_fields (sharding.gather_fields), exchanged as there
+    # the counts every rank passes to alifmm_gather_fields (bench.rccl_gather_fields), exchanged as there
     counts = [None] * world
     dist.all_gather_object(counts, len(out[False][0][rank]))
-    m = sharding.max_over_ranks(float(rank) + 0.5, dist)
+    m = bench.max_over_ranks(float(rank) + 0.5, dist)
     if rank == 0:
         q.put((out, counts, m))
     dist.barrier()
@@ -272,3 +272,21 @@ def test_model_key_tracks_every_cell():
         A.trust_model_identity = False
         A._identity_cache.clear()
     assert A._model_digest(args) != k3
+
+
+def test_shutdown_keeps_library_mapped(monkeypatch):
+    """The atexit teardown (_alifmm.shutdown) destroys contexts but leaves libalifmm.so mapped, so
+    the process maps name the HIP library to the end; only under rocprofv3 (ROCPROF* variables) is
+    it unloaded early (the profiler's finalisation runs before the module destructor otherwise)."""
+    import _alifmm
+
+    for k in list(os.environ):
+        if k.startswith(("ROCPROF", "ROCP_")):
+            monkeypatch.delenv(k)
+    _alifmm.lib()
+    _alifmm.shutdown()
+    maps = open("/proc/self/maps").read()
+    assert os.path.realpath(_alifmm.LIB_PATH) in maps
+    assert _alifmm.lib() is not None  # still usable after the teardown
+    monkeypatch.setenv("ROCPROFILER_TEST_MARKER", "1")
+    assert _alifmm._profiler_attached()
