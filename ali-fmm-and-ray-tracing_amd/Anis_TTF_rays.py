@@ -386,6 +386,7 @@ class ALI_FMM:
         self.nsts = self.btg = None
         self.ray_paths_x = self.ray_paths_y = self.ray_len = None
         self.rays = None  # RayStore of the last find_all_TTF_rays* call (compact layout)
+        self.last_timing = None  # time split of the last find_all_TTF_rays* call
         self._ctxs = {}
         self._comms = {}  # device tuple -> _alifmm.Comm (result_return = "rccl")
 
@@ -437,19 +438,46 @@ class ALI_FMM:
         parts = sharding.deal(idx, len(devices))
         results = {}
         errors = []
-        key = _model_key(veln, velpn, vel_map, stif_den, self.velocity_dat, self.phase_vel, self.dnx, self.dnz,
-                         self.gox, self.goz)
+        # The model digest runs in its own thread beside the GPU work (the library calls release the
+        # GIL).  A GPU that holds a resident model computes on it speculatively; if the digest then
+        # differs, the new model is uploaded and the fields are computed again (never returned from
+        # the old model).  A GPU without a model uploads it while the digest runs.
+        mtab = (veln, velpn, vel_map, stif_den, self.velocity_dat, self.phase_vel)
+        box = {}
+
+        def digest():
+            try:
+                box["key"] = _model_key(*mtab, self.dnx, self.dnz, self.gox, self.goz)
+            except Exception as e:  # surfaced by key()
+                box["err"] = e
+
+        hasher = threading.Thread(target=digest)
+        hasher.start()
+
+        def key():
+            hasher.join()
+            if "err" in box:
+                raise box["err"]
+            return box["key"]
 
         def work(dev, ids):
             try:
                 ctx = self._ctx(dev)
-                _load_model(ctx, veln, velpn, vel_map, stif_den, self.velocity_dat, self.phase_vel, self.dnx,
-                            self.dnz, self.gox, self.goz, key=key)
+                speculative = ctx.model_key is not None and bool(ids) and ctx.shape == tuple(np.shape(veln))
+                if not speculative:
+                    if ctx.model_key is None:
+                        ctx.set_model(*_prep_model(*mtab), self.dnx, self.dnz, self.gox, self.goz)
+                        ctx._model_key = key()
+                    else:
+                        _load_model(ctx, *mtab, self.dnx, self.dnz, self.gox, self.goz, key=key())
                 if not ids:
                     return
                 x = np.array([float(self.scx[i]) for i in ids])
                 z = np.array([float(self.scz[i]) for i in ids])
                 ctx.travel(x, z, subgrid=int(subgrid_size), first_slot=0, copy_out=False)
+                if speculative and ctx.model_key != key():  # computed on a stale model: redo
+                    _load_model(ctx, *mtab, self.dnx, self.dnz, self.gox, self.goz, key=key())
+                    ctx.travel(x, z, subgrid=int(subgrid_size), first_slot=0, copy_out=False)
                 out = None
                 if copy_out:
                     if dest is not None:
@@ -470,6 +498,7 @@ class ALI_FMM:
                 t.start()
             for t in th:
                 t.join()
+        hasher.join()
         if errors:
             raise errors[0]
         return results
@@ -639,8 +668,15 @@ class ALI_FMM:
         times = np.zeros((n_trans, n_trans))
         devices = self._devices(n_devices)
         # receivers block-distributed over GPUs; each ray is traced on the GPU holding its receiver field
+        import time
+
+        t0 = time.perf_counter()
         res = self._fields(veln, velpn, vel_map, stif_den, sg, rec, devices, copy_out=False)
+        t_fields = time.perf_counter() - t0
         errors = []
+        # where the call's time goes, per GPU (last_timing): receiver fields, the find_rays call (ray
+        # and packing kernels, points left on the GPU) and its copy-out (take_rays), the host store
+        per_dev = {}
 
         def trace(dev):
             try:
@@ -662,12 +698,18 @@ class ALI_FMM:
                 ctx = self._ctx(dev)
                 src = np.stack([new_trans_x[ii], new_trans_y[ii]], axis=1)
                 dst = np.stack([new_trans_x[jj], new_trans_y[jj]], axis=1)
+                ta = time.perf_counter()
                 t, lens, flags, pts = ctx.find_rays(slots, src, dst, with_points=save_rays, packed=True)
+                tb = time.perf_counter()
                 for _ in range(int(np.count_nonzero(flags & 1))):
                     print(_EARLY_MSG)
                 times[ii, jj] = t
                 if save_rays:
                     store.add(ii, jj, lens, pts if sg == 1 else pts / sg)  # (x / 1 == x: no pass over the points)
+                per_dev[dev] = {"rays": int(len(ii)), "points": int(np.sum(lens, dtype=np.int64)),
+                                "rays_s": tb - ta, "store_s": time.perf_counter() - tb,
+                                **{k: ctx.get_option(k) for k in ("ray_kernel_ms", "ray_pack_ms", "find_rays_ms",
+                                                                  "take_rays_ms")}}
             except Exception as e:
                 errors.append(e)
 
@@ -683,6 +725,8 @@ class ALI_FMM:
             self._ctx(d).release_fields()
         if errors:
             raise errors[0]
+        self.last_timing = {"fields_s": t_fields, "rays_total_s": time.perf_counter() - t0 - t_fields,
+                            "per_gpu": per_dev}
         if save_rays:
             self.rays = store
             self.ray_len = store.ray_len

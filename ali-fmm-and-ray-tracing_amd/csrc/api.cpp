@@ -205,6 +205,12 @@ int alifmm_get_option(alifmm_ctx* ctx, const char* name, double* value) {
   else if (!strcmp(name, "last_k")) *value = ctx->last_k;
   else if (!strcmp(name, "n_cu")) *value = ctx->n_cu;
   else if (!strcmp(name, "vmax")) *value = ctx->vmax;  // model's fastest speed (set_model; the exact-walk stop)
+  // timings of the last alifmm_find_rays / alifmm_take_rays call (ms): ray kernel and point-packing
+  // kernel (HIP events, summed over the launches), the whole call, and the kept points' copy-out
+  else if (!strcmp(name, "ray_kernel_ms")) *value = ctx->t_ray_kernel;
+  else if (!strcmp(name, "ray_pack_ms")) *value = ctx->t_ray_pack;
+  else if (!strcmp(name, "find_rays_ms")) *value = ctx->t_find_rays;
+  else if (!strcmp(name, "take_rays_ms")) *value = ctx->t_take_rays;
   else return fail(ctx, ALIFMM_E_ARG, "unknown option: %s", name);
   return ALIFMM_OK;
 }
@@ -916,6 +922,8 @@ int alifmm_find_rays(alifmm_ctx* ctx, int npairs, const int32_t* field_slot, con
   if (!ctx || !ctx->have_model) return fail(ctx, ALIFMM_E_ARG, "find_rays: no model");
   if (npairs <= 0) return ALIFMM_OK;
   HIPCHK(hipSetDevice(ctx->device));
+  const auto t_call = std::chrono::steady_clock::now();
+  ctx->t_ray_kernel = ctx->t_ray_pack = 0;
   const int max_pts = 5 * (ctx->nz0 + ctx->nx0);
   // group rays by subgrid (one launch per subgrid size present)
   std::map<int, std::vector<int>> by_sg;
@@ -1059,13 +1067,20 @@ int alifmm_find_rays(alifmm_ctx* ctx, int npairs, const int32_t* field_slot, con
       P.ray_len = d_len;
       P.times = d_t;
       P.flags = d_flags;
+      RCHK(hipEventRecord(ctx->ev[0], ctx->stream));
       RCHK(af_launch_rays(&P, ctx->stream));
+      RCHK(hipEventRecord(ctx->ev[1], ctx->stream));
       std::vector<double> t(n);
       std::vector<int> l(n), fl(n);
       RCHK(hipMemcpyAsync(t.data(), d_t, 8 * n, hipMemcpyDeviceToHost, ctx->stream));
       RCHK(hipMemcpyAsync(l.data(), d_len, 4 * n, hipMemcpyDeviceToHost, ctx->stream));
       RCHK(hipMemcpyAsync(fl.data(), d_flags, 4 * n, hipMemcpyDeviceToHost, ctx->stream));
       RCHK(hipStreamSynchronize(ctx->stream));
+      {
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]);
+        ctx->t_ray_kernel += ms;
+      }
       for (int i = 0; i < n; i++) {
         int k = ids[c0 + i];
         tms[k] = t[i];
@@ -1079,7 +1094,15 @@ int alifmm_find_rays(alifmm_ctx* ctx, int npairs, const int32_t* field_slot, con
         d_packed = nullptr;
         RCHK(dalloc(&d_packed, (size_t)2 * std::max<long long>(off[n], 1)));
         RCHK(hipMemcpyAsync(d_off, off.data(), 8 * n, hipMemcpyHostToDevice, ctx->stream));
+        RCHK(hipEventRecord(ctx->ev[2], ctx->stream));
         RCHK(af_launch_pack_rays(d_rx, d_ry, d_len, d_off, n, max_pts, d_packed, ctx->stream));
+        RCHK(hipEventRecord(ctx->ev[3], ctx->stream));
+        RCHK(hipEventSynchronize(ctx->ev[3]));
+        {
+          float ms = 0;
+          (void)hipEventElapsedTime(&ms, ctx->ev[2], ctx->ev[3]);
+          ctx->t_ray_pack += ms;
+        }
         if (dev_keep && kept_bytes + 16 * (size_t)off[n] > keep_budget) RCHK(spill_kept(ids));
         if (dev_keep) {  // the chunk's packed points stay on the device (the context owns them now)
           kept_bytes += 16 * (size_t)off[n];
@@ -1116,6 +1139,7 @@ int alifmm_find_rays(alifmm_ctx* ctx, int npairs, const int32_t* field_slot, con
     if (!rc) rc = fail(ctx, ALIFMM_E_KERNEL, "find_rays: kept points do not add up to the ray lengths");
   }
   cleanup();
+  ctx->t_find_rays = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_call).count();
   // point buffers above kRayBufKeepBytes (C4: 8192 rays x 40 960 points x 16 B = 5.4 GB) are not kept
   // between calls, so they do not hold device memory that later travel / arena allocations need
   if (rb.pts * 2 * sizeof(double) > kRayBufKeepBytes) free_ray_bufs(ctx);
@@ -1130,6 +1154,11 @@ int alifmm_take_rays(alifmm_ctx* ctx, double* ray_xy, int64_t ray_xy_cap, int64_
     return fail(ctx, ALIFMM_E_ARG, "take_rays: ray_xy capacity %lld < %lld", (long long)ray_xy_cap,
                 (long long)ctx->kept_pts);
   int64_t off = 0;
+  const auto t_call = std::chrono::steady_clock::now();
+  auto done = [&](int rc) {
+    ctx->t_take_rays = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_call).count();
+    return rc;
+  };
   if (!ctx->kept_dev.empty()) {  // device-resident chunks: one pass through the pinned ring
     std::vector<D2HSeg> segs;
     for (auto& k : ctx->kept_dev) {
@@ -1139,14 +1168,14 @@ int alifmm_take_rays(alifmm_ctx* ctx, double* ray_xy, int64_t ray_xy_cap, int64_
     HIPCHK(hipSetDevice(ctx->device));
     const int rc = d2h_pageable(ctx, segs);
     release_kept_rays(ctx);
-    return rc;
+    return done(rc);
   }
   for (auto& r : ctx->kept_rays) {
     std::copy(r.begin(), r.end(), ray_xy + 2 * off);
     off += (int64_t)r.size() / 2;
   }
   release_kept_rays(ctx);
-  return ALIFMM_OK;
+  return done(ALIFMM_OK);
 }
 
 int alifmm_put_field(alifmm_ctx* ctx, int slot, int subgrid, const double* data) {

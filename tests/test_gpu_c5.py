@@ -111,6 +111,9 @@ def test_c5_full_matrix_capture(golden, envelope):
                       "trans_pairs[i, 256 + j] = 1 (Weld_rays.py:52-55 pattern)",
            "receiver_fields": ns, "rays": int(ns * ns), "wall_s": wall, "fields_ms": fields_ms,
            "rays_and_host_s": wall - fields_ms / 1e3, "points": int(len(st.points)),
+           # kernel / host split of the call (ALI_FMM.last_timing): fields, then per GPU the ray and
+           # packing kernels (HIP events), the find_rays call, the points' copy-out and the host store
+           "split": M.last_timing,
            "f7_time_rel_err": {str(k): float(v) for k, v in errs.items()}, "sampled_pairs_bit_identical": same}
     envelope["c5_capture"] = rec
     with open(_envelope_file(), "w") as f:

@@ -1,16 +1,22 @@
 #!/bin/bash
 # rocprofv3 passes over the bench configuration (run on the GPU box from the repo root):
 #   tools/profile.sh TAG "stats fetch write sq" [bench args...]  ->  gpurun_out/prof_TAG/PASS/
+# or over another program: PROG="python3 tools/c3_bench.py" tools/profile.sh TAG "stats fetch write"
 # One process per pass (PMC passes never combine with tracing domains); every pass has its own
 # time limit and the script stops at the first failure.  Summarise here afterwards with
-#   python3 tools/traffic.py gpurun_out/prof_TAG TAG   (-> profiles/TAG_kernel_stats.csv, TAG_traffic.json)
+#   python3 tools/traffic.py gpurun_out/prof_TAG TAG [KERNEL]
+#   (-> profiles/TAG_kernel_stats.csv, TAG_traffic.json for KERNEL, default fmm_band_k_kernel)
 TAG=$1; PASSES=$2; shift 2
 ROOT=$PWD
 OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 cd /tmp
-B="python3 $ROOT/bench.py --no-cpu --no-return --no-e2e"
+if [ -n "$PROG" ]; then
+  B=$(echo "$PROG" | sed "s|tools/|$ROOT/tools/|")
+else
+  B="python3 $ROOT/bench.py --no-cpu --no-return --no-e2e"
+fi
 for PASS in $PASSES; do
   case $PASS in
     stats) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o run -- $B "$@" > $OUT/stats.log 2>&1 ;;
@@ -27,4 +33,4 @@ for PASS in $PASSES; do
   echo "pass $PASS exit status $rc"
   [ $rc -eq 0 ] || exit $rc
 done
-grep -h '"metric"' $OUT/*.log | tail -1 | cut -c1-300
+grep -h '^{' $OUT/*.log | tail -1 | cut -c1-300 || true

@@ -1,6 +1,8 @@
 """Summarise a tools/profile.sh run: kernel-trace stats -> profiles/TAG_kernel_stats.csv, and the
-per-launch HBM-side traffic of the band kernel (fmm_band_k_kernel) from the FETCH_SIZE / WRITE_SIZE passes ->
-profiles/TAG_traffic.json (bench.py reports it as roofline.traffic when the library matches).
+per-launch HBM-side traffic of one kernel (argv[3], default the band kernel fmm_band_k_kernel) from
+the FETCH_SIZE / WRITE_SIZE passes, with its SQ issue profile when that pass ran ->
+profiles/TAG_traffic.json (bench.py reports it as roofline.traffic when the library and the bench
+workload match).
 
 Correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE counts 128-B requests at 64 B on gfx950,
 so read bytes = 2 x FETCH_SIZE; WRITE_SIZE is taken as is.  Both derive from the L2's memory-side
@@ -16,6 +18,7 @@ import shutil
 import sys
 
 out, tag = sys.argv[1], sys.argv[2]
+kernel = sys.argv[3] if len(sys.argv) > 3 else "fmm_band_k_kernel"
 repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 stats = glob.glob(os.path.join(out, "stats", "*kernel_stats.csv"))
 if stats:
@@ -26,9 +29,18 @@ def per_launch(d, counter):
     vals = {}
     for f in glob.glob(os.path.join(out, d, "*counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            if "fmm_band_k_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
                 vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
     return sum(vals.values()) / len(vals) if vals else None
+
+
+def n_launch(d):
+    ids = set()
+    for f in glob.glob(os.path.join(out, d, "*counter_collection.csv")):
+        for r in csv.DictReader(open(f)):
+            if kernel in r["Kernel_Name"]:
+                ids.add(r["Dispatch_Id"])
+    return len(ids)
 
 
 fetch_kb = per_launch("pmc_fetch", "FETCH_SIZE")
@@ -51,7 +63,8 @@ for f in ("pmc_fetch.log", "pmc_write.log", "pmc_sq.log"):
     except (OSError, IndexError):
         pass
 res = {
-    "kernel": "fmm_band_k_kernel",
+    "kernel": kernel,
+    "launches": {d: n for d, n in (("pmc_fetch", n_launch("pmc_fetch")), ("pmc_sq", n_launch("pmc_sq"))) if n},
     "fetch_size_kb_per_launch": fetch_kb,
     "write_size_kb_per_launch": write_kb,
     "traffic_bytes_per_launch": (2 * fetch_kb + write_kb) * 1024 if fetch_kb and write_kb else None,
@@ -62,6 +75,7 @@ res = {
     "valu_insts_per_launch": sq["SQ_INSTS_VALU"],
     "sq_wait_any_frac": (sq["SQ_WAIT_ANY"] / sq["SQ_WAVE_CYCLES"]) if sq["SQ_WAIT_ANY"] and sq["SQ_WAVE_CYCLES"] else None,
     "sq_active_valu_frac": (sq["SQ_ACTIVE_INST_VALU"] / sq["SQ_WAVE_CYCLES"]) if sq["SQ_ACTIVE_INST_VALU"] and sq["SQ_WAVE_CYCLES"] else None,
+    "sq_per_launch": sq,
     # the workload keys bench.py matches before it reports the figure as roofline.traffic
     "sources_per_gpu": (bench_config or {}).get("sources_per_gpu"),
     "grid": (bench_config or {}).get("grid"),
