@@ -14,6 +14,9 @@
 #include <cstring>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <cstdlib>
+#include <mutex>
 #include <map>
 #include <string>
 #include <thread>
@@ -143,10 +146,13 @@ int alifmm_release_fields(alifmm_ctx* ctx) {
   return ALIFMM_OK;
 }
 
+static void destroy_team(alifmm_ctx* ctx);
+
 int alifmm_ctx_destroy(alifmm_ctx* ctx) {
   if (!ctx) return ALIFMM_OK;
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
+  destroy_team(ctx);
   alifmm_release_fields(ctx);
   free_arena(ctx->arena);
   dfree(ctx->ho_all);
@@ -183,6 +189,7 @@ int alifmm_set_option(alifmm_ctx* ctx, const char* name, double value) {
   else if (!strcmp(name, "prof")) ctx->prof = value != 0;
   else if (!strcmp(name, "coop")) ctx->coop = value != 0;
   else if (!strcmp(name, "exact_r") && value >= 0 && value <= 48) ctx->exact_r = (int)value;
+  else if (!strcmp(name, "exact_lds")) ctx->exact_lds = value != 0;
   else if (!strcmp(name, "members") && value >= 0 && value <= af::kMaxK && value == (int)value)
     ctx->members = (int)value;
   else if (!strcmp(name, "stripe_log") && (value == 0 || (value >= 3 && value <= 12))) ctx->stripe_log = (int)value;
@@ -198,6 +205,7 @@ int alifmm_get_option(alifmm_ctx* ctx, const char* name, double* value) {
   else if (!strcmp(name, "r_far")) *value = ctx->r_far;
   else if (!strcmp(name, "batch")) *value = ctx->batch;
   else if (!strcmp(name, "exact_r")) *value = ctx->exact_r;
+  else if (!strcmp(name, "exact_lds")) *value = ctx->exact_lds;
   else if (!strcmp(name, "prof")) *value = ctx->prof;
   else if (!strcmp(name, "coop")) *value = ctx->coop;
   else if (!strcmp(name, "members")) *value = ctx->members;
@@ -647,10 +655,30 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
     // beyond the stage-2 window (field units before the final / subgrid: coarse dnx per fine node)
     const long size2 = 2L * sg + (sg - 1) / 2 + 3L * sg;
     P.tstop = (double)(size2 + ctx->exact_r) * ctx->dnx / ctx->vmax;
+    P.exact_r = ctx->exact_r;
     P.capL = (int)capL;
     P.capS = (int)capS;
     P.src = a.srcs;
-    HIPCHK(af_launch_exact(&P, ctx->stream));
+    if (ctx->exact_lds && af_exact_lds_fits(sg, ctx->exact_r)) {
+      HIPCHK(af_launch_exact_lds(&P, ctx->stream));
+      // a heap past the LDS walk's capacity (error 9): those sources again, from scratch, with
+      // the HBM walk (fmm_exact.hip)
+      std::vector<af::BandSrc> chk(n);
+      HIPCHK(hipMemcpyAsync(chk.data(), a.srcs, sizeof(af::BandSrc) * n, hipMemcpyDeviceToHost, ctx->stream));
+      HIPCHK(hipStreamSynchronize(ctx->stream));
+      bool redo = false;
+      for (int i = 0; i < n; i++) redo |= chk[i].err == 9;
+      if (redo) {
+        for (int i = 0; i < n; i++) {
+          HIPCHK(hipMemsetAsync(hs[i].T, 0xFF, (size_t)cells * 8, ctx->stream));
+          HIPCHK(hipMemsetAsync(hs[i].S, 0xFF, (size_t)cells * 4, ctx->stream));
+        }
+        HIPCHK(hipMemcpyAsync(a.srcs, hs.data(), sizeof(af::BandSrc) * n, hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(af_launch_exact(&P, ctx->stream));
+      }
+    } else {
+      HIPCHK(af_launch_exact(&P, ctx->stream));
+    }
   }
   HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
   if (fs != ctx->stream) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_fill, 0));
@@ -792,20 +820,89 @@ int alifmm_get_field(alifmm_ctx* ctx, int slot, double* out) {
   return ALIFMM_OK;
 }
 
-// host copy of one staged piece by a team of threads (one slice each)
-static void team_memcpy(char* dst, const char* src, size_t n, int nthreads) {
-  if (nthreads <= 1 || n < (4u << 20)) {
-    memcpy(dst, src, n);
-    return;
+// Host copy of one staged piece by a persistent team of threads (one slice each), one team per
+// context (created on first use, joined by alifmm_ctx_destroy); its size is OMP_NUM_THREADS when
+// set (the job's CPU share on the GPU box, 16), else up to 8.  Creating the threads per piece cost
+// ~0.1 ms per 32 MiB piece (≈60 ms for a 17 GB stack).
+class CopyTeam {
+ public:
+  explicit CopyTeam(int n) : n_(n) {
+    for (int t = 1; t < n_; t++) th_.emplace_back([this, t] { run(t); });
   }
-  std::vector<std::thread> team;
-  const size_t slice = (n + nthreads - 1) / nthreads;
-  for (int t = 0; t < nthreads; t++) {
-    const size_t o = t * slice;
-    if (o >= n) break;
-    team.emplace_back([=] { memcpy(dst + o, src + o, std::min(slice, n - o)); });
+  ~CopyTeam() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+      gen_++;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
   }
-  for (auto& th : team) th.join();
+  int size() const { return n_; }
+  void copy(char* dst, const char* src, size_t n) {
+    if (n_ <= 1 || n < (4u << 20)) {
+      memcpy(dst, src, n);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> g(m_);
+      dst_ = dst;
+      src_ = src;
+      bytes_ = n;
+      left_ = n_ - 1;
+      gen_++;
+    }
+    cv_.notify_all();
+    slice(0);
+    std::unique_lock<std::mutex> l(m_);
+    done_.wait(l, [&] { return left_ == 0; });
+  }
+
+ private:
+  void slice(int t) const {
+    const size_t s = ((bytes_ + n_ - 1) / n_ + 4095) & ~(size_t)4095, o = (size_t)t * s;
+    if (o < bytes_) memcpy(dst_ + o, src_ + o, std::min(s, bytes_ - o));
+  }
+  void run(int t) {
+    unsigned long seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> l(m_);
+        cv_.wait(l, [&] { return gen_ != seen; });
+        seen = gen_;
+        if (stop_) return;
+      }
+      slice(t);
+      std::lock_guard<std::mutex> g(m_);
+      if (--left_ == 0) done_.notify_one();
+    }
+  }
+  int n_;
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_, done_;
+  char* dst_ = nullptr;
+  const char* src_ = nullptr;
+  size_t bytes_ = 0;
+  int left_ = 0;
+  unsigned long gen_ = 0;
+  bool stop_ = false;
+};
+
+static CopyTeam& copy_team(alifmm_ctx* ctx) {
+  if (!ctx->team) {
+    int n = (int)std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
+    if (const char* e = getenv("OMP_NUM_THREADS")) {
+      const int v = atoi(e);
+      if (v >= 1) n = std::min(v, 32);
+    }
+    ctx->team = new CopyTeam(n);
+  }
+  return *static_cast<CopyTeam*>(ctx->team);
+}
+static void destroy_team(alifmm_ctx* ctx) {
+  delete static_cast<CopyTeam*>(ctx->team);
+  ctx->team = nullptr;
 }
 
 // Device -> pageable host copy of a list of segments: pieces of kPinBytes through kPinBufs pinned
@@ -831,11 +928,11 @@ static int d2h_pageable(alifmm_ctx* ctx, const std::vector<D2HSeg>& segs) {
     hipError_t e = hipMemcpyAsync(ctx->pin[i % nb], pieces[i].src, pieces[i].bytes, hipMemcpyDeviceToHost, ctx->stream);
     return e == hipSuccess ? hipEventRecord(ctx->pin_ev[i % nb], ctx->stream) : e;
   };
-  const int team = (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+  CopyTeam& team = copy_team(ctx);
   for (long i = 0; i < std::min<long>(nb, np); i++) HIPCHK(issue(i));
   for (long i = 0; i < np; i++) {
     HIPCHK(hipEventSynchronize(ctx->pin_ev[i % nb]));
-    team_memcpy(pieces[i].dst, (const char*)ctx->pin[i % nb], pieces[i].bytes, team);
+    team.copy(pieces[i].dst, (const char*)ctx->pin[i % nb], pieces[i].bytes);
     if (i + nb < np) HIPCHK(issue(i + nb));
   }
   return ALIFMM_OK;

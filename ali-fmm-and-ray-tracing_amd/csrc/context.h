@@ -80,6 +80,8 @@ struct alifmm_ctx {
   double cdelta = 0.5, r0 = 40.0;
   double cdelta_far = 0.0, r_far = 0.0;  // band width beyond r_far nodes (0: off)
   int exact_r = 20;
+  void* team = nullptr;  // api.cpp CopyTeam: host copy threads of the pinned staging ring
+  int exact_lds = 1;  // subgrid > 1: the LDS exact walk (fmm_exact_lds.hip) when it fits (0: fmm_exact.hip)
   int batch = 256;
   // subgrid-1 source init of a whole multi-launch travel call (one init launch for every chunk)
   af::HandoverOut* ho_all = nullptr;

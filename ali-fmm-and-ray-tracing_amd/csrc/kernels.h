@@ -68,6 +68,7 @@ struct BandParams {
   double cdelta, vmax, r0;
   double cdelta_far, r_far;  // band width beyond r_far nodes (0: off), ramped in over r_far .. 2 r_far
   double tstop;  // mode 1: the exact main-loop prefix stops when the heap root reaches it (fmm_exact_kernel)
+  int exact_r;   // mode 1: tstop = (stage-2 half-width + exact_r) dnx / vmax (fmm_exact_lds: its window)
   int capL, capC, capS;  // list capacities, stage-grid capacity (cells)
   BandSrc* src;
   const HandoverOut* ho;  // mode 0
@@ -139,6 +140,8 @@ struct LocalOpsParams {
 extern "C" {
 hipError_t af_launch_init(const af::DevModel* M, af::InitJob* jobs, int njobs, af::HandoverOut* out, hipStream_t stream);
 hipError_t af_launch_exact(const af::BandParams* P, hipStream_t stream);
+hipError_t af_launch_exact_lds(const af::BandParams* P, hipStream_t stream);
+int af_exact_lds_fits(int sg, int exact_r);  // fmm_exact_lds holds the stage grids of subgrid sg
 hipError_t af_launch_band_k(const af::BandParams* P, hipStream_t stream);
 int af_band_wgs_per_cu(void);  // band-kernel workgroups resident per CU (fmm_band_k.hip AF_WG_PER_CU)
 // the band kernel's working-field layout: pitch and size (doubles) for an nz x nx main grid
