@@ -419,8 +419,11 @@ template <int MODE, bool LDSMAT, bool PROF>
 #ifndef AF_WPE
 #define AF_WPE 1
 #endif
+#ifndef AF_WPE_N
+#define AF_WPE_N 3  // waves per SIMD the registers are sized for
+#endif
 #if AF_WPE
-#define AF_WPE_ATTR __attribute__((amdgpu_waves_per_eu(3)))
+#define AF_WPE_ATTR __attribute__((amdgpu_waves_per_eu(AF_WPE_N)))
 #else
 #define AF_WPE_ATTR
 #endif

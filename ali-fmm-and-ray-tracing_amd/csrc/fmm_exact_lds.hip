@@ -155,7 +155,8 @@ struct Heap {
     int tpp = parent(tpc);
     while (tpp > 0) {
       const double kp = L->key[tpp];
-      const unsigned ep = L->ent[tpp];
+      unsigned ep = L->ent[tpp];
+      asm volatile("" : "+v"(ep));  // both reads in one LDS round trip (not the entry after the compare)
       if (!(km < kp)) break;
       setpos(em, tpp);
       setpos(ep, tpc);
@@ -197,14 +198,16 @@ struct Heap {
     setpos(e, ntr);
     sift_up(ntr, key);
   }
-  AF_DEV void upd(int c, double key) {
+  // returns whether the node has another heap entry (its keys then follow, sync)
+  AF_DEV bool upd(int c, double key) {
     const int tpc = pos_of(c);
     L->key[tpc] = key;
+    const bool d = (L->ent[tpc] & kDupF) != 0u;
     sift_up(tpc, key);
+    return d;
   }
-  // node c's ttn is now key: every heap entry of a node with two entries takes it
+  // node c (with two heap entries) has ttn key now: every entry of it takes it
   AF_DEV void sync(int c, double key) {
-    if (!isdup(c)) return;
     for (int k = 1; k <= ntr; k++)
       if ((int)(L->ent[k] & kNodeM) == c) L->key[k] = key;
   }
@@ -226,7 +229,8 @@ struct Heap {
     int tpp = 1, tpc = 2;
     while (tpc < ntr) {
       const double k1 = L->key[tpc], k2 = L->key[tpc + 1];
-      const unsigned e1 = L->ent[tpc], e2 = L->ent[tpc + 1];
+      unsigned e1 = L->ent[tpc], e2 = L->ent[tpc + 1];
+      asm volatile("" : "+v"(e1), "+v"(e2));  // keys and entries in one LDS round trip
       const bool right = k1 > k2;
       const int t = right ? tpc + 1 : tpc;
       const double kc = right ? k2 : k1;
@@ -559,9 +563,9 @@ AF_DEV long long walk(Lds* L, Heap& h, const DevModel& M, const XG& g, bool stag
           v = fouds18(F, M, cell_mat(M, g.mv, rz, rx), rz, rx, g.dnx, g.dnz, g.nx, g.nz, mat_slo(M, g.mv, rz, rx));
         }
         gst(g.T + (long)rz * g.nx + rx, v);
+        // a far node's new entry is its only one; an updated node's entry says whether it has two
         if ((fm >> k) & 1ull) h.add(r, v, true);
-        else h.upd(r, v);
-        if (h.ndup) h.sync(r, v);
+        else if (h.upd(r, v)) h.sync(r, v);
       }
       v = rlane(v, 0);
       patch(L, sp, rz, rx, v, lane);

@@ -58,7 +58,7 @@ struct InitLds {
   long long rbusy;                  // profile: relax-role ticks of the current walk
   long long rjobs;                  // profile: relaxations | fouds18_A() fallbacks << 32
 #if AF_INIT_DIAG
-  long long dg[8];                  // diagnostic build: shader-clock cycles per activity (AF_DG)
+  long long dg[12];                 // diagnostic build: shader-clock cycles per activity (AF_DG)
 #endif
 };
 
@@ -426,6 +426,7 @@ AF_DEV void relax_role(InitLds* L, const DevModel& M, const MatView& mv, const M
     if (cmd < 0) break;  // stop (or timeout: the heap role is gone)
     last = cmd;
     const long long t0 = wall_clock64();
+    AF_DG_T0(tjl)
     // the pop's jobs (read once: the heap role refills them after the last one is done), in
     // wave-uniform registers; job(i) selects without dynamic indexing
     const int nj = L->njob;
@@ -536,6 +537,8 @@ AF_DEV void relax_role(InitLds* L, const DevModel& M, const MatView& mv, const M
     // neighbours as the heap wavefront will (x-1, x+1, z-1, z+1; far -> add, close -> update, the
     // stage-1 quirk on x-neighbour updates), and verify those jobs now.  Only an identical job list
     // at the next command uses the result.
+    if (lane == 0) { AF_DG_ADD(L, 11, tjl) }
+    AF_DG_T0(tpb)
     pred_n = -1;
 #if AF_INIT_PREDICT
     if (nj > 0) {
@@ -568,11 +571,14 @@ AF_DEV void relax_role(InitLds* L, const DevModel& M, const MatView& mv, const M
       }
       if (pn > 0) {
         pred_jv = make_int4(o[0], o[1], o[2], o[3]);
+        AF_DG_T0(tpv)
         pred_hk = verify(pred_jv, pn, 0, pred_src, pred_sv);
+        if (lane == 0) { AF_DG_ADD(L, 9, tpv) }
         pred_n = pn;
       }
     }
 #endif
+    if (lane == 0) { AF_DG_ADD(L, 8, tpb) }
     busy += wall_clock64() - t0;
   }
   if (lane == 0) {
@@ -726,7 +732,7 @@ __global__ __launch_bounds__(128) void fmm_init_kernel(DevModel M0, InitJob* job
   if (src >= njobs) return;
   const int lane = threadIdx.x, nl = blockDim.x;
 #if AF_INIT_DIAG
-  if (lane < 8) L->dg[lane] = 0;
+  if (lane < 12) L->dg[lane] = 0;
 #endif
   InitJob J = jobs[src];
   const int nnz = M.nz0, nnx = M.nx0;
@@ -880,6 +886,7 @@ __global__ __launch_bounds__(128) void fmm_init_kernel(DevModel M0, InitJob* job
         }
 #if AF_INIT_DIAG
         for (int k = 0; k < 8; k++) O->prof[8 + k] = L->dg[k];
+        for (int k = 0; k < 4; k++) O->prof[k] = L->dg[8 + k];  // (diagnostic builds: the stage ticks' slots)
 #endif
         O->n = n;
         O->err = err;
@@ -903,6 +910,7 @@ __global__ __launch_bounds__(128) void fmm_init_kernel(DevModel M0, InitJob* job
     }
 #if AF_INIT_DIAG
     for (int k = 0; k < 8; k++) O->prof[8 + k] = L->dg[k];
+    for (int k = 0; k < 4; k++) O->prof[k] = L->dg[8 + k];  // (diagnostic builds: the stage ticks' slots)
 #endif
     O->n = n;
     O->err = err;

@@ -296,10 +296,15 @@ def main():
         ctx.release_fields()
         M = A.ALI_FMM(model[0], model[1], model[2], scx, scz, stif_den=model[3], dnx=dnx)
         M.update(model[0], model[1], model[2], model[3])
-        t1 = time.perf_counter()
-        F = M.update(model[0], model[1], model[2], model[3])
-        te = time.perf_counter() - t1
-        e2e = {"update_s": te, "cell_updates_per_s": cells * ns / te, "sources_per_s": ns / te,
+        runs = []
+        for _ in range(2):  # steady state: the better of two calls (each returns a fresh 17 GB stack)
+            t1 = time.perf_counter()
+            F = M.update(model[0], model[1], model[2], model[3])
+            runs.append(time.perf_counter() - t1)
+            if _ == 0:
+                del F
+        te = min(runs)
+        e2e = {"update_s": te, "update_s_runs": runs, "cell_updates_per_s": cells * ns / te, "sources_per_s": ns / te,
                "stack_bytes": int(F.nbytes), "fields_ms": M._ctx(0).last_timing()[2],
                "what": "ALI_FMM.update() at C4: model digest (xxh3 of every array) + fields on the GPU + one "
                        "copy of each field into the returned stack (no intermediate array; host peak = one stack)"}

@@ -52,7 +52,10 @@ int alifmm_set_model(alifmm_ctx* ctx, int nnz, int nnx, const double* veln, cons
  * band profile, alifmm_band_profile), "cdelta" (band width in units of dnx/vmax, default 0.5),
  * "r0" (near-source band schedule radius in cells, default 40), "exact_r" (radius in cells of the
  * exact heap-ordered main-loop prefix, 0..48, default 20), "batch" (sources per launch, default
- * 256). */
+ * 256), "exact_lds" (subgrid > 1: 1 = the exact walk with its state in LDS, fmm_exact_lds.hip,
+ * where the stage grids fit — subgrid <= 9; 0 = the HBM walk, fmm_exact.hip; bit-identical),
+ * "coop" (band launch: 1 = cooperative, 0 = plain after a residency check), "cdelta_far" /
+ * "r_far" (optional wider band beyond r_far cells; off by default). */
 int alifmm_set_option(alifmm_ctx* ctx, const char* name, double value);
 /* Read an option, or "last_k" (workgroups per source of the last band launch), "n_cu"
  * (compute units of the device) and "vmax" (the model's fastest speed [m/s]: the exact prefix

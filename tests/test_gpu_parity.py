@@ -364,6 +364,31 @@ def test_members_bit_identical(ctx, envelope):
     ctx.release_fields()
 
 
+def test_exact_walk_lds_equals_hbm(ctx, envelope):
+    """travel_finer_grid()'s exact heap walk in LDS (fmm_exact_lds.hip: statuses, heap indices and
+    speculative stencils in LDS) gives the same bits as the HBM walk (fmm_exact.hip) it replaces:
+    weld sources on the bottom edge and in the interior (the whole 397 x 397 stage-1 grid) at
+    subgrid 9, edge sources at subgrid 3 and 5 (Anis_TTF_rays.py:2187-2504, :2775-2817)."""
+    vt = W.default_table()
+    veln, velpn, vm, sd = W.weld_model()
+    ctx.set_model(veln, velpn, vm, sd, vt, vt, 2e-4)
+    scx, scz = W.weld_transducers()
+    cases = [(np.array([scx[46], 250 * 2e-4]), np.array([scz[46], 212 * 2e-4]), 9),
+             (scx[[0, 15, 46]], scz[[0, 15, 46]], 3), (scx[[30, 61]], scz[[30, 61]], 5)]
+    try:
+        for x, z, sg in cases:
+            ctx.set_option("exact_lds", 0)
+            ref = ctx.travel(x, z, subgrid=sg)
+            ctx.set_option("exact_lds", 1)
+            F = ctx.travel(x, z, subgrid=sg)
+            same = [bool(np.array_equal(F[i], ref[i], equal_nan=True)) for i in range(len(x))]
+            envelope.setdefault("exact_walk_lds_vs_hbm", []).append({"subgrid": sg, "bit_identical": same})
+            assert all(same), (sg, same)
+    finally:
+        ctx.set_option("exact_lds", 1)
+    ctx.release_fields()
+
+
 def test_band_fouds18_path_vs_oracle(golden, ctx, envelope):
     """fouds18_A() as the band kernel runs it (the material record + the per-material slownesses
     precomputed by mat_slowness_kernel, fouds18<true>) against the oracle's fouds18_A with the

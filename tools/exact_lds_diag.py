@@ -1,0 +1,34 @@
+"""Cycle split of the LDS exact walk (diagnostic build AF_XL_DIAG=1, GPU box): weld example, 31
+bottom receivers at subgrid 9; per source 0: shader-clock cycles of pop, relaxation value by path
+(clean speculative entry / stencil stage unchanged / finish on the entry's lane / evaluation pass)
+and commit, with the path counts -> one JSON line.
+ALIFMM_LIB=variants/xdiag/libalifmm.so python tools/exact_lds_diag.py"""
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "ali-fmm-and-ray-tracing_amd"), os.path.join(REPO, "tests")]
+import numpy as np  # noqa: E402
+import _alifmm  # noqa: E402
+import workloads as W  # noqa: E402
+
+ctx = _alifmm.Context(0)
+vt = W.default_table()
+veln, velpn, vm, sd = W.weld_model()
+ctx.set_model(veln, velpn, vm, sd, vt, vt, 2e-4)
+sx, sz = W.weld_transducers()
+rx, rz = np.asarray(sx[31:]), np.asarray(sz[31:])
+ctx.travel(rx, rz, subgrid=9, copy_out=False)
+init_ms = ctx.last_timing()[0]
+bp = ctx.band_profile(0).astype(float)
+steps = ctx.source_stats(0)[0]
+pops = float(steps[0] + steps[1] + steps[2])
+names = ["pop", "entry_clean", "entry_same_stage", "entry_finish", "eval_pass", "commit"]
+out = {"fields": len(rx), "subgrid": 9, "init_ms": init_ms, "pops_src0": pops,
+       "relaxations_src0": bp[10], "passes_src0": bp[11], "same_stage_src0": bp[12], "finishes_src0": bp[13],
+       "cycles_per_pop": {n: round(bp[k] / pops, 1) for k, n in enumerate(names)},
+       "cycles_per_event": {"entry_same_stage": round(bp[2] / max(bp[12], 1), 1),
+                            "entry_finish": round(bp[3] / max(bp[13], 1), 1),
+                            "eval_pass": round(bp[4] / max(bp[11], 1), 1)}}
+print(json.dumps(out))
