@@ -36,8 +36,8 @@ constexpr int kThreads = 256;  // 4 waves clear and hand over; wave 0 walks
 #ifndef AF_XL_DIAG
 #define AF_XL_DIAG 0  // diagnostic build: cycle counters of the walk (walk(), BandSrc::ph / sub)
 #endif
-#ifndef AF_XL_POPWAVE
-#define AF_XL_POPWAVE 0  // pop_wave (1) measured no faster than the one-lane pop (618 vs 606 ms, weld sg 9)
+#ifndef AF_XL_TWO_ROLE
+#define AF_XL_TWO_ROLE 1  // heap wavefront + relax wavefront (1), or one wavefront doing both (0)
 #endif
 constexpr int kCap = 163840;   // status nodes (2 bits each): stage grids up to 404 x 404
 constexpr int kHeap = 4096;    // heap slots (1-based)
@@ -60,6 +60,12 @@ struct Lds {
   signed char dec[kDec];
   int dup[kDup];
   int nused;  // hash slots that are live or tombstones
+  // two-role walk (heap wavefront -> relax wavefront): command sequence number (-1 stop), the
+  // pop's relaxation jobs (node | fresh << 31), relaxations done / applied to the heap (running
+  // counts), their values, the heap size (for the relax role's guesses), serial (see heap_role)
+  int cmd, done, applied, njob, serial, ntr_hint;
+  int job[4];
+  double jval[4];
 };
 
 AF_DEV double rlane(double v, int l) {
@@ -114,6 +120,7 @@ struct XField {
 struct Heap {
   Lds* L;
   int ntr = 0, err = 0, ndup = 0;
+  int livedup = 0;  // heap entries carrying kDupF
   AF_DEV static int parent(int t) {  // round(t / 2), half-even (:123)
     const int m = t >> 1;
     return (t & 1) ? ((m & 1) ? m + 1 : m) : m;
@@ -186,7 +193,10 @@ struct Heap {
       L->dup[ndup++] = c;
       const int hs = hfind(c);
       for (int k = 1; k < ntr; k++)  // its other entries now carry the flag
-        if ((int)(L->ent[k] & kNodeM) == c) L->ent[k] |= kDupF;
+        if ((int)(L->ent[k] & kNodeM) == c && !(L->ent[k] & kDupF)) {
+          L->ent[k] |= kDupF;
+          livedup++;
+        }
       e = (unsigned)c | ((unsigned)hs << 18) | kDupF;
     } else {
       int hs = fresh ? -1 : hfind(c);  // a popped node with two entries keeps its slot
@@ -194,6 +204,7 @@ struct Heap {
       e = (unsigned)c | ((unsigned)hs << 18) | (!fresh && isdup(c) ? kDupF : 0u);
       sset(L, c, kSClose);
     }
+    if (e & kDupF) livedup++;
     L->ent[ntr] = e;
     setpos(e, ntr);
     sift_up(ntr, key);
@@ -214,10 +225,14 @@ struct Heap {
   // pop the root (its status -> known, its heap-index slot freed unless the node has another
   // entry), then downtree
   AF_DEV void pop() {
+    pop_known();
+    pop_rest();
+  }
+  AF_DEV void pop_known() { sset(L, (int)(L->ent[1] & kNodeM), kSKnown); }
+  AF_DEV void pop_rest() {
     const unsigned e0 = L->ent[1];
-    const int c = (int)(e0 & kNodeM);
-    sset(L, c, kSKnown);
     if (!(e0 & kDupF)) L->ht[(e0 >> 18) & (kHT - 1)] = kTomb;
+    else livedup--;
     if (ntr == 1) {
       ntr = 0;
       return;
@@ -261,103 +276,6 @@ struct Heap {
     L->key[tpp] = km;
   }
 };
-
-// Pop + downtree over the whole wavefront (wave 0, every lane).  downtree's path is the chain of
-// smaller children (ties to the left, :178-237) for as long as they are below the moved key; the
-// lanes load a 4-level subtree (30 nodes) at a time, one ballot gives every pair's smaller child
-// and one the children below the moved key, and the path is walked on those masks — one LDS round
-// trip per 4 levels instead of one per level.  The moved entries are then written in parallel
-// (each to its parent's slot), which leaves heap, keys and heap indices as the sequential
-// downtree does, except where a node with two heap entries moves (the order of its index writes
-// matters): then Heap::pop runs instead.
-AF_DEV void pop_wave(Lds* L, Heap& h, int lane) {
-  const int ntr = __shfl(h.ntr, 0);
-  if (ntr <= 1) {
-    if (lane == 0) h.pop();
-    return;
-  }
-  const unsigned em = L->ent[ntr];
-  const double km = L->key[ntr];
-  const int n = ntr - 1;
-  const bool sl = lane < 30;
-  const int d = lane < 2 ? 1 : lane < 6 ? 2 : lane < 14 ? 3 : 4;  // level below the chunk base
-  const int o = lane - ((1 << d) - 2);
-  double ck[4];
-  unsigned ce[4];
-  int cn[4];
-  bool cm[4];
-  int b = 1, tpp = 1;
-  bool done = false, dup = (em & kDupF) != 0u;
-#pragma unroll
-  for (int ch = 0; ch < 4; ch++) {
-    cm[ch] = false;
-    ck[ch] = 0.0;
-    ce[ch] = 0u;
-    cn[ch] = 0;
-    if (done) continue;
-    const int node = sl ? (b << d) + o : 0;
-    const bool valid = sl && node <= n;
-    const double k = valid ? L->key[node] : INFINITY;
-    const unsigned e = valid ? L->ent[node] : 0u;
-    const double sk = __shfl_xor(k, 1);
-    const bool left = (node & 1) == 0;
-    const unsigned long long CH = __ballot(valid && (left ? !(k > sk) : (sk > k)));
-    const unsigned long long LT = __ballot(valid && k < km);
-    unsigned long long PM = 0ull;
-    int p = tpp;
-    for (int dd = 1; dd <= 4; dd++) {
-      const int tpc = 2 * p;
-      if (tpc > n) {
-        done = true;
-        break;
-      }
-      const int lc = ((1 << dd) - 2) + (tpc - (b << dd));
-      const bool take_left = tpc == n || ((CH >> lc) & 1ull);
-      const int t = take_left ? tpc : tpc + 1, lt = take_left ? lc : lc + 1;
-      if (!((LT >> lt) & 1ull)) {
-        done = true;
-        break;
-      }
-      PM |= 1ull << lt;
-      p = t;
-      if (tpc == n) {
-        done = true;
-        break;
-      }
-    }
-    tpp = p;
-    b = p;
-    ck[ch] = k;
-    ce[ch] = e;
-    cn[ch] = node;
-    cm[ch] = ((PM >> lane) & 1ull) != 0ull;
-    dup = dup || __ballot(cm[ch] && (e & kDupF)) != 0ull;
-  }
-  if (dup) {
-    if (lane == 0) h.pop();
-    return;
-  }
-  if (lane == 0) {
-    const unsigned e0 = L->ent[1];
-    sset(L, (int)(e0 & kNodeM), kSKnown);
-    if (!(e0 & kDupF)) L->ht[(e0 >> 18) & (kHT - 1)] = kTomb;
-    h.ntr = n;
-  }
-#pragma unroll
-  for (int ch = 0; ch < 4; ch++) {
-    if (cm[ch]) {
-      const int pos = cn[ch] >> 1;
-      L->ent[pos] = ce[ch];
-      L->key[pos] = ck[ch];
-      L->ht[(ce[ch] >> 18) & (kHT - 1)] = kLive | ((unsigned)pos << 18) | (ce[ch] & kNodeM);
-    }
-  }
-  if (lane == 0) {
-    L->ent[tpp] = em;
-    L->key[tpp] = km;
-    L->ht[(em >> 18) & (kHT - 1)] = kLive | ((unsigned)tpp << 18) | (em & kNodeM);
-  }
-}
 
 // Rebuild the hash without its tombstones (wave 0, every lane): each heap entry's node is
 // re-inserted with the heap index of that entry (nodes with two entries: the index the old slot
@@ -541,8 +459,7 @@ AF_DEV long long walk(Lds* L, Heap& h, const DevModel& M, const XG& g, bool stag
     if (__ballot(edge) != 0ull) finished = true;
     const unsigned long long fm = __ballot(inb && st == kSFar);
     const long long tp0 = AF_XL_DIAG ? clock64() : 0;
-    if (AF_XL_POPWAVE) pop_wave(L, h, lane);
-    else if (lane == 0) h.pop();
+    if (lane == 0) h.pop();
     if (AF_XL_DIAG) dg[0] += clock64() - tp0;
     pops++;
     for (int k = 0; k < 4; k++) {
@@ -583,6 +500,146 @@ AF_DEV long long walk(Lds* L, Heap& h, const DevModel& M, const XG& g, bool stag
     }
   }
   return pops;
+}
+
+// ---- the walk over two wavefronts (AF_XL_TWO_ROLE) ----
+// The heap wavefront pops, classifies the popped node's neighbours (far -> addtree, close ->
+// updtree, read before downtree as in walk()), makes the node known and hands the relaxation jobs
+// to the relax wavefront, then runs downtree while the relaxations are evaluated, and each job's
+// addtree / updtree as soon as its value is posted.  The relax wavefront evaluates the jobs in
+// order (speculative entries / evaluation passes / fouds18_A(), walk()'s relax_value) and stores
+// T.  update() reads T and validity only, which neither downtree nor addtree / updtree change, so
+// the values are walk()'s.  fouds18_A() reads known-ness, which the heap side changes only through
+// a node with two heap entries (setpos makes it close again): while such entries are in the heap
+// (Heap::livedup) the heap runs downtree before posting the jobs and the relax side waits for the
+// earlier jobs' addtree / updtree before a fouds18_A() — the sequential order.
+AF_DEV void xpost(int* w, int v) { __hip_atomic_store(w, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP); }
+AF_DEV int xload(int* w) { return __hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP); }
+AF_DEV bool xawait_at_least(int* w, int v) {  // false: timeout (the other role is gone)
+  for (long spins = 0; xload(w) < v; spins++) {
+    __builtin_amdgcn_s_sleep(1);
+    if (spins > (1L << 28)) return false;
+  }
+  return true;
+}
+AF_DEV int xawait_change(int* w, int last) {  // the next value != last, or -2 on timeout
+  for (long spins = 0;; spins++) {
+    const int v = xload(w);
+    if (v != last) return v;
+    __builtin_amdgcn_s_sleep(1);
+    if (spins > (1L << 28)) return -2;
+  }
+}
+
+// heap wavefront (every lane; lane 0 holds the heap).  Returns the pops.
+AF_DEV long long heap_role(Lds* L, Heap& h, const XG& g, bool stage, int isx_s, int isz_s, int max_dist,
+                           double tstop, int lane) {
+  long long pops = 0;
+  bool finished = false;
+  int seq = 0, jobs = 0;
+  while (true) {
+    int go = 0, c = 0;
+    if (lane == 0) {
+      if (L->nused > (kHT * 3) / 4) go = -1;  // rehash first
+      else go = h.ntr > 0 && !finished && !h.err && !(tstop > 0 && L->key[1] >= tstop);
+      c = (int)(L->ent[1] & kNodeM);
+    }
+    go = __shfl(go, 0);
+    if (go < 0) {
+      rehash(L, h, lane);
+      continue;
+    }
+    if (!go) break;
+    c = __shfl(c, 0);
+    const int iz = g.gz(c), ix = g.gx(c);
+    if (!stage && ((g.wz0 > 0 && iz - g.wz0 < 3) || (g.wz0 + g.wh < g.nz && g.wz0 + g.wh - 1 - iz < 3) ||
+                   (g.wx0 > 0 && ix - g.wx0 < 3) || (g.wx0 + g.ww < g.nx && g.wx0 + g.ww - 1 - ix < 3)))
+      break;
+    const int kz = lane == 2 ? iz - 1 : lane == 3 ? iz + 1 : iz;
+    const int kx = lane == 0 ? ix - 1 : lane == 1 ? ix + 1 : ix;
+    const bool inb = lane < 4 && (lane < 2 ? (0 <= kx && kx <= g.nx - 1) : (0 <= kz && kz <= g.nz - 1));
+    const unsigned st = inb ? sget(L, g.loc(kz, kx)) : kSKnown;
+    const bool edge = lane < 4 && !inb && stage && (lane < 2 ? abs(isx_s - kx) : abs(isz_s - kz)) == max_dist + 1;
+    const unsigned long long jm = __ballot(inb && st != kSKnown);
+    if (__ballot(edge) != 0ull) finished = true;
+    const unsigned long long fm = __ballot(inb && st == kSFar);
+    const int n = __popcll(jm);
+    pops++;
+    if (lane == 0) {
+      h.pop_known();  // the popped node is known before any relaxation of this pop (fouds18_A)
+      const bool serial = h.livedup > 0;
+      if (serial || n == 0) h.pop_rest();
+      if (n > 0) {
+        int q = 0;
+        for (int k = 0; k < 4; k++) {
+          if (!((jm >> k) & 1ull)) continue;
+          const int rz = k == 2 ? iz - 1 : k == 3 ? iz + 1 : iz, rx = k == 0 ? ix - 1 : k == 1 ? ix + 1 : ix;
+          L->job[q++] = g.loc(rz, rx) | (((fm >> k) & 1ull) ? (int)0x80000000 : 0);
+        }
+        L->njob = n;
+        L->serial = serial ? 1 : 0;
+        L->ntr_hint = h.ntr;
+        xpost(&L->cmd, ++seq);
+        if (!serial) h.pop_rest();  // downtree beside the relaxations
+        for (int q2 = 0; q2 < n; q2++) {
+          if (!xawait_at_least(&L->done, jobs + q2 + 1)) {
+            h.err = 10;
+            break;
+          }
+          const int jw = L->job[q2];
+          const int r = jw & 0x7fffffff;
+          const double v = L->jval[q2];
+          if (jw < 0) h.add(r, v, true);
+          else if (h.upd(r, v)) h.sync(r, v);
+          xpost(&L->applied, jobs + q2 + 1);
+        }
+        jobs += n;
+      }
+    }
+  }
+  if (lane == 0) xpost(&L->cmd, -1);
+  return pops;
+}
+
+// relax wavefront (every lane)
+AF_DEV void relax_role(Lds* L, const DevModel& M, const XG& g, Spec& sp, int lane, long long* prof) {
+  long long nrel = 0, npass = 0;
+  int last = 0, jobs = 0;
+  sp.c = -1;
+  while (true) {
+    int cmd = 0;
+    if (lane == 0) cmd = xawait_change(&L->cmd, last);
+    cmd = __shfl(cmd, 0);
+    if (cmd < 0) break;  // stop (or timeout: the heap wavefront is gone)
+    last = cmd;
+    const int n = L->njob, serial = L->serial, ntr = L->ntr_hint;
+    const int4 jv = *reinterpret_cast<const int4*>(L->job);
+    for (int q = 0; q < n; q++) {
+      const int jw = q == 0 ? jv.x : q == 1 ? jv.y : q == 2 ? jv.z : jv.w;
+      const int r = jw & 0x7fffffff;
+      const int rz = g.gz(r), rx = g.gx(r);
+      int path = 0;
+      double v = relax_value(L, M, g, sp, r, rz, rx, ntr, lane, npass, path);
+      nrel++;
+      if (lane == 0) {
+        if (v == -1.0) {
+          if (serial) xawait_at_least(&L->applied, jobs + q);  // the earlier jobs' heap updates first
+          const XField F{L, &g};
+          v = fouds18(F, M, cell_mat(M, g.mv, rz, rx), rz, rx, g.dnx, g.dnz, g.nx, g.nz, mat_slo(M, g.mv, rz, rx));
+        }
+        gst(g.T + (long)rz * g.nx + rx, v);
+        L->jval[q] = v;
+        xpost(&L->done, jobs + q + 1);
+      }
+      v = rlane(v, 0);
+      patch(L, sp, rz, rx, v, lane);
+    }
+    jobs += n;
+  }
+  if (prof && lane == 0) {
+    prof[0] += nrel;
+    prof[1] += npass;
+  }
 }
 
 // all threads: the hand-over class of every 3rd node of the grid just walked (:2391-2425,
@@ -719,6 +776,7 @@ __global__ __launch_bounds__(kThreads) void fmm_exact_lds_kernel(BandParams P) {
     __syncthreads();
     h.ntr = 0;
     h.ndup = 0;
+    h.livedup = 0;
     if (stg == 0) {
       // straight rays (:2223-2267; veln + angle, SURVEY B-D5), material of the source's fine cell
       const int side1 = (9 - 1) / 2 + 9 * ((sg - 1) / 2);
@@ -752,7 +810,25 @@ __global__ __launch_bounds__(kThreads) void fmm_exact_lds_kernel(BandParams P) {
     } else if (w0) {
       handover(L, h, pT, pnz, pnx, pisz, pisx, g, isz_s, isx_s, lane);
     }
-    if (w0) {
+    if (AF_XL_TWO_ROLE) {
+      if (tid == 0) {
+        L->cmd = 0;
+        L->done = 0;
+        L->applied = 0;
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // wave 0's grid stores before wave 1 reads them
+      __syncthreads();
+      if (w0) {
+        const long long pops = heap_role(L, h, g, true, isx_s, isz_s, scale * size, 0.0, lane);
+        if (lane == 0) {
+          B->steps[stg] = pops;
+          if (h.err) err_s = h.err;
+        }
+      } else if (tid < 128) {
+        relax_role(L, M, g, sp, lane, B->sub);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if (w0) {
       sp.c = -1;
       const long long pops = walk(L, h, M, g, true, isx_s, isz_s, scale * size, 0.0, sp, lane, B->sub, B->ph);
       if (lane == 0) {
@@ -792,7 +868,29 @@ __global__ __launch_bounds__(kThreads) void fmm_exact_lds_kernel(BandParams P) {
     if (w0) {
       h.ntr = 0;
       h.ndup = 0;
+      h.livedup = 0;
       handover(L, h, pT, pnz, pnx, pisz, pisx, g, (int)isz, (int)isx, lane);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    if (AF_XL_TWO_ROLE) {
+      if (tid == 0) {
+        L->cmd = 0;
+        L->done = 0;
+        L->applied = 0;
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // wave 0's grid stores before wave 1 reads them
+      __syncthreads();
+      if (w0) {
+        const long long pops = heap_role(L, h, g, false, 0, 0, 0, P.tstop, lane);
+        if (lane == 0) {
+          B->steps[2] = pops;
+          if (h.err) err_s = h.err;
+        }
+      } else if (tid < 128) {
+        relax_role(L, M, g, sp, lane, B->sub);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if (w0) {
       sp.c = -1;
       const long long pops = walk(L, h, M, g, false, 0, 0, 0, P.tstop, sp, lane, B->sub, B->ph);
       if (lane == 0) {
