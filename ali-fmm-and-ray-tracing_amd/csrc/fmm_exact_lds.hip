@@ -533,8 +533,10 @@ AF_DEV int xawait_change(int* w, int last) {  // the next value != last, or -2 o
 
 // heap wavefront (every lane; lane 0 holds the heap).  Returns the pops.
 AF_DEV long long heap_role(Lds* L, Heap& h, const XG& g, bool stage, int isx_s, int isz_s, int max_dist,
-                           double tstop, int lane) {
+                           double tstop, int lane, long long* dgo) {
   long long pops = 0;
+  long long dg[4] = {0, 0, 0, 0};  // AF_XL_DIAG: waits for relaxations, downtree, addtree / updtree, the rest
+  long long tl = AF_XL_DIAG ? clock64() : 0;
   bool finished = false;
   int seq = 0, jobs = 0;
   while (true) {
@@ -580,36 +582,57 @@ AF_DEV long long heap_role(Lds* L, Heap& h, const XG& g, bool stage, int isx_s, 
         L->serial = serial ? 1 : 0;
         L->ntr_hint = h.ntr;
         xpost(&L->cmd, ++seq);
+        long long t1 = AF_XL_DIAG ? clock64() : 0;
+        if (AF_XL_DIAG) dg[3] += t1 - tl;
         if (!serial) h.pop_rest();  // downtree beside the relaxations
+        if (AF_XL_DIAG) {
+          const long long t2 = clock64();
+          dg[1] += t2 - t1;
+          t1 = t2;
+        }
         for (int q2 = 0; q2 < n; q2++) {
           if (!xawait_at_least(&L->done, jobs + q2 + 1)) {
             h.err = 10;
             break;
           }
+          long long t3 = AF_XL_DIAG ? clock64() : 0;
+          if (AF_XL_DIAG) dg[0] += t3 - t1;
           const int jw = L->job[q2];
           const int r = jw & 0x7fffffff;
           const double v = L->jval[q2];
           if (jw < 0) h.add(r, v, true);
           else if (h.upd(r, v)) h.sync(r, v);
           xpost(&L->applied, jobs + q2 + 1);
+          if (AF_XL_DIAG) {
+            t1 = clock64();
+            dg[2] += t1 - t3;
+          }
         }
+        if (AF_XL_DIAG) tl = t1;
         jobs += n;
       }
     }
   }
   if (lane == 0) xpost(&L->cmd, -1);
+  if (AF_XL_DIAG && lane == 0)
+    for (int k = 0; k < 4; k++) dgo[k] += dg[k];
   return pops;
 }
 
 // relax wavefront (every lane)
-AF_DEV void relax_role(Lds* L, const DevModel& M, const XG& g, Spec& sp, int lane, long long* prof) {
+AF_DEV void relax_role(Lds* L, const DevModel& M, const XG& g, Spec& sp, int lane, long long* prof,
+                       long long* dgo) {
   long long nrel = 0, npass = 0;
+  long long dg[2] = {0, 0};  // AF_XL_DIAG: waits for a command, the rest
   int last = 0, jobs = 0;
   sp.c = -1;
   while (true) {
     int cmd = 0;
+    const long long tw = AF_XL_DIAG ? clock64() : 0;
     if (lane == 0) cmd = xawait_change(&L->cmd, last);
     cmd = __shfl(cmd, 0);
+    const long long tw2 = AF_XL_DIAG ? clock64() : 0;
+    if (AF_XL_DIAG) dg[0] += tw2 - tw;
     if (cmd < 0) break;  // stop (or timeout: the heap wavefront is gone)
     last = cmd;
     const int n = L->njob, serial = L->serial, ntr = L->ntr_hint;
@@ -635,10 +658,15 @@ AF_DEV void relax_role(Lds* L, const DevModel& M, const XG& g, Spec& sp, int lan
       patch(L, sp, rz, rx, v, lane);
     }
     jobs += n;
+    if (AF_XL_DIAG) dg[1] += clock64() - tw2;
   }
   if (prof && lane == 0) {
     prof[0] += nrel;
     prof[1] += npass;
+  }
+  if (AF_XL_DIAG && lane == 0) {
+    dgo[4] += dg[0];
+    dgo[5] += dg[1];
   }
 }
 
@@ -819,13 +847,13 @@ __global__ __launch_bounds__(kThreads) void fmm_exact_lds_kernel(BandParams P) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // wave 0's grid stores before wave 1 reads them
       __syncthreads();
       if (w0) {
-        const long long pops = heap_role(L, h, g, true, isx_s, isz_s, scale * size, 0.0, lane);
+        const long long pops = heap_role(L, h, g, true, isx_s, isz_s, scale * size, 0.0, lane, B->ph);
         if (lane == 0) {
           B->steps[stg] = pops;
           if (h.err) err_s = h.err;
         }
       } else if (tid < 128) {
-        relax_role(L, M, g, sp, lane, B->sub);
+        relax_role(L, M, g, sp, lane, B->sub, B->ph);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else if (w0) {
@@ -881,13 +909,13 @@ __global__ __launch_bounds__(kThreads) void fmm_exact_lds_kernel(BandParams P) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // wave 0's grid stores before wave 1 reads them
       __syncthreads();
       if (w0) {
-        const long long pops = heap_role(L, h, g, false, 0, 0, 0, P.tstop, lane);
+        const long long pops = heap_role(L, h, g, false, 0, 0, 0, P.tstop, lane, B->ph);
         if (lane == 0) {
           B->steps[2] = pops;
           if (h.err) err_s = h.err;
         }
       } else if (tid < 128) {
-        relax_role(L, M, g, sp, lane, B->sub);
+        relax_role(L, M, g, sp, lane, B->sub, B->ph);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else if (w0) {

@@ -263,10 +263,6 @@ AF_DEV int job_z(int j) { return (j >> 8) & 255; }
 AF_DEV int job_x(int j) { return j & 255; }
 AF_DEV int job_kind(int j) { return j >> 16; }
 AF_DEV int job_pack(int z, int x, int kind) { return (z << 8) | x | (kind << 16); }
-// the relax wavefront verifies the predicted next pop's jobs while the heap wavefront sifts (1)
-#ifndef AF_INIT_PREDICT
-#define AF_INIT_PREDICT 1
-#endif
 AF_DEV void post(int* w, int v) { __hip_atomic_store(w, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP); }
 // the waiting role backs off between polls (s_sleep) so that it does not take issue slots and
 // LDS cycles from the working one
@@ -327,17 +323,6 @@ AF_DEV bool pop_two_role(Heap& h, int& seq, int& jobs, int n) {
   return true;
 }
 
-// The relax role (wavefront 1).  A pop's neighbours are relaxed in order, each seeing the earlier
-// ones' new values (the reference's sequence).  Relaxations are evaluated ahead of their turn, 64 at
-// a time: when a job has no usable speculative value, the whole wavefront runs one pass in which
-// lane 0 evaluates that job and every other lane a neighbour of one of the heap's first 16 entries
-// (the next pops), against the current state; each lane keeps its result in registers.  A job whose
-// node has an entry only re-runs update()'s cheap stencil stage on the state of its turn: equal
-// to the entry's (same stencil, same input values), the entry's value is the job's value —
-// update()'s value is a function of its stencil stage's outputs — so the results are the
-// sequential ones bit for bit, and most jobs skip the expensive finish (wavefront angle, phase
-// velocity).  fouds18_A() (no usable stencil) always runs in turn.  The heap may be mid-sift
-// while the lanes read it: any node read there is only a guess, never trusted.
 struct RelaxWin {
   int z0, x0, z1, x1, w;  // LDS window: rows z0..z1, columns x0..x1 (stage grids: the whole grid)
   int oz, ox;             // job coordinates (LDS-local) + (oz, ox) = operator coordinates
@@ -355,135 +340,68 @@ AF_DEV double readlane_d(double v, int l) {
   return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
+// The relax role (wavefront 1).  A pop's neighbours are relaxed in order, each seeing the earlier
+// ones' new values (the reference's sequence).  Relaxations are evaluated ahead of their turn, 64 at
+// a time: when a job has no speculative entry, the whole wavefront runs one pass in which lane 0
+// evaluates that job and every other lane a neighbour of one of the heap's first 16 entries (the
+// next pops), against the current state; each lane keeps its result (node, value, update()'s
+// stencil stage, the bounds mode it ran with) in registers, and a dirty flag that every committed
+// relaxation sets when its node lies in the entry's 12-point stencil (only relaxations change T
+// and validity: pops and sift-ups do not).  A job whose node has a clean entry takes the entry's
+// value as it is; a dirty entry re-runs the cheap stencil stage on the state of its turn — equal
+// to the entry's, the entry's value is the job's value (update()'s value is a function of its
+// stencil stage's outputs), else the finish runs on that lane — so the results are the sequential
+// ones bit for bit.  fouds18_A() (no usable stencil) always runs in turn.  The heap may be
+// mid-sift while the lanes read it: any node read there is only a guess, never trusted.  (Round 3's
+// relax role also predicted the next pop and verified its jobs ahead: the same speed, more code.)
 template <bool LDSMAT>
 AF_DEV void relax_role(InitLds* L, const DevModel& M, const MatView& mv, const MidWin& mw, const RelaxWin& R,
-                       int lane) {
+                          int lane) {
   int last = 0;
   long long busy = 0, njobs = 0, nf18 = 0, nburst = 0;
-  const int wz = R.z1 - R.z0, wx = R.x1 - R.x0;  // local coordinate bounds (0..wz, 0..wx)
-  // this lane's speculative relaxation, kept in registers: node (LDS-local z << 8 | x; -1: none),
-  // value, and update()'s stencil stage on the state it saw
-  int my_cell = -1;
+  const int wz = R.z1 - R.z0, wx = R.x1 - R.x0;
+  int my_cell = -1, my_nnz = 0;
+  bool my_dirty = true;
   double my_val = 0.0;
   UpdSel my_sel{};
-  // Verification of jobs k0.. of the job list jw (n jobs): the entries of the jobs (one ballot
-  // each: the lowest lane holding the job's node) and their values (src / sv); then the lane
-  // holding job k's entry re-runs its stencil stage on the current state with jobs k0..k-1 set to
-  // their entries' values.  Returns the number of leading confirmed jobs.
-  auto verify = [&](const int4& jw, int n, int k0, int (&src)[4], double (&sv)[4]) -> int {
-    auto job = [&](int i) { return i == 0 ? jw.x : i == 1 ? jw.y : i == 2 ? jw.z : jw.w; };
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      src[k] = -1;
-      sv[k] = -1.0;
-      if (k0 + k < n) {
-        const unsigned long long hm = __ballot(my_cell == (job(k0 + k) & 0xffff));
-        if (hm) {
-          src[k] = __ffsll((long long)hm) - 1;
-          sv[k] = readlane_d(my_val, src[k]);
-        }
-      }
-    }
-    bool ok = false;
-    {
-      int q = -1;  // the job whose entry this lane holds
-#pragma unroll
-      for (int k = 0; k < 4; k++) q = src[k] == lane ? k : q;
-      bool prior = true;  // every job k0..k0+q-1 has an entry with a usable value
-#pragma unroll
-      for (int u = 0; u < 4; u++) prior = prior && (u >= q || (src[u] >= 0 && sv[u] != -1.0));
-      if (q >= 0 && prior && my_val != -1.0) {
-        const int jq = job(k0 + q);
-        const int lz = job_z(jq), lx = job_x(jq);
-        const int iz = lz + R.oz, ix = lx + R.ox;
-        NbFieldT nb;
-        nb.load_lds(L->T, L->S, R.z0, R.x0, R.z1, R.x1, R.w, iz, ix);
-#pragma unroll
-        for (int u = 0; u < 3; u++)
-          if (u < q) nb.patch(job_z(job(k0 + u)) - lz, job_x(job(k0 + u)) - lx, sv[u]);
-        ok = update_nb_select(nb, iz, ix, (job_kind(jq) & kJobQuirk) ? R.quirk_nnz : R.nnz, R.nnx).same(my_sel);
-      }
-    }
-    const unsigned long long okm = __ballot(ok);
-    int hk = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++)
-      if (hk == k && k0 + k < n && src[k] >= 0 && ((okm >> src[k]) & 1ull)) hk = k + 1;
-    return hk;
-  };
-  // the next pop's job list as predicted after the last pop (wave-uniform; pred_n -1: none), and
-  // its verification done ahead, while the heap wavefront sifts and classifies
-  int pred_n = -1, pred_hk = 0;
-  int4 pred_jv = make_int4(0, 0, 0, 0);
-  int pred_src[4] = {-1, -1, -1, -1};
-  double pred_sv[4] = {-1.0, -1.0, -1.0, -1.0};
   while (true) {
     int cmd = 0;
     AF_DG_T0(tcw)
     if (lane == 0) cmd = await_change(&L->cmd, last);
     if (lane == 0) { AF_DG_ADD(L, 4, tcw) }
     cmd = __shfl(cmd, 0);
-    if (cmd < 0) break;  // stop (or timeout: the heap role is gone)
+    if (cmd < 0) break;
     last = cmd;
     const long long t0 = wall_clock64();
-    AF_DG_T0(tjl)
-    // the pop's jobs (read once: the heap role refills them after the last one is done), in
-    // wave-uniform registers; job(i) selects without dynamic indexing
     const int nj = L->njob;
     const int4 jv = *reinterpret_cast<const int4*>(L->job);
-    auto job = [&](int i) { return i == 0 ? jv.x : i == 1 ? jv.y : i == 2 ? jv.z : jv.w; };
-    // the prediction holds when the job lists are equal: the verification read the same state
-    // (only relaxations write T; sift-ups and pops change no node's validity)
-    const bool hit = pred_n == nj && nj > 0 && pred_jv.x == jv.x && (nj < 2 || pred_jv.y == jv.y) &&
-                     (nj < 3 || pred_jv.z == jv.z) && (nj < 4 || pred_jv.w == jv.w);
-    double jval[4] = {0.0, 0.0, 0.0, 0.0};  // the values this pop's jobs receive (next prediction)
-    int k0 = 0;
-    while (k0 < nj) {
+    for (int k = 0; k < nj; k++) {
       AF_DG_T0(tv)
-      int src[4];
-      double sv[4];
-      int hk;
-      if (hit && k0 == 0) {
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          src[k] = pred_src[k];
-          sv[k] = pred_sv[k];
-        }
-        hk = pred_hk;
-#if AF_INIT_DIAG
-        if (lane == 0) L->dg[7]++;
-#endif
-      } else {
-        hk = verify(jv, nj, k0, src, sv);
-      }
-      if (lane == 0 && hk > 0) {
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-          if (u < hk) {
-            const int ju = job(k0 + u);
-            L->T[job_z(ju) * R.w + job_x(ju)] = sv[u];
-            if (job_kind(ju) & kJobAdd) L->S[job_z(ju) * R.w + job_x(ju)] = 1;  // valid for the next relaxations
-          }
-        }
-        post(&L->done, (int)(njobs + hk));
-      }
-#pragma unroll
-      for (int i = 0; i < 4; i++)
-#pragma unroll
-        for (int u = 0; u < 4; u++)
-          if (u < hk && i == k0 + u) jval[i] = sv[u];
-      njobs += hk;
-      k0 += hk;
-      if (lane == 0) { AF_DG_ADD(L, 5, tv) }
-      if (k0 >= nj) break;
-      AF_DG_T0(tf)
-      // job k0 in turn: one pass, this job on lane 0, guesses of the next pops' jobs on the others
-      const int jk = job(k0);
+      const int jk = k == 0 ? jv.x : k == 1 ? jv.y : k == 2 ? jv.z : jv.w;
       const int lz = job_z(jk), lx = job_x(jk), kind = job_kind(jk);
       const int iz = lz + R.oz, ix = lx + R.ox;
-      double v = 0.0;
-      {
-        int cz = lz, cx = lx, cnnz = (kind & kJobQuirk) ? R.quirk_nnz : R.nnz;
+      const int qnnz = (kind & kJobQuirk) ? R.quirk_nnz : R.nnz;
+      const unsigned long long hm = __ballot(my_cell == (jk & 0xffff));
+      double v;
+      if (hm) {
+        const int e = __ffsll((long long)hm) - 1;
+        if (lane == e && (my_dirty || my_nnz != qnnz)) {
+          NbFieldT nb;
+          nb.load_lds(L->T, L->S, R.z0, R.x0, R.z1, R.x1, R.w, iz, ix);
+          const UpdSel s2 = update_nb_select(nb, iz, ix, qnnz, R.nnx);
+          if (!s2.same(my_sel)) {
+            const double* pre;
+            const CellMat cm = init_mat<LDSMAT>(M, L, mv, mw, iz, ix, &pre);
+            my_val = update_nb_finish(M, cm, iz, ix, R.dnx, s2);
+            my_sel = s2;
+          }
+          my_dirty = false;
+          my_nnz = qnnz;
+        }
+        v = readlane_d(my_val, e);
+        if (lane == 0) { AF_DG_ADD(L, 5, tv) }
+      } else {  // one pass: this job on lane 0, guesses of the next pops' jobs on the others
+        int cz = lz, cx = lx, cnnz = qnnz;
         bool cand = true;
         if (lane > 0) {
           const int p = 1 + ((lane - 1) >> 2), d = (lane - 1) & 3;
@@ -504,11 +422,14 @@ AF_DEV void relax_role(InitLds* L, const DevModel& M, const MatView& mv, const M
           my_sel = update_nb_select(nb, gz, gx, cnnz, R.nnx);
           my_val = update_nb_finish(M, cm, gz, gx, R.dnx, my_sel);
           my_cell = (cz << 8) | cx;
-          if (lane == 0) v = my_val;
+          my_dirty = false;
+          my_nnz = cnnz;
         } else {
           my_cell = -1;
         }
         nburst++;
+        v = readlane_d(my_val, 0);
+        if (lane == 0) { AF_DG_ADD(L, 6, tv) }
       }
       if (lane == 0) {
         if (v == -1.0) {
@@ -521,64 +442,13 @@ AF_DEV void relax_role(InitLds* L, const DevModel& M, const MatView& mv, const M
         L->T[lz * R.w + lx] = v;
         if (kind & kJobAdd) L->S[lz * R.w + lx] = 1;  // valid for the next relaxations (addtree sets the index)
         post(&L->done, (int)(njobs + 1));
-        AF_DG_ADD(L, 6, tf)
       }
-      {
-        const double vj = readlane_d(v, 0);
-#pragma unroll
-        for (int i = 0; i < 4; i++)
-          if (i == k0) jval[i] = vj;
+      if (my_cell >= 0) {  // the committed node changes the stencils that hold it
+        const int dz = lz - (my_cell >> 8), dx = lx - (my_cell & 255), ad = abs(dz) + abs(dx);
+        if (ad >= 1 && ad <= 2 && !(dz != 0 && dx != 0 && (abs(dz) != 1 || abs(dx) != 1))) my_dirty = true;
       }
       njobs++;
-      k0++;
     }
-    // Predict the next pop — the heap's root after downtree (read while the heap wavefront may still
-    // be sifting: a guess) or, when smaller, this pop's smallest new value — classify its
-    // neighbours as the heap wavefront will (x-1, x+1, z-1, z+1; far -> add, close -> update, the
-    // stage-1 quirk on x-neighbour updates), and verify those jobs now.  Only an identical job list
-    // at the next command uses the result.
-    if (lane == 0) { AF_DG_ADD(L, 11, tjl) }
-    AF_DG_T0(tpb)
-    pred_n = -1;
-#if AF_INIT_PREDICT
-    if (nj > 0) {
-      int pc = __builtin_amdgcn_readfirstlane((int)L->hcell[1]);
-      double pk = readlane_d(L->hkey[1], 0);
-#pragma unroll
-      for (int k = 0; k < 4; k++)
-        if (k < nj && jval[k] < pk) {
-          pk = jval[k];
-          pc = job(k) & 0xffff;
-        }
-      const int pz = pc >> 8, px = pc & 255;
-      int o[4] = {0, 0, 0, 0}, pn = 0;
-#pragma unroll
-      for (int d = 0; d < 4; d++) {
-        const int zz = pz + (d == 2 ? -1 : d == 3 ? 1 : 0), xx = px + (d == 0 ? -1 : d == 1 ? 1 : 0);
-        const int gz = zz + R.oz, gx = xx + R.ox;
-        const bool inb = d < 2 ? (gx >= 0 && gx <= R.nnx - 1) : (gz >= 0 && gz <= R.nnz - 1);
-        if (inb && zz >= 0 && zz <= wz && xx >= 0 && xx <= wx) {
-          const int st = __builtin_amdgcn_readfirstlane((int)L->S[zz * R.w + xx]);
-          if (st == -1 || st > 0) {
-            const int kind = st == -1 ? kJobAdd : (kJobUpd | (d < 2 && R.has_quirk ? kJobQuirk : 0));
-            const int jp = job_pack(zz, xx, kind);
-#pragma unroll
-            for (int s2 = 0; s2 < 4; s2++)
-              if (s2 == pn) o[s2] = jp;
-            pn++;
-          }
-        }
-      }
-      if (pn > 0) {
-        pred_jv = make_int4(o[0], o[1], o[2], o[3]);
-        AF_DG_T0(tpv)
-        pred_hk = verify(pred_jv, pn, 0, pred_src, pred_sv);
-        if (lane == 0) { AF_DG_ADD(L, 9, tpv) }
-        pred_n = pn;
-      }
-    }
-#endif
-    if (lane == 0) { AF_DG_ADD(L, 8, tpb) }
     busy += wall_clock64() - t0;
   }
   if (lane == 0) {

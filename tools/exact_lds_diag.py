@@ -24,11 +24,13 @@ init_ms = ctx.last_timing()[0]
 bp = ctx.band_profile(0).astype(float)
 steps = ctx.source_stats(0)[0]
 pops = float(steps[0] + steps[1] + steps[2])
-names = ["pop", "entry_clean", "entry_same_stage", "entry_finish", "eval_pass", "commit"]
-out = {"fields": len(rx), "subgrid": 9, "init_ms": init_ms, "pops_src0": pops,
-       "relaxations_src0": bp[10], "passes_src0": bp[11], "same_stage_src0": bp[12], "finishes_src0": bp[13],
-       "cycles_per_pop": {n: round(bp[k] / pops, 1) for k, n in enumerate(names)},
-       "cycles_per_event": {"entry_same_stage": round(bp[2] / max(bp[12], 1), 1),
-                            "entry_finish": round(bp[3] / max(bp[13], 1), 1),
-                            "eval_pass": round(bp[4] / max(bp[11], 1), 1)}}
+two_role = ctx.get_option("exact_lds") == 1 and os.environ.get("AF_XL_ONE_WAVE") is None
+if two_role:  # heap_role / relax_role timers (the default build: AF_XL_TWO_ROLE)
+    names = ["heap_wait_relax", "heap_downtree", "heap_add_upd", "heap_classify_rest", "relax_wait_cmd",
+             "relax_work"]
+else:
+    names = ["pop", "entry_clean", "entry_same_stage", "entry_finish", "eval_pass", "commit"]
+out = {"fields": len(rx), "subgrid": 9, "init_ms": init_ms, "pops_src0": pops, "two_role": two_role,
+       "relaxations_src0": bp[10], "passes_src0": bp[11],
+       "cycles_per_pop": {n: round(bp[k] / pops, 1) for k, n in enumerate(names)}}
 print(json.dumps(out))

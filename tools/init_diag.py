@@ -24,11 +24,8 @@ ti, tb, _ = ctx.last_timing()
 P = np.array([ctx.init_profile(i) for i in range(ns)], dtype=np.float64)
 m = P.mean(axis=0)
 pops = float(m[4:8].sum())
-names = ["heap_wait_relax", "heap_down", "heap_addupd", "heap_classify", "relax_wait_pop", "relax_verify",
-         "relax_eval", "pred_hits"]
-# the diagnostic build puts the relax role's prediction timers where the stage ticks were (prof[0..3])
-names2 = ["relax_predict_block", "relax_predict_verify", "-", "relax_job_loop"]
+names = ["heap_wait_relax", "heap_down", "heap_addupd", "heap_classify", "relax_wait_pop", "relax_entry",
+         "relax_pass", "-"]
 out = {"sources": ns, "init_ms": ti, "pops": pops, "walk_us_per_pop": ti * 1e3 / pops,
-       "cycles_per_pop": {n: round(m[8 + k] / pops, 1) for k, n in enumerate(names)}}
-out["cycles_per_pop"].update({n: round(m[k] / pops, 1) for k, n in enumerate(names2) if n != "-"})
+       "cycles_per_pop": {n: round(m[8 + k] / pops, 1) for k, n in enumerate(names) if n != "-"}}
 print(json.dumps(out))
