@@ -474,16 +474,21 @@ class ALI_FMM:
                     return
                 x = np.array([float(self.scx[i]) for i in ids])
                 z = np.array([float(self.scz[i]) for i in ids])
-                ctx.travel(x, z, subgrid=int(subgrid_size), first_slot=0, copy_out=False)
+                into = copy_out and dest is not None  # straight into the caller's rows, streamed
+
+                def run():
+                    if into:
+                        ctx.travel_into(x, z, dest, ids, subgrid=int(subgrid_size), first_slot=0)
+                    else:
+                        ctx.travel(x, z, subgrid=int(subgrid_size), first_slot=0, copy_out=False)
+
+                run()
                 if speculative and ctx.model_key != key():  # computed on a stale model: redo
                     _load_model(ctx, *mtab, self.dnx, self.dnz, self.gox, self.goz, key=key())
-                    ctx.travel(x, z, subgrid=int(subgrid_size), first_slot=0, copy_out=False)
+                    run()
                 out = None
-                if copy_out:
-                    if dest is not None:
-                        ctx.copy_fields_into(0, dest, ids, int(subgrid_size))
-                    else:
-                        out = ctx.copy_fields(0, len(ids), int(subgrid_size))[0]
+                if copy_out and not into:
+                    out = ctx.copy_fields(0, len(ids), int(subgrid_size))[0]
                     # the device slots stay allocated for the next call (a hipMalloc / hipFree of
                     # every 134 MB field per call cost more than the copy's overlap gains); they are
                     # reused in place, reallocated only for a larger grid, freed with the context

@@ -68,6 +68,7 @@ def _load():
             "alifmm_get_option": (_i, [_p, ctypes.c_char_p, _p]),
             "alifmm_field_shape": (_i, [_p, _i, _p, _p]),
             "alifmm_travel": (_i, [_p, _i, _i, _p, _p, _i, _p]),
+            "alifmm_travel_into": (_i, [_p, _i, _i, _p, _p, _i, _p]),
             "alifmm_get_field": (_i, [_p, _i, _p]),
             "alifmm_release_fields": (_i, [_p]),
             "alifmm_copy_fields": (_i, [_p, _i, _i, _p, _i, _p]),
@@ -262,6 +263,27 @@ class Context:
         self._chk(lib().alifmm_travel(self._h, int(subgrid), len(scx), _ptr(scx), _ptr(scz), int(first_slot),
                                       _ptr(out)), "travel")
         return out
+
+    def travel_into(self, scx, scz, dest, rows, subgrid=1, first_slot=0):
+        """travel() with field i written to dest[rows[i]] of a caller-visible C-contiguous float64
+        (n, fnz, fnx) stack (alifmm_travel_into: at subgrid 1 the fields stream out of the band
+        kernel tile by tile while it runs).  The fields also stay resident in slots first_slot.. ."""
+        scx = _c64(np.atleast_1d(scx))
+        scz = _c64(np.atleast_1d(scz))
+        if not (isinstance(dest, np.ndarray) and dest.dtype == np.float64 and dest.flags.c_contiguous
+                and dest.ndim == 3):
+            raise ValueError("dest must be a C-contiguous float64 (n, fnz, fnx) array")
+        if dest.shape[1:] != self.field_shape(subgrid):
+            raise ValueError("dest fields %s, travel fields %s" % (dest.shape[1:], self.field_shape(subgrid)))
+        rows = [int(r) for r in rows]
+        if len(rows) != len(scx):
+            raise ValueError("one dest row per source")
+        if rows and (min(rows) < 0 or max(rows) >= dest.shape[0]):
+            raise IndexError("travel_into: row outside dest")
+        base, step = dest.ctypes.data, dest[0].nbytes if dest.shape[0] else 0
+        ptrs = (ctypes.c_void_p * max(1, len(rows)))(*[base + r * step for r in rows])
+        self._chk(lib().alifmm_travel_into(self._h, int(subgrid), len(scx), _ptr(scx), _ptr(scz), int(first_slot),
+                                           ptrs), "travel_into")
 
     def get_field(self, slot, subgrid):
         fz, fx = self.field_shape(subgrid)

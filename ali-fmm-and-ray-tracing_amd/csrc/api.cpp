@@ -16,8 +16,10 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdlib>
+#include <functional>
 #include <mutex>
 #include <map>
+#include <memory>
 #include <string>
 #include <thread>
 #include <vector>
@@ -136,6 +138,8 @@ static void free_model(alifmm_ctx* c) {
   c->have_model = false;
 }
 
+static void free_stream_bufs(alifmm_ctx* ctx);
+
 int alifmm_release_fields(alifmm_ctx* ctx) {
   if (!ctx) return ALIFMM_E_ARG;
   (void)hipSetDevice(ctx->device);
@@ -143,6 +147,7 @@ int alifmm_release_fields(alifmm_ctx* ctx) {
   ctx->fields.clear();
   free_ray_bufs(ctx);  // the ray tracer's point buffers (chunk x max_pts per coordinate) go with the fields
   release_kept_rays(ctx);
+  free_stream_bufs(ctx);  // the pinned staging of streamed fields too
   return ALIFMM_OK;
 }
 
@@ -190,6 +195,7 @@ int alifmm_set_option(alifmm_ctx* ctx, const char* name, double value) {
   else if (!strcmp(name, "coop")) ctx->coop = value != 0;
   else if (!strcmp(name, "exact_r") && value >= 0 && value <= 48) ctx->exact_r = (int)value;
   else if (!strcmp(name, "exact_lds")) ctx->exact_lds = value != 0;
+  else if (!strcmp(name, "stream_out")) ctx->stream_out = value != 0;
   else if (!strcmp(name, "members") && value >= 0 && value <= af::kMaxK && value == (int)value)
     ctx->members = (int)value;
   else if (!strcmp(name, "stripe_log") && (value == 0 || (value >= 3 && value <= 12))) ctx->stripe_log = (int)value;
@@ -206,6 +212,9 @@ int alifmm_get_option(alifmm_ctx* ctx, const char* name, double* value) {
   else if (!strcmp(name, "batch")) *value = ctx->batch;
   else if (!strcmp(name, "exact_r")) *value = ctx->exact_r;
   else if (!strcmp(name, "exact_lds")) *value = ctx->exact_lds;
+  else if (!strcmp(name, "stream_out")) *value = ctx->stream_out;
+  else if (!strcmp(name, "stream_tail_ms")) *value = ctx->t_stream_tail;      // last travel with a host destination
+  else if (!strcmp(name, "stream_fallback")) *value = (double)ctx->stream_fallback;
   else if (!strcmp(name, "prof")) *value = ctx->prof;
   else if (!strcmp(name, "coop")) *value = ctx->coop;
   else if (!strcmp(name, "members")) *value = ctx->members;
@@ -508,13 +517,29 @@ static int launch_source_init(alifmm_ctx* ctx, int n, const double* scx, const d
   return ALIFMM_OK;
 }
 
+// alifmm_travel_into / alifmm_travel with a host destination: the caller's field of each source of
+// a chunk, and the state of streaming them out of the band kernel (subgrid 1)
+struct StreamOut {
+  double* const* dst = nullptr;  // per source of the chunk
+  int n = 0;
+  bool active = false;  // the band launch streams (stream_setup)
+  int K = 0, wlog = 0, trlog = 0, nstr = 0, ntz = 0, nz = 0, nx = 0, qcap = 0;
+  std::atomic<int> kernel_done{0};
+  std::unique_ptr<std::atomic<int>[]> missing;  // per source: a tile never arrived (copied after)
+  std::chrono::steady_clock::time_point t_done;
+};
+static int stream_setup(alifmm_ctx* ctx, StreamOut* so, int n, int K, int wlog, int fz, int fx);
+static void stream_start(alifmm_ctx* ctx, StreamOut* so);
+static void stream_finish(alifmm_ctx* ctx, StreamOut* so);
+
 // travel_chunk: a plain band launch whose members were not all resident (another process held CUs);
 // alifmm_travel re-runs the chunk once with a cooperative launch
 static const int kRetryCoop = -100;
 
 // one chunk of sources; returns ALIFMM_E_CAPACITY when a work list overflowed
 static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const double* scz, int first_slot, int fz,
-                        int fx, float* ms_init, float* ms_band, const af::HandoverOut* pre_ho = nullptr) {
+                        int fx, float* ms_init, float* ms_band, const af::HandoverOut* pre_ho = nullptr,
+                        StreamOut* so = nullptr) {
   const long cells = (long)fz * fx;
   long capL = std::min(cells, std::max(65536L, cells / 8) * ctx->cap_scale);
   long capC = capL;
@@ -629,6 +654,16 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
   P.tb_cells = tb_cells;
   P.sb_pitch = af_band_sb_pitch(fx);
   P.max_steps = 200L * (fz + fx) + 100000;
+  if (so) {  // stream the fields to the host while the band runs (subgrid 1)
+    so->active = false;
+    if (sg == 1 && ctx->stream_out && (rc = stream_setup(ctx, so, n, K, wlog, fz, fx))) return rc;
+    if (so->active) {
+      P.hs = static_cast<double*>(ctx->hstage);
+      P.hq = ctx->hq;
+      P.qcap = so->qcap;
+      P.tr_log = so->trlog;
+    }
+  }
   HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
   if (sg == 1) {
     if (pre_ho) {  // initialised by the travel call for all its chunks (alifmm_travel)
@@ -684,12 +719,28 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
   if (fs != ctx->stream) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_fill, 0));
   HIPCHK(hipMemsetAsync(a.kx, 0, sizeof(af::KX) * n, ctx->stream));
   HIPCHK(af_launch_band_k(&P, ctx->stream));
+  // the copy team takes the tiles as they arrive; joined on every return path below
+  struct StreamJoin {
+    alifmm_ctx* c;
+    StreamOut* s;
+    ~StreamJoin() {
+      if (s) stream_finish(c, s);
+    }
+  } sjoin{ctx, nullptr};
+  if (so && so->active) {
+    stream_start(ctx, so);
+    sjoin.s = so;
+  }
   ctx->last_k = K;
   HIPCHK(hipEventRecord(ctx->ev[2], ctx->stream));
   if (sg > 1)
     for (int i = 0; i < n; i++) HIPCHK(af_launch_scale(hs[i].T, cells, (double)sg, ctx->stream));
   HIPCHK(hipMemcpyAsync(hs.data(), a.srcs, sizeof(af::BandSrc) * n, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
+  if (sjoin.s) {
+    stream_finish(ctx, so);
+    sjoin.s = nullptr;
+  }
   float t1 = 0, t2 = 0;
   (void)hipEventElapsedTime(&t1, ctx->ev[0], ctx->ev[1]);
   (void)hipEventElapsedTime(&t2, ctx->ev[1], ctx->ev[2]);
@@ -716,8 +767,9 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
   return ALIFMM_OK;
 }
 
-int alifmm_travel(alifmm_ctx* ctx, int subgrid, int nsrc, const double* scx, const double* scz, int first_slot,
-                  double* out) {
+// dsts: per source, the caller's (pageable) field, or null (the fields stay resident only)
+static int travel_impl(alifmm_ctx* ctx, int subgrid, int nsrc, const double* scx, const double* scz, int first_slot,
+                       double* const* dsts) {
   if (!ctx || !ctx->have_model) return fail(ctx, ALIFMM_E_ARG, "travel: no model");
   if ((long)subgrid * (ctx->nz0 - 1) + 1 >= 32768 || (long)subgrid * (ctx->nx0 - 1) + 1 >= 32768)
     return fail(ctx, ALIFMM_E_ARG, "travel: field sides must stay below 32768 nodes (packed list keys)");
@@ -753,6 +805,8 @@ int alifmm_travel(alifmm_ctx* ctx, int subgrid, int nsrc, const double* scx, con
     HIPCHK(dalloc(&ctx->jobs_all, nsrc));
     ctx->n_all = nsrc;
   }
+  ctx->t_stream_tail = 0;
+  ctx->stream_fallback = 0;
   HIPCHK(hipEventRecord(ctx->ev[3], ctx->stream));
   // the call's timing events, destroyed on every return path
   struct Ev {
@@ -781,14 +835,18 @@ int alifmm_travel(alifmm_ctx* ctx, int subgrid, int nsrc, const double* scx, con
   for (int s0 = 0; s0 < nsrc; s0 += chunk) {
     int n = std::min(chunk, nsrc - s0);
     int rc;
+    StreamOut so;
+    so.dst = dsts ? dsts + s0 : nullptr;
+    so.n = n;
+    StreamOut* sop = dsts ? &so : nullptr;
     for (;;) {
       rc = travel_chunk(ctx, subgrid, n, scx + s0, scz + s0, first_slot + s0, fz, fx, &ms_init, &ms_band,
-                        pre ? pre + s0 : nullptr);
+                        pre ? pre + s0 : nullptr, sop);
       if (rc == kRetryCoop) {  // once, gang-scheduled
         const int c0 = ctx->coop;
         ctx->coop = 1;
         rc = travel_chunk(ctx, subgrid, n, scx + s0, scz + s0, first_slot + s0, fz, fx, &ms_init, &ms_band,
-                          pre ? pre + s0 : nullptr);
+                          pre ? pre + s0 : nullptr, sop);
         ctx->coop = c0;
         if (rc == kRetryCoop) rc = ALIFMM_E_KERNEL;
       }
@@ -796,9 +854,13 @@ int alifmm_travel(alifmm_ctx* ctx, int subgrid, int nsrc, const double* scx, con
       ctx->cap_scale *= 4;  // retry the chunk with larger work lists
     }
     if (rc) return rc;
-    if (out) {  // pageable host destination: through the pinned staging ring
-      rc = alifmm_copy_fields(ctx, first_slot + s0, n, out + (size_t)s0 * cells, 0, nullptr);
-      if (rc) return rc;
+    if (dsts) {  // fields not streamed (or a tile that never arrived): through the pinned staging ring
+      for (int i = 0; i < n; i++) {
+        if (so.active && !so.missing[i].load()) continue;
+        if (so.active) ctx->stream_fallback++;
+        rc = alifmm_copy_fields(ctx, first_slot + s0 + i, 1, dsts[s0 + i], 0, nullptr);
+        if (rc) return rc;
+      }
     }
   }
   HIPCHK(hipEventRecord(t_end.e, ctx->stream));
@@ -809,6 +871,24 @@ int alifmm_travel(alifmm_ctx* ctx, int subgrid, int nsrc, const double* scx, con
   ctx->t_band = ms_band;
   ctx->t_total = tot;
   return ALIFMM_OK;
+}
+
+int alifmm_travel(alifmm_ctx* ctx, int subgrid, int nsrc, const double* scx, const double* scz, int first_slot,
+                  double* out) {
+  if (!out) return travel_impl(ctx, subgrid, nsrc, scx, scz, first_slot, nullptr);
+  int fz = 0, fx = 0;
+  if (ctx && ctx->have_model) alifmm_field_shape(ctx, subgrid, &fz, &fx);
+  std::vector<double*> d(std::max(nsrc, 0));
+  for (int i = 0; i < nsrc; i++) d[i] = out + (size_t)i * fz * fx;
+  return travel_impl(ctx, subgrid, nsrc, scx, scz, first_slot, d.data());
+}
+
+int alifmm_travel_into(alifmm_ctx* ctx, int subgrid, int nsrc, const double* scx, const double* scz, int first_slot,
+                       double* const* dst) {
+  if (nsrc > 0 && !dst) return fail(ctx, ALIFMM_E_ARG, "travel_into: no destinations");
+  for (int i = 0; i < nsrc; i++)
+    if (!dst[i]) return fail(ctx, ALIFMM_E_ARG, "travel_into: destination %d is null", i);
+  return travel_impl(ctx, subgrid, nsrc, scx, scz, first_slot, dst);
 }
 
 int alifmm_get_field(alifmm_ctx* ctx, int slot, double* out) {
@@ -839,23 +919,31 @@ class CopyTeam {
     for (auto& t : th_) t.join();
   }
   int size() const { return n_; }
+  // f(t) on the team's threads t = 1 .. size() - 1 (not the caller's); wait() joins them
+  void start(std::function<void(int)> f) {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      job_ = std::move(f);
+      left_ = n_ - 1;
+      gen_++;
+    }
+    cv_.notify_all();
+  }
+  void wait() {
+    std::unique_lock<std::mutex> l(m_);
+    done_.wait(l, [&] { return left_ == 0; });
+  }
   void copy(char* dst, const char* src, size_t n) {
     if (n_ <= 1 || n < (4u << 20)) {
       memcpy(dst, src, n);
       return;
     }
-    {
-      std::lock_guard<std::mutex> g(m_);
-      dst_ = dst;
-      src_ = src;
-      bytes_ = n;
-      left_ = n_ - 1;
-      gen_++;
-    }
-    cv_.notify_all();
+    dst_ = dst;
+    src_ = src;
+    bytes_ = n;
+    start([this](int t) { slice(t); });
     slice(0);
-    std::unique_lock<std::mutex> l(m_);
-    done_.wait(l, [&] { return left_ == 0; });
+    wait();
   }
 
  private:
@@ -866,13 +954,15 @@ class CopyTeam {
   void run(int t) {
     unsigned long seen = 0;
     for (;;) {
+      std::function<void(int)> f;
       {
         std::unique_lock<std::mutex> l(m_);
         cv_.wait(l, [&] { return gen_ != seen; });
         seen = gen_;
         if (stop_) return;
+        f = job_;
       }
-      slice(t);
+      f(t);
       std::lock_guard<std::mutex> g(m_);
       if (--left_ == 0) done_.notify_one();
     }
@@ -881,6 +971,7 @@ class CopyTeam {
   std::vector<std::thread> th_;
   std::mutex m_;
   std::condition_variable cv_, done_;
+  std::function<void(int)> job_;
   char* dst_ = nullptr;
   const char* src_ = nullptr;
   size_t bytes_ = 0;
@@ -903,6 +994,124 @@ static CopyTeam& copy_team(alifmm_ctx* ctx) {
 static void destroy_team(alifmm_ctx* ctx) {
   delete static_cast<CopyTeam*>(ctx->team);
   ctx->team = nullptr;
+}
+
+static void free_stream_bufs(alifmm_ctx* ctx) {
+  if (ctx->hstage) (void)hipHostFree(ctx->hstage);
+  if (ctx->hq) (void)hipHostFree(ctx->hq);
+  ctx->hstage = nullptr;
+  ctx->hq = nullptr;
+  ctx->hstage_bytes = ctx->hq_bytes = 0;
+}
+
+// Tile geometry and host buffers of a streamed band launch: W x 2^trlog tiles, the fewest rows
+// that keep every member's own tiles within the kernel's 1024 LDS counters (16-bit: <= 32768
+// cells a tile).  No geometry, no copy team or no pinned memory: so->active stays false (the
+// fields are copied after the launch).
+static int stream_setup(alifmm_ctx* ctx, StreamOut* so, int n, int K, int wlog, int fz, int fx) {
+  so->active = false;
+  if (copy_team(ctx).size() < 2) return ALIFMM_OK;
+  const int W = 1 << wlog, nstr = (fx + W - 1) / W, own = (nstr + K - 1) / K;
+  int trlog = 2;
+  while (trlog < 14 && (long)own * ((fz + (1 << trlog) - 1) >> trlog) > 1024) trlog++;
+  const int ntz = (fz + (1 << trlog) - 1) >> trlog;
+  if ((long)own * ntz > 1024 || ((long)W << trlog) > 32768) return ALIFMM_OK;
+  const size_t sbytes = (size_t)n * fz * fx * sizeof(double), qcap = (size_t)own * ntz;
+  const size_t qbytes = (size_t)n * K * qcap * sizeof(unsigned long long);
+  if (ctx->hstage_bytes < sbytes || ctx->hq_bytes < qbytes) {
+    free_stream_bufs(ctx);
+    if (hipHostMalloc(&ctx->hstage, sbytes, hipHostMallocCoherent) != hipSuccess ||
+        hipHostMalloc((void**)&ctx->hq, qbytes, hipHostMallocCoherent) != hipSuccess) {
+      (void)hipGetLastError();
+      free_stream_bufs(ctx);
+      return ALIFMM_OK;
+    }
+    ctx->hstage_bytes = sbytes;
+    ctx->hq_bytes = qbytes;
+  }
+  memset(ctx->hq, 0, qbytes);  // (the previous launch that used it has completed)
+  so->K = K;
+  so->wlog = wlog;
+  so->trlog = trlog;
+  so->nstr = nstr;
+  so->ntz = ntz;
+  so->nz = fz;
+  so->nx = fx;
+  so->qcap = (int)qcap;
+  so->active = true;
+  return ALIFMM_OK;
+}
+
+// copy-team thread w of nw: the queues of members w, w + nw, ... (member m = source * K + k owns
+// the stripes k, k + K, ...); each entry's tile goes from the staging field to the caller's, row
+// by row.  Ends when every expected tile has arrived, or once the launch has completed and a pass
+// over the queues finds nothing new (the missing sources are then copied from the device).
+static void stream_worker(alifmm_ctx* ctx, StreamOut* so, int w, int nw) {
+  struct Q {
+    int m, pos, expect;
+  };
+  std::vector<Q> qs;
+  long remaining = 0;
+  for (int m = w; m < so->n * so->K; m += nw) {
+    const int k = m % so->K;
+    const int nown = k < so->nstr ? (so->nstr - k + so->K - 1) / so->K : 0;
+    qs.push_back({m, 0, nown * so->ntz});
+    remaining += (long)nown * so->ntz;
+  }
+  const size_t cells = (size_t)so->nz * so->nx;
+  const double* stage = static_cast<const double*>(ctx->hstage);
+  const int W = 1 << so->wlog, TR = 1 << so->trlog;
+  int quiet = 0;
+  while (remaining > 0) {
+    bool any = false;
+    for (auto& q : qs) {
+      while (q.pos < q.expect) {
+        const unsigned long long v = __atomic_load_n(ctx->hq + (size_t)q.m * so->qcap + q.pos, __ATOMIC_ACQUIRE);
+        if ((long)(v >> 32) != (long)q.pos + 1) break;
+        const int t = (int)(unsigned)v, src = q.m / so->K;
+        const int tz = t / so->nstr, st = t - tz * so->nstr;
+        const int z0 = tz * TR, x0 = st * W;
+        const int rows = std::min(TR, so->nz - z0), cols = std::min(W, so->nx - x0);
+        double* d = so->dst[src];
+        const double* sp = stage + (size_t)src * cells;
+        for (int r = 0; r < rows; r++) {
+          const size_t o = (size_t)(z0 + r) * so->nx + x0;
+          memcpy(d + o, sp + o, (size_t)cols * sizeof(double));
+        }
+        q.pos++;
+        remaining--;
+        any = true;
+      }
+    }
+    if (any) {
+      quiet = 0;
+      continue;
+    }
+    if (so->kernel_done.load(std::memory_order_acquire)) {
+      if (++quiet > 1) break;
+    } else {
+      for (int i = 0; i < 64; i++) __builtin_ia32_pause();
+    }
+  }
+  for (auto& q : qs)
+    if (q.pos < q.expect) so->missing[q.m / so->K].store(1);
+}
+
+static void stream_start(alifmm_ctx* ctx, StreamOut* so) {
+  CopyTeam& team = copy_team(ctx);
+  so->kernel_done.store(0);
+  so->missing.reset(new std::atomic<int>[so->n]);
+  for (int i = 0; i < so->n; i++) so->missing[i].store(0);
+  const int nw = team.size() - 1;
+  team.start([ctx, so, nw](int t) { stream_worker(ctx, so, t - 1, nw); });
+}
+
+// the launch has completed (or failed): the workers finish the queues, then the team is joined
+static void stream_finish(alifmm_ctx* ctx, StreamOut* so) {
+  const auto t0 = std::chrono::steady_clock::now();
+  so->kernel_done.store(1, std::memory_order_release);
+  copy_team(ctx).wait();
+  ctx->t_stream_tail += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
 // Device -> pageable host copy of a list of segments: pieces of kPinBytes through kPinBufs pinned

@@ -162,6 +162,11 @@ constexpr int kStabLds = AF_STABLDS, kPtabLds = 722, kMatLds = AF_MATLDS;
 constexpr int kDirty = (int)0x80000000u;  // close-set slot: committed last step (edge cell)
 constexpr int kCell = 0x7fffffff;
 
+// host streaming of final tiles (BandParams::hs): completed tiles staged per step (more wait for
+// the flush at the end), own tiles per member with an LDS counter
+constexpr int kTdCap = 32;
+constexpr int kTileMax = 1024;
+
 struct Lds {
   double red[kWaves];
   double Lt[kLcap];  // close set: T of the slot (+inf: free)
@@ -185,6 +190,11 @@ struct Lds {
   int Sb[kSortB];    // bucket counts -> offsets
   int Sw[kWaves];    // per-wave bucket sums of the scan
 #endif
+  // host streaming (BandParams::hs): known-cell counters of the own tiles (two 16-bit counters per
+  // word; 0xffff once published), this step's completed tiles (own tile indices)
+  unsigned tcnt[kTileMax / 2];
+  int Td[kTdCap];
+  int nTd, qpos;
   double tmin_g, thr;
   unsigned long long nE2;  // claimed-list lengths: interior (low half), boundary (high half)
   int nA, nF, hi, taken, nD, nR, nRx, live_g, err_g, err, nFb;
@@ -369,6 +379,92 @@ __device__ AF_F18_ATTR double fouds18_w5(const Win5& F, const DevModel& M, const
   return fouds18<PRE_ONLY>(F, M, cm, z, x, dnx, dnz, nx, nz, pre);
 }
 
+// Host streaming.  Tiles are W columns (one stripe) x TR = 2^tr_log rows; member me's own tiles
+// are numbered o = tz * nown + js (stripe s = me + js K).  A tile whose cells are all known is
+// final: its cells go to the host field (system-scope stores, each wave instruction a contiguous
+// row piece), and once every wave's stores have completed (the X1 drain) its global index
+// tz * nstr + s is appended to the member's host queue.
+struct TileStream {
+  unsigned long long* hs;  // this source's host field (row-major doubles, as bits)
+  unsigned long long* hq;  // this member's queue
+  int wlog, trlog, nstr, nown, ntiles, K, me, kmagic, nz, nx;
+  AF_DEV int own(int z, int x) const {
+    const int s = x >> wlog;
+    return (z >> trlog) * nown + ((s * kmagic) >> 16);
+  }
+  AF_DEV int total(int z, int x) const {  // cells of the tile holding (z, x)
+    const int z0 = z & ~((1 << trlog) - 1), x0 = x & ~((1 << wlog) - 1);
+    return min(1 << trlog, nz - z0) * min(1 << wlog, nx - x0);
+  }
+  AF_DEV void origin(int o, int& z0, int& x0) const {
+    const int tz = o / nown, js = o - tz * nown;
+    z0 = tz << trlog;
+    x0 = (me + js * K) << wlog;
+  }
+  AF_DEV int global(int o) const {
+    const int tz = o / nown, js = o - tz * nown;
+    return tz * nstr + me + js * K;
+  }
+};
+
+// own cell (z, x) became known: count it; a completed tile joins this step's list
+AF_DEV void tile_known(Lds* sh, const TileStream& ts, int z, int x) {
+  const int o = ts.own(z, x);
+  const unsigned sft = (o & 1) * 16;
+  const unsigned old = (atomicAdd(&sh->tcnt[o >> 1], 1u << sft) >> sft) & 0xffffu;
+  if ((int)old + 1 == ts.total(z, x)) {
+    const int p = atomicAdd(&sh->nTd, 1);
+    if (p < kTdCap) sh->Td[p] = o;
+  }
+}
+
+// the listed tiles' cells -> host field (every thread; loads of 8 items, then their stores)
+AF_DEV void stage_tiles(const Lds* sh, int n, const TileStream& ts, const double* Tb, const TbLayout& TL, int tid) {
+  const int clog = ts.wlog + ts.trlog;
+  const long total = (long)n << clog;
+  for (long q0 = tid; q0 < total; q0 += 8L * kThreads) {
+    double v[8];
+    long d[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const long q = q0 + (long)u * kThreads;
+      d[u] = -1;
+      v[u] = 0.0;
+      if (q < total) {
+        int z0, x0;
+        ts.origin(sh->Td[q >> clog], z0, x0);
+        const int r = (int)(q & ((1L << clog) - 1));
+        const int z = z0 + (r >> ts.wlog), x = x0 + (r & ((1 << ts.wlog) - 1));
+        if (z < ts.nz && x < ts.nx) {
+          v[u] = gld(Tb + TL.at(z, x));
+          d[u] = (long)z * ts.nx + x;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++)
+      if (d[u] >= 0)
+        __hip_atomic_store(ts.hs + d[u], (unsigned long long)__double_as_longlong(v[u]), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// after every wave's stores of the listed tiles completed (a drain + barrier): wave 0 appends them
+// to the host queue and marks them published
+AF_DEV void publish_tiles(Lds* sh, const TileStream& ts, int lane) {
+  const int n = min(sh->nTd, kTdCap), q0 = sh->qpos;
+  if (lane < n) {
+    const int o = sh->Td[lane];
+    __hip_atomic_store(ts.hq + q0 + lane, ((unsigned long long)(q0 + lane + 1) << 32) | (unsigned)ts.global(o),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    atomicOr(&sh->tcnt[o >> 1], 0xffffu << ((o & 1) * 16));
+  }
+  if (lane == 0) {
+    sh->qpos = q0 + n;
+    sh->nTd = 0;
+  }
+}
+
 // X1 read side (wave 0): lane l polls word l & 3 of member l >> 2 (K <= kMaxK = 16 members, one
 // word per lane) until every member's words carry this step's tag, then the wave reduces them:
 // global Tmin, live close cells (sum), error (or), and the neighbour members' rim-list lengths.
@@ -482,7 +578,27 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
   // edge buffer of parity p: Tb + tb_cells + p * ecells, compact (KGeom::eidx)
   const int cells = nz * nx, ecells = (int)P.ecells, tbc = (int)P.tb_cells;
   double* const E0 = Tb + tbc;
+  // host streaming (mode 0 only)
+  const bool hstream = MODE == 0 && P.hs != nullptr;
+  TileStream ts{};
+  if (hstream) {
+    ts.wlog = P.wlog;
+    ts.trlog = P.tr_log;
+    ts.nstr = (nx + (1 << P.wlog) - 1) >> P.wlog;
+    ts.nown = (ts.nstr - me + K - 1) / K;
+    ts.ntiles = ts.nown * ((nz + (1 << P.tr_log) - 1) >> P.tr_log);
+    ts.K = K;
+    ts.me = me;
+    ts.kmagic = g.kmagic;
+    ts.nz = nz;
+    ts.nx = nx;
+    ts.hs = reinterpret_cast<unsigned long long*>(P.hs) + (long)src * nz * nx;
+    ts.hq = P.hq + (long)(src * K + me) * P.qcap;
+    for (int k = tid; k < kTileMax / 2; k += kThreads) sh->tcnt[k] = 0u;
+  }
   if (tid == 0) {
+    sh->nTd = 0;
+    sh->qpos = 0;
     sh->hi = 0;
     sh->nF = 0;
     sh->nD = 0;
@@ -513,8 +629,12 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
             gst_sc1(E0 + g.eidx(z, x), known ? -t : t);
             gst_sc1(E0 + ecells + g.eidx(z, x), known ? -t : t);
           }
-          if (known) gst(Sb + SL.at(z, x), (int)kKnown);
-          else push = true;
+          if (known) {
+            gst(Sb + SL.at(z, x), (int)kKnown);
+            if (hstream) tile_known(sh, ts, z, x);
+          } else {
+            push = true;
+          }
         }
       }
       const int s = wave_push(&sh->hi, push, capL, &sh->err);
@@ -608,6 +728,11 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
     const double* const Eprv = E0 + prv * ecells;
     const int eprv = tbc + prv * ecells;  // Eprv as an index from Tb
     const int hi = sh->hi;
+    // ---- P0h: the tiles completed last step -> host (drained with the X1 stores below) ----
+    if (hstream) {
+      const int nT = min(sh->nTd, kTdCap);
+      if (nT > 0) stage_tiles(sh, nT, ts, Tb, TL, tid);
+    }
     // ---- P1: local Tmin over the close set (LDS); publish every own close RIM cell (cell, T) for
     // the neighbour members, which keep those with T <= thr; clear the claim hash ----
     double tmin = INFINITY;
@@ -649,6 +774,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
 #if !AF_PROF_FBWAIT && !AF_PROF_SPILL
     AF_SUBT(3, tdr)
 #endif
+    if (hstream && wv == 0 && sh->nTd > 0) publish_tiles(sh, ts, lane);
     const long long tx1 = prof ? wall_clock64() : 0;
     if (K > 1) {
       if (tid == 0) {
@@ -767,6 +893,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
             } else {
               AL.put(sa, c[u]);
               gst(Sb + SL.at(pkz(c[u]), pkx(c[u])), (int)kKnown);
+              if (hstream) tile_known(sh, ts, pkz(c[u]), pkx(c[u]));
               if (LO) {
                 Lt.put_lds(e, INFINITY);
                 FS.put_lds(sf, e);
@@ -1171,6 +1298,27 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
   // done, so the copy-out of early sources overlaps the band of the late ones
   __syncthreads();
   copy_out_own(T, Tb, TL, g, me, nz, nx, tid);
+  // host streaming: every own tile not yet published (incomplete: cells never reached; or past a
+  // step's list), in windows of kTdCap tiles
+  if (hstream) {
+    for (int base = 0; base < ts.ntiles; base += kTdCap) {
+      if (tid == 0) sh->nTd = 0;
+      __syncthreads();
+      if (tid < kTdCap && base + tid < ts.ntiles) {
+        const int o = base + tid;
+        if (((sh->tcnt[o >> 1] >> ((o & 1) * 16)) & 0xffffu) != 0xffffu) sh->Td[atomicAdd(&sh->nTd, 1)] = o;
+      }
+      __syncthreads();
+      const int nT = sh->nTd;
+      if (nT > 0) {
+        stage_tiles(sh, nT, ts, Tb, TL, tid);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (wv == 0) publish_tiles(sh, ts, lane);
+      }
+      __syncthreads();
+    }
+  }
   if (prof) {
     for (int k = 0; k < 6; k++) B->ph[k] += ph[k];
     for (int k = 0; k < 4; k++) B->sub[k] += sub[k];

@@ -85,6 +85,15 @@ struct BandParams {
   long tb_cells;  // fmm_band_k: working-field size in doubles (the edge buffers follow)
   int sb_pitch;   // fmm_band_k: status-array pitch
   long max_steps;  // fmm_band_k: a band still running after this many steps stops with error 8
+  // fmm_band_k, mode 0: stream final tiles to the host while the band runs (hs null: off).  A tile
+  // is W (stripe width) columns x 2^tr_log rows of one member's stripe; it is final once all its
+  // cells are known (a per-member LDS counter); then its cells go to hs (host-mapped pinned memory:
+  // nsrc row-major fields) and, once stored, its index to the member's host queue hq (qcap entries
+  // per member src * K + member; entry k = (k + 1) << 32 | tz * nstripes + stripe)
+  double* hs;
+  unsigned long long* hq;
+  int qcap;
+  int tr_log;  // tile rows log2 (W x 2^tr_log cells per tile; own tiles per member <= 1024)
 };
 
 struct RayJob {

@@ -306,8 +306,11 @@ def main():
         te = min(runs)
         e2e = {"update_s": te, "update_s_runs": runs, "cell_updates_per_s": cells * ns / te, "sources_per_s": ns / te,
                "stack_bytes": int(F.nbytes), "fields_ms": M._ctx(0).last_timing()[2],
-               "what": "ALI_FMM.update() at C4: model digest (xxh3 of every array) + fields on the GPU + one "
-                       "copy of each field into the returned stack (no intermediate array; host peak = one stack)"}
+               "stream_tail_ms": M._ctx(0).get_option("stream_tail_ms"),
+               "stream_fallback_fields": M._ctx(0).get_option("stream_fallback"),
+               "what": "ALI_FMM.update() at C4: model digest (xxh3 of every array) + fields on the GPU, each "
+                       "streamed tile by tile out of the band kernel into the returned stack while it runs "
+                       "(alifmm_travel_into; stream_tail_ms = kernel end to last tile copied)"}
         del F
         for c in M._ctxs.values():
             c.close()

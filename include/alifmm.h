@@ -55,11 +55,14 @@ int alifmm_set_model(alifmm_ctx* ctx, int nnz, int nnx, const double* veln, cons
  * 256), "exact_lds" (subgrid > 1: 1 = the exact walk with its state in LDS, fmm_exact_lds.hip,
  * where the stage grids fit — subgrid <= 9; 0 = the HBM walk, fmm_exact.hip; bit-identical),
  * "coop" (band launch: 1 = cooperative, 0 = plain after a residency check), "cdelta_far" /
- * "r_far" (optional wider band beyond r_far cells; off by default). */
+ * "r_far" (optional wider band beyond r_far cells; off by default), "stream_out" (subgrid-1 travels
+ * with a host destination stream the fields out of the band kernel, alifmm_travel_into; default 1). */
 int alifmm_set_option(alifmm_ctx* ctx, const char* name, double value);
 /* Read an option, or "last_k" (workgroups per source of the last band launch), "n_cu"
- * (compute units of the device) and "vmax" (the model's fastest speed [m/s]: the exact prefix
- * covers T <= exact_r * dnx / vmax). */
+ * (compute units of the device), "vmax" (the model's fastest speed [m/s]: the exact prefix
+ * covers T <= exact_r * dnx / vmax), "stream_tail_ms" and "stream_fallback" (last travel with a host
+ * destination: ms from the band kernel's end to the last streamed tile copied; fields copied after
+ * the launch instead of streamed). */
 int alifmm_get_option(alifmm_ctx* ctx, const char* name, double* value);
 
 /* Shape of a travel-time field for subgrid size sg: (sg*(nnz-1)+1, sg*(nnx-1)+1). */
@@ -72,6 +75,18 @@ int alifmm_field_shape(alifmm_ctx* ctx, int subgrid, int* fnz, int* fnx);
  * also copied to out (nsrc x fnz x fnx float64).  Field semantics: SURVEY/DESIGN parity contract. */
 int alifmm_travel(alifmm_ctx* ctx, int subgrid, int nsrc, const double* scx, const double* scz,
                   int first_slot, double* out);
+
+/* alifmm_travel() with a caller-owned destination per source: field i goes to dst[i] (pageable
+ * host memory, fnz x fnx float64 each; e.g. rows of the (nsrc, fnz, fnx) stack of
+ * ALI_FMM.update() :3870-3936, which need not be consecutive).  Subgrid 1: the band kernel
+ * streams every tile of a field (one member's stripe, a few thousand cells) to coherent pinned
+ * staging as soon as all its cells are final, and the context's copy threads move it on to dst[i]
+ * while the band runs (option "stream_out", default 1; "stream_tail_ms" = the time from the
+ * kernel's end to the last tile copied).  Otherwise (and for a field a tile of which did not
+ * arrive) the fields are copied after the launch, as alifmm_copy_fields() kind 0.  The fields also
+ * stay resident in slots first_slot .. first_slot+nsrc-1. */
+int alifmm_travel_into(alifmm_ctx* ctx, int subgrid, int nsrc, const double* scx, const double* scz,
+                       int first_slot, double* const* dst);
 
 /* Copy a resident field to the host; release all resident fields. */
 int alifmm_get_field(alifmm_ctx* ctx, int slot, double* out);

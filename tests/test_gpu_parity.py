@@ -329,6 +329,22 @@ def test_c4_full_128_source_batch(golden, ctx, envelope):
         S = ctx.travel([sx[i]], [sz[i]])[0]
         assert int(ctx.get_option("last_k")) != kb or kb == 16
         assert np.array_equal(S, Ti), i
+    # the whole batch streamed out of the band kernel tile by tile (alifmm_travel_into) into
+    # non-consecutive rows of a larger stack, in reverse order: every field equals the resident one
+    # and no row outside the destinations is touched
+    fz, fx = ctx.field_shape(1)
+    D = np.zeros((130, fz, fx))
+    rows = list(range(129, 1, -1))
+    ctx.travel_into(sx, sz, D, rows)
+    envelope["c4_batch128_stream"] = {"tail_ms": ctx.get_option("stream_tail_ms"),
+                                      "fallback_fields": ctx.get_option("stream_fallback")}
+    assert ctx.get_option("stream_fallback") == 0
+    for i in (0, 1, k, 126, 127):
+        assert np.array_equal(D[rows[i]], ctx.get_field(i, 1)), i
+        if i in others:
+            assert np.array_equal(D[rows[i]], others[i]), i
+    assert not D[0].any() and not D[1].any()
+    del D
     ctx.release_fields()
 
 
