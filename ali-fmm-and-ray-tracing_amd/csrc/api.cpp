@@ -1024,7 +1024,7 @@ static int host_buf(void** p, size_t* have, size_t need) {  // coherent pinned m
 
 // Tile geometry and host buffers of a streamed band launch: W x 2^trlog tiles, the fewest rows
 // that keep every member's own tiles within the kernel's 1024 LDS counters (16-bit: <= 32768
-// cells a tile); a ring of rslots tiles per member, <= 1 GB in all.  No geometry, no copy team or
+// cells a tile); a ring of 64 tile slots per member.  No geometry, no copy team or
 // no pinned memory: so->active stays false (the fields are copied after the launch).
 static int stream_setup(alifmm_ctx* ctx, StreamOut* so, int n, int K, int wlog, int fz, int fx) {
   so->active = false;
@@ -1035,7 +1035,9 @@ static int stream_setup(alifmm_ctx* ctx, StreamOut* so, int n, int K, int wlog, 
   const int ntz = (fz + (1 << trlog) - 1) >> trlog;
   if ((long)own * ntz > 1024 || ((long)W << trlog) > 32768) return ALIFMM_OK;
   const size_t members = (size_t)n * K, tile_bytes = ((size_t)W << trlog) * sizeof(double);
-  const int rslots = (int)std::max<size_t>(8, std::min<size_t>(64, (1ull << 30) / (members * tile_bytes)));
+  // 64 slots per member: the kernel may hold two staged, unpublished lists of up to 32 tiles when
+  // it asks for slots for the next ones (fmm_band_k.hip kTdCap); C4: 256 members x 64 x 64 KB = 1 GB
+  const int rslots = 64;
   const size_t qcap = (size_t)own * ntz;
   if (host_buf(&ctx->hstage, &ctx->hstage_bytes, members * rslots * tile_bytes) ||
       host_buf((void**)&ctx->hq, &ctx->hq_bytes, members * qcap * sizeof(unsigned long long)) ||

@@ -645,7 +645,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
     ts.nz = nz;
     ts.nx = nx;
     const long mid = (long)src * K + me;
-    ts.rslots = P.rslots;
+    ts.rslots = max(P.rslots, 1);
     ts.ring = reinterpret_cast<unsigned long long*>(P.hs) + (mid * P.rslots << (P.wlog + P.tr_log));
     ts.hq = P.hq + mid * P.qcap;
     ts.cons = P.hcons + mid;
@@ -660,6 +660,9 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
     sh->nR = 0;
     sh->err = 0;
     sh->nrim[0] = sh->nrim[1] = 0;
+    // two lists of up to kTdCap tiles can be staged and not yet published when a third asks for
+    // slots: fewer slots could wait for the host forever (the host gives 2 kTdCap)
+    if (hstream && P.rslots < 2 * kTdCap) sh->err = 11;
   }
   __syncthreads();
   // ---------------- hand-over: own cells only ----------------
@@ -1365,7 +1368,14 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
   // step's list; or staged in the last steps), in windows of kTdCap tiles, each published once
   // its stores have drained
   if (hstream) {
-    if (tid == 0) sh->spos = sh->qpos;  // the unpublished staged tiles are staged again below
+    // the last step's staged list: its stores drained (every wave), then published
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (wv == 0 && sh->nst > 0) publish_tiles(sh, ts, (int)(steps & 1) ^ 1, lane);
+    if (tid == 0) {
+      sh->spos += sh->nst;
+      sh->nst = 0;
+    }
     for (int base = 0; base < ts.ntiles; base += kTdCap) {
       if (tid == 0) sh->nTd[0] = 0;
       __syncthreads();
