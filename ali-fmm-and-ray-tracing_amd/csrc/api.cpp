@@ -523,7 +523,7 @@ struct StreamOut {
   double* const* dst = nullptr;  // per source of the chunk
   int n = 0;
   bool active = false;  // the band launch streams (stream_setup)
-  int K = 0, wlog = 0, trlog = 0, nstr = 0, ntz = 0, nz = 0, nx = 0, qcap = 0;
+  int K = 0, wlog = 0, trlog = 0, nstr = 0, ntz = 0, nz = 0, nx = 0, qcap = 0, rslots = 0;
   std::atomic<int> kernel_done{0};
   std::unique_ptr<std::atomic<int>[]> missing;  // per source: a tile never arrived (copied after)
   std::chrono::steady_clock::time_point t_done;
@@ -660,7 +660,9 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
     if (so->active) {
       P.hs = static_cast<double*>(ctx->hstage);
       P.hq = ctx->hq;
+      P.hcons = ctx->hcons;
       P.qcap = so->qcap;
+      P.rslots = so->rslots;
       P.tr_log = so->trlog;
     }
   }
@@ -999,15 +1001,31 @@ static void destroy_team(alifmm_ctx* ctx) {
 static void free_stream_bufs(alifmm_ctx* ctx) {
   if (ctx->hstage) (void)hipHostFree(ctx->hstage);
   if (ctx->hq) (void)hipHostFree(ctx->hq);
+  if (ctx->hcons) (void)hipHostFree(ctx->hcons);
   ctx->hstage = nullptr;
   ctx->hq = nullptr;
-  ctx->hstage_bytes = ctx->hq_bytes = 0;
+  ctx->hcons = nullptr;
+  ctx->hstage_bytes = ctx->hq_bytes = ctx->hcons_bytes = 0;
+}
+
+static int host_buf(void** p, size_t* have, size_t need) {  // coherent pinned memory, grown on demand
+  if (*have >= need) return 0;
+  if (*p) (void)hipHostFree(*p);
+  *p = nullptr;
+  *have = 0;
+  if (hipHostMalloc(p, need, hipHostMallocCoherent) != hipSuccess) {
+    (void)hipGetLastError();
+    *p = nullptr;
+    return -1;
+  }
+  *have = need;
+  return 0;
 }
 
 // Tile geometry and host buffers of a streamed band launch: W x 2^trlog tiles, the fewest rows
 // that keep every member's own tiles within the kernel's 1024 LDS counters (16-bit: <= 32768
-// cells a tile).  No geometry, no copy team or no pinned memory: so->active stays false (the
-// fields are copied after the launch).
+// cells a tile); a ring of 64 tile slots per member.  No geometry, no copy team or
+// no pinned memory: so->active stays false (the fields are copied after the launch).
 static int stream_setup(alifmm_ctx* ctx, StreamOut* so, int n, int K, int wlog, int fz, int fx) {
   so->active = false;
   if (copy_team(ctx).size() < 2) return ALIFMM_OK;
@@ -1016,20 +1034,20 @@ static int stream_setup(alifmm_ctx* ctx, StreamOut* so, int n, int K, int wlog, 
   while (trlog < 14 && (long)own * ((fz + (1 << trlog) - 1) >> trlog) > 1024) trlog++;
   const int ntz = (fz + (1 << trlog) - 1) >> trlog;
   if ((long)own * ntz > 1024 || ((long)W << trlog) > 32768) return ALIFMM_OK;
-  const size_t sbytes = (size_t)n * fz * fx * sizeof(double), qcap = (size_t)own * ntz;
-  const size_t qbytes = (size_t)n * K * qcap * sizeof(unsigned long long);
-  if (ctx->hstage_bytes < sbytes || ctx->hq_bytes < qbytes) {
+  const size_t members = (size_t)n * K, tile_bytes = ((size_t)W << trlog) * sizeof(double);
+  // 64 slots per member: the kernel may hold two staged, unpublished lists of up to 32 tiles when
+  // it asks for slots for the next ones (fmm_band_k.hip kTdCap); C4: 256 members x 64 x 64 KB = 1 GB
+  const int rslots = 64;
+  const size_t qcap = (size_t)own * ntz;
+  if (host_buf(&ctx->hstage, &ctx->hstage_bytes, members * rslots * tile_bytes) ||
+      host_buf((void**)&ctx->hq, &ctx->hq_bytes, members * qcap * sizeof(unsigned long long)) ||
+      host_buf((void**)&ctx->hcons, &ctx->hcons_bytes, members * sizeof(unsigned))) {
     free_stream_bufs(ctx);
-    if (hipHostMalloc(&ctx->hstage, sbytes, hipHostMallocCoherent) != hipSuccess ||
-        hipHostMalloc((void**)&ctx->hq, qbytes, hipHostMallocCoherent) != hipSuccess) {
-      (void)hipGetLastError();
-      free_stream_bufs(ctx);
-      return ALIFMM_OK;
-    }
-    ctx->hstage_bytes = sbytes;
-    ctx->hq_bytes = qbytes;
+    return ALIFMM_OK;
   }
-  memset(ctx->hq, 0, qbytes);  // (the previous launch that used it has completed)
+  // (the previous launch that used them has completed)
+  memset(ctx->hq, 0, members * qcap * sizeof(unsigned long long));
+  memset(ctx->hcons, 0, members * sizeof(unsigned));
   so->K = K;
   so->wlog = wlog;
   so->trlog = trlog;
@@ -1038,14 +1056,16 @@ static int stream_setup(alifmm_ctx* ctx, StreamOut* so, int n, int K, int wlog, 
   so->nz = fz;
   so->nx = fx;
   so->qcap = (int)qcap;
+  so->rslots = rslots;
   so->active = true;
   return ALIFMM_OK;
 }
 
 // copy-team thread w of nw: the queues of members w, w + nw, ... (member m = source * K + k owns
-// the stripes k, k + K, ...); each entry's tile goes from the staging field to the caller's, row
-// by row.  Ends when every expected tile has arrived, or once the launch has completed and a pass
-// over the queues finds nothing new (the missing sources are then copied from the device).
+// the stripes k, k + K, ...); each entry's tile goes from its ring slot to the caller's field, row
+// by row, and the slot is handed back.  Ends when every expected tile has arrived, or once the
+// launch has completed and a pass over the queues finds nothing new (the missing sources are then
+// copied from the device).
 static void stream_worker(alifmm_ctx* ctx, StreamOut* so, int w, int nw) {
   struct Q {
     int m, pos, expect;
@@ -1058,9 +1078,8 @@ static void stream_worker(alifmm_ctx* ctx, StreamOut* so, int w, int nw) {
     qs.push_back({m, 0, nown * so->ntz});
     remaining += (long)nown * so->ntz;
   }
-  const size_t cells = (size_t)so->nz * so->nx;
-  const double* stage = static_cast<const double*>(ctx->hstage);
-  const int W = 1 << so->wlog, TR = 1 << so->trlog;
+  const double* ring = static_cast<const double*>(ctx->hstage);
+  const int W = 1 << so->wlog, TR = 1 << so->trlog, clog = so->wlog + so->trlog;
   int quiet = 0;
   while (remaining > 0) {
     bool any = false;
@@ -1073,12 +1092,11 @@ static void stream_worker(alifmm_ctx* ctx, StreamOut* so, int w, int nw) {
         const int z0 = tz * TR, x0 = st * W;
         const int rows = std::min(TR, so->nz - z0), cols = std::min(W, so->nx - x0);
         double* d = so->dst[src];
-        const double* sp = stage + (size_t)src * cells;
-        for (int r = 0; r < rows; r++) {
-          const size_t o = (size_t)(z0 + r) * so->nx + x0;
-          memcpy(d + o, sp + o, (size_t)cols * sizeof(double));
-        }
+        const double* sp = ring + (((size_t)q.m * so->rslots + q.pos % so->rslots) << clog);
+        for (int r = 0; r < rows; r++)
+          memcpy(d + (size_t)(z0 + r) * so->nx + x0, sp + (size_t)r * W, (size_t)cols * sizeof(double));
         q.pos++;
+        __atomic_store_n(ctx->hcons + q.m, (unsigned)q.pos, __ATOMIC_RELEASE);  // the slot is free
         remaining--;
         any = true;
       }

@@ -124,15 +124,17 @@ struct alifmm_ctx {
   static constexpr size_t kPinBytes = 32u << 20;
   void* pin[kPinBufs] = {};
   hipEvent_t pin_ev[kPinBufs] = {};
-  // alifmm_travel_into (subgrid 1): the band kernel streams final tiles into hstage (coherent
-  // pinned memory, the chunk's fields row-major) and their indices into hq (per-member queues)
-  // while it runs; the copy team moves each tile on to the caller's field.  Kept across calls
-  // (freed by alifmm_release_fields / alifmm_ctx_destroy).
+  // alifmm_travel_into (subgrid 1): the band kernel streams final tiles into a ring of slots per
+  // band member (hstage: coherent pinned memory) and their indices into hq (per-member queues);
+  // the copy team moves each tile on to the caller's field and returns its slot (hcons).  Kept
+  // across calls (freed by alifmm_release_fields / alifmm_ctx_destroy).
   int stream_out = 1;
   void* hstage = nullptr;
   size_t hstage_bytes = 0;
   unsigned long long* hq = nullptr;
   size_t hq_bytes = 0;
+  unsigned* hcons = nullptr;
+  size_t hcons_bytes = 0;
   double t_stream_tail = 0;  // last travel_into: ms from the band kernel's end to the last tile copied
   long stream_fallback = 0;  // last travel_into: fields copied after the kernel (not streamed)
 };

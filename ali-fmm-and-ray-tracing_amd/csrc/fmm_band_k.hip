@@ -166,6 +166,13 @@ constexpr int kCell = 0x7fffffff;
 // the flush at the end), own tiles per member with an LDS counter
 constexpr int kTdCap = 32;
 constexpr int kTileMax = 1024;
+// AF_HS_VEC: 16-byte system-scope stores (1) or 8-byte (0)
+#ifndef AF_HS_VEC
+#define AF_HS_VEC 1
+#endif
+#ifndef AF_HS_U
+#define AF_HS_U 4  // items per thread and batch of stage_tiles
+#endif
 
 struct Lds {
   double red[kWaves];
@@ -193,8 +200,11 @@ struct Lds {
   // host streaming (BandParams::hs): known-cell counters of the own tiles (two 16-bit counters per
   // word; 0xffff once published), this step's completed tiles (own tile indices)
   unsigned tcnt[kTileMax / 2];
-  int Td[kTdCap];
-  int nTd, qpos;
+  int Td[2][kTdCap];  // [step parity]: tiles completed in a step (staged, then published later)
+  int nTd[2];
+  int qpos;      // tiles published (host queue entries written)
+  int spos, nst; // tiles staged before this step; tiles staged this step
+  int cons;      // tiles the host has taken out of the ring (last read)
   double tmin_g, thr;
   unsigned long long nE2;  // claimed-list lengths: interior (low half), boundary (high half)
   int nA, nF, hi, taken, nD, nR, nRx, live_g, err_g, err, nFb;
@@ -381,13 +391,16 @@ __device__ AF_F18_ATTR double fouds18_w5(const Win5& F, const DevModel& M, const
 
 // Host streaming.  Tiles are W columns (one stripe) x TR = 2^tr_log rows; member me's own tiles
 // are numbered o = tz * nown + js (stripe s = me + js K).  A tile whose cells are all known is
-// final: its cells go to the host field (system-scope stores, each wave instruction a contiguous
-// row piece), and once every wave's stores have completed (the X1 drain) its global index
-// tz * nstr + s is appended to the member's host queue.
+// final.  Tiles completed in step k are staged in step k + 1, right after the X1 drain: their cells
+// go to the member's ring of host slots (tile i of the member to slot i mod rslots, row-major with
+// row pitch W; system-scope stores, each wave instruction a contiguous piece), and after the next
+// drain (every wave's stores complete) their global indices tz * nstr + s are appended to the
+// member's host queue.  A slot is reused once the host has taken its tile (its count in cons).
 struct TileStream {
-  unsigned long long* hs;  // this source's host field (row-major doubles, as bits)
-  unsigned long long* hq;  // this member's queue
-  int wlog, trlog, nstr, nown, ntiles, K, me, kmagic, nz, nx;
+  unsigned long long* ring;  // this member's slots (as bits of doubles)
+  unsigned long long* hq;    // this member's queue
+  const unsigned* cons;      // tiles of this member the host has copied out (host-written)
+  int wlog, trlog, nstr, nown, ntiles, K, me, kmagic, nz, nx, rslots;
   AF_DEV int own(int z, int x) const {
     const int s = x >> wlog;
     return (z >> trlog) * nown + ((s * kmagic) >> 16);
@@ -407,61 +420,100 @@ struct TileStream {
   }
 };
 
-// own cell (z, x) became known: count it; a completed tile joins this step's list
-AF_DEV void tile_known(Lds* sh, const TileStream& ts, int z, int x) {
+// before tiles i0 .. i0 + n - 1 of the member are staged: wait until the host has taken the tiles
+// that used their slots (one lane; the cached count is re-read only when it falls short)
+AF_DEV void ring_space(Lds* sh, const TileStream& ts, int i0, int n) {
+  for (long spins = 0; i0 + n - sh->cons > ts.rslots; spins++) {
+    sh->cons = (int)__hip_atomic_load(ts.cons, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (i0 + n - sh->cons <= ts.rslots) break;
+    __builtin_amdgcn_s_sleep(2);
+    if (spins > (1L << 24)) {  // the host stopped taking tiles
+      sh->err = 11;
+      sh->cons = i0 + n;
+    }
+  }
+}
+
+// own cell (z, x) became known: count it; a completed tile joins list b (the step's parity)
+AF_DEV void tile_known(Lds* sh, const TileStream& ts, int z, int x, int b) {
   const int o = ts.own(z, x);
   const unsigned sft = (o & 1) * 16;
   const unsigned old = (atomicAdd(&sh->tcnt[o >> 1], 1u << sft) >> sft) & 0xffffu;
   if ((int)old + 1 == ts.total(z, x)) {
-    const int p = atomicAdd(&sh->nTd, 1);
-    if (p < kTdCap) sh->Td[p] = o;
+    const int p = atomicAdd(&sh->nTd[b], 1);
+    if (p < kTdCap) sh->Td[b][p] = o;
   }
 }
 
-// the listed tiles' cells -> host field (every thread; loads of 8 items, then their stores)
-AF_DEV void stage_tiles(const Lds* sh, int n, const TileStream& ts, const double* Tb, const TbLayout& TL, int tid) {
+typedef double d2v __attribute__((ext_vector_type(2)));
+// system-scope 16-byte store (host memory): write-through, complete when the wave's vmcnt drains
+AF_DEV void st_sys16(unsigned long long* p, double a, double b) {
+  const d2v v = {a, b};
+  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+}
+AF_DEV void st_sys8(unsigned long long* p, double a) {
+  __hip_atomic_store(p, (unsigned long long)__double_as_longlong(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// list b's tiles' cells -> their ring slots (tile i0 + k of the member for entry k; every thread;
+// loads of AF_HS_U items, then their stores).  An item is one cell (AF_HS_VEC 0) or two adjacent
+// cells of a row (1); consecutive lanes take consecutive items of a tile, so one wave instruction
+// writes a contiguous piece of the slot
+AF_DEV void stage_tiles(const Lds* sh, int n, int b, int i0, const TileStream& ts, const double* Tb,
+                        const TbLayout& TL, int tid) {
+  constexpr int kV = AF_HS_VEC ? 2 : 1;
   const int clog = ts.wlog + ts.trlog;
-  const long total = (long)n << clog;
-  for (long q0 = tid; q0 < total; q0 += 8L * kThreads) {
-    double v[8];
-    long d[8];
+  const int ilog = clog - (kV - 1), rlog = ts.wlog - (kV - 1);  // items per tile / row (log2)
+  const long total = (long)n << ilog;
+  for (long q0 = tid; q0 < total; q0 += (long)AF_HS_U * kThreads) {
+    double v0[AF_HS_U], v1[AF_HS_U];
+    long d[AF_HS_U];
+    int w[AF_HS_U];  // cells of the item inside the grid (0, 1, 2)
 #pragma unroll
-    for (int u = 0; u < 8; u++) {
+    for (int u = 0; u < AF_HS_U; u++) {
       const long q = q0 + (long)u * kThreads;
-      d[u] = -1;
-      v[u] = 0.0;
+      d[u] = 0;
+      w[u] = 0;
+      v0[u] = v1[u] = 0.0;
       if (q < total) {
+        const int k = (int)(q >> ilog);
         int z0, x0;
-        ts.origin(sh->Td[q >> clog], z0, x0);
-        const int r = (int)(q & ((1L << clog) - 1));
-        const int z = z0 + (r >> ts.wlog), x = x0 + (r & ((1 << ts.wlog) - 1));
+        ts.origin(sh->Td[b][k], z0, x0);
+        const int r = (int)(q & ((1L << ilog) - 1));
+        const int zr = r >> rlog, xr = kV * (r & ((1 << rlog) - 1));
+        const int z = z0 + zr, x = x0 + xr;
         if (z < ts.nz && x < ts.nx) {
-          v[u] = gld(Tb + TL.at(z, x));
-          d[u] = (long)z * ts.nx + x;
+          w[u] = (kV == 2 && x + 1 < ts.nx) ? 2 : 1;
+          v0[u] = gld(Tb + TL.at(z, x));
+          if (w[u] == 2) v1[u] = gld(Tb + TL.at(z, x + 1));
+          d[u] = ((long)((i0 + k) % ts.rslots) << clog) + (zr << ts.wlog) + xr;
         }
       }
     }
 #pragma unroll
-    for (int u = 0; u < 8; u++)
-      if (d[u] >= 0)
-        __hip_atomic_store(ts.hs + d[u], (unsigned long long)__double_as_longlong(v[u]), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
+    for (int u = 0; u < AF_HS_U; u++) {
+      if (w[u] == 2) {
+        st_sys16(ts.ring + d[u], v0[u], v1[u]);
+      } else if (w[u] == 1) {
+        st_sys8(ts.ring + d[u], v0[u]);
+      }
+    }
   }
 }
 
-// after every wave's stores of the listed tiles completed (a drain + barrier): wave 0 appends them
-// to the host queue and marks them published
-AF_DEV void publish_tiles(Lds* sh, const TileStream& ts, int lane) {
-  const int n = min(sh->nTd, kTdCap), q0 = sh->qpos;
+// after every wave's stores of list b completed (a drain + barrier): wave 0 appends its tiles to
+// the host queue, marks them published and empties the list
+AF_DEV void publish_tiles(Lds* sh, const TileStream& ts, int b, int lane) {
+  const int n = min(sh->nTd[b], kTdCap), q0 = sh->qpos;
   if (lane < n) {
-    const int o = sh->Td[lane];
+    const int o = sh->Td[b][lane];
     __hip_atomic_store(ts.hq + q0 + lane, ((unsigned long long)(q0 + lane + 1) << 32) | (unsigned)ts.global(o),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     atomicOr(&sh->tcnt[o >> 1], 0xffffu << ((o & 1) * 16));
   }
   if (lane == 0) {
     sh->qpos = q0 + n;
-    sh->nTd = 0;
+    sh->nTd[b] = 0;
   }
 }
 
@@ -592,19 +644,25 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
     ts.kmagic = g.kmagic;
     ts.nz = nz;
     ts.nx = nx;
-    ts.hs = reinterpret_cast<unsigned long long*>(P.hs) + (long)src * nz * nx;
-    ts.hq = P.hq + (long)(src * K + me) * P.qcap;
+    const long mid = (long)src * K + me;
+    ts.rslots = max(P.rslots, 1);
+    ts.ring = reinterpret_cast<unsigned long long*>(P.hs) + (mid * P.rslots << (P.wlog + P.tr_log));
+    ts.hq = P.hq + mid * P.qcap;
+    ts.cons = P.hcons + mid;
     for (int k = tid; k < kTileMax / 2; k += kThreads) sh->tcnt[k] = 0u;
   }
   if (tid == 0) {
-    sh->nTd = 0;
-    sh->qpos = 0;
+    sh->nTd[0] = sh->nTd[1] = 0;
+    sh->qpos = sh->spos = sh->nst = sh->cons = 0;
     sh->hi = 0;
     sh->nF = 0;
     sh->nD = 0;
     sh->nR = 0;
     sh->err = 0;
     sh->nrim[0] = sh->nrim[1] = 0;
+    // two lists of up to kTdCap tiles can be staged and not yet published when a third asks for
+    // slots: fewer slots could wait for the host forever (the host gives 2 kTdCap)
+    if (hstream && P.rslots < 2 * kTdCap) sh->err = 11;
   }
   __syncthreads();
   // ---------------- hand-over: own cells only ----------------
@@ -631,7 +689,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
           }
           if (known) {
             gst(Sb + SL.at(z, x), (int)kKnown);
-            if (hstream) tile_known(sh, ts, z, x);
+            if (hstream) tile_known(sh, ts, z, x, 1);  // as if completed in step -1
           } else {
             push = true;
           }
@@ -728,10 +786,12 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
     const double* const Eprv = E0 + prv * ecells;
     const int eprv = tbc + prv * ecells;  // Eprv as an index from Tb
     const int hi = sh->hi;
-    // ---- P0h: the tiles completed last step -> host (drained with the X1 stores below) ----
-    if (hstream) {
-      const int nT = min(sh->nTd, kTdCap);
-      if (nT > 0) stage_tiles(sh, nT, ts, Tb, TL, tid);
+    // ---- P0h: ring space for the tiles completed last step (staged after the X1 drain) ----
+    if (hstream && tid == 0) {
+      sh->spos += sh->nst;
+      const int nT = min(sh->nTd[prv], kTdCap);
+      sh->nst = nT;
+      if (nT > 0) ring_space(sh, ts, sh->spos, nT);
     }
     // ---- P1: local Tmin over the close set (LDS); publish every own close RIM cell (cell, T) for
     // the neighbour members, which keep those with T <= thr; clear the claim hash ----
@@ -774,7 +834,13 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
 #if !AF_PROF_FBWAIT && !AF_PROF_SPILL
     AF_SUBT(3, tdr)
 #endif
-    if (hstream && wv == 0 && sh->nTd > 0) publish_tiles(sh, ts, lane);
+    if (hstream) {
+      // publish the tiles staged last step (their stores have drained: the wait above), then stage
+      // the ones completed last step (slots reserved in P0h)
+      if (wv == 0 && sh->nTd[par] > 0) publish_tiles(sh, ts, par, lane);
+      const int nT = sh->nst;
+      if (nT > 0) stage_tiles(sh, nT, prv, sh->spos, ts, Tb, TL, tid);
+    }
     const long long tx1 = prof ? wall_clock64() : 0;
     if (K > 1) {
       if (tid == 0) {
@@ -893,7 +959,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
             } else {
               AL.put(sa, c[u]);
               gst(Sb + SL.at(pkz(c[u]), pkx(c[u])), (int)kKnown);
-              if (hstream) tile_known(sh, ts, pkz(c[u]), pkx(c[u]));
+              if (hstream) tile_known(sh, ts, pkz(c[u]), pkx(c[u]), par);
               if (LO) {
                 Lt.put_lds(e, INFINITY);
                 FS.put_lds(sf, e);
@@ -1298,23 +1364,35 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
   // done, so the copy-out of early sources overlaps the band of the late ones
   __syncthreads();
   copy_out_own(T, Tb, TL, g, me, nz, nx, tid);
-  // host streaming: every own tile not yet published (incomplete: cells never reached; or past a
-  // step's list), in windows of kTdCap tiles
+  // host streaming: every own tile not yet published (incomplete: cells never reached; past a
+  // step's list; or staged in the last steps), in windows of kTdCap tiles, each published once
+  // its stores have drained
   if (hstream) {
+    // the last step's staged list: its stores drained (every wave), then published
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (wv == 0 && sh->nst > 0) publish_tiles(sh, ts, (int)(steps & 1) ^ 1, lane);
+    if (tid == 0) {
+      sh->spos += sh->nst;
+      sh->nst = 0;
+    }
     for (int base = 0; base < ts.ntiles; base += kTdCap) {
-      if (tid == 0) sh->nTd = 0;
+      if (tid == 0) sh->nTd[0] = 0;
       __syncthreads();
       if (tid < kTdCap && base + tid < ts.ntiles) {
         const int o = base + tid;
-        if (((sh->tcnt[o >> 1] >> ((o & 1) * 16)) & 0xffffu) != 0xffffu) sh->Td[atomicAdd(&sh->nTd, 1)] = o;
+        if (((sh->tcnt[o >> 1] >> ((o & 1) * 16)) & 0xffffu) != 0xffffu) sh->Td[0][atomicAdd(&sh->nTd[0], 1)] = o;
       }
       __syncthreads();
-      const int nT = sh->nTd;
+      const int nT = sh->nTd[0];
       if (nT > 0) {
-        stage_tiles(sh, nT, ts, Tb, TL, tid);
+        if (tid == 0) ring_space(sh, ts, sh->spos, nT);
+        __syncthreads();
+        stage_tiles(sh, nT, 0, sh->spos, ts, Tb, TL, tid);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (wv == 0) publish_tiles(sh, ts, lane);
+        if (wv == 0) publish_tiles(sh, ts, 0, lane);
+        if (tid == 0) sh->spos += nT;
       }
       __syncthreads();
     }

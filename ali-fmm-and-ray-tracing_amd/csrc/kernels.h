@@ -87,13 +87,17 @@ struct BandParams {
   long max_steps;  // fmm_band_k: a band still running after this many steps stops with error 8
   // fmm_band_k, mode 0: stream final tiles to the host while the band runs (hs null: off).  A tile
   // is W (stripe width) columns x 2^tr_log rows of one member's stripe; it is final once all its
-  // cells are known (a per-member LDS counter); then its cells go to hs (host-mapped pinned memory:
-  // nsrc row-major fields) and, once stored, its index to the member's host queue hq (qcap entries
-  // per member src * K + member; entry k = (k + 1) << 32 | tz * nstripes + stripe)
+  // cells are known (a per-member LDS counter).  Member m = src * K + member owns rslots slots of
+  // W << tr_log doubles in hs (coherent pinned host memory); its i-th final tile goes to slot
+  // i mod rslots (row-major, row pitch W), then entry i = (i + 1) << 32 | tz * nstripes + stripe
+  // to its host queue hq + m * qcap; the slot is reused once hcons[m] (host-written: tiles taken)
+  // exceeds i
   double* hs;
   unsigned long long* hq;
+  const unsigned* hcons;
   int qcap;
-  int tr_log;  // tile rows log2 (W x 2^tr_log cells per tile; own tiles per member <= 1024)
+  int rslots;
+  int tr_log;  // tile rows log2 (own tiles per member <= 1024, <= 32768 cells a tile)
 };
 
 struct RayJob {
