@@ -79,9 +79,9 @@ int alifmm_travel(alifmm_ctx* ctx, int subgrid, int nsrc, const double* scx, con
 /* alifmm_travel() with a caller-owned destination per source: field i goes to dst[i] (pageable
  * host memory, fnz x fnx float64 each; e.g. rows of the (nsrc, fnz, fnx) stack of
  * ALI_FMM.update() :3870-3936, which need not be consecutive).  Subgrid 1: the band kernel
- * streams every tile of a field (one member's stripe, a few thousand cells) to coherent pinned
- * staging as soon as all its cells are final, and the context's copy threads move it on to dst[i]
- * while the band runs (option "stream_out", default 1; "stream_tail_ms" = the time from the
+ * streams every tile of a field (one member's stripe, a few thousand cells) to a ring of coherent
+ * pinned slots as soon as all its cells are final, and the context's copy threads move it on to
+ * dst[i] while the band runs (option "stream_out", default 1; "stream_tail_ms" = the time from the
  * kernel's end to the last tile copied).  Otherwise (and for a field a tile of which did not
  * arrive) the fields are copied after the launch, as alifmm_copy_fields() kind 0.  The fields also
  * stay resident in slots first_slot .. first_slot+nsrc-1. */
