@@ -27,6 +27,7 @@
 #include "../../include/alifmm.h"
 #include "context.h"
 #include "kernels.h"
+#include "tile_stream.h"
 
 extern char** environ;
 
@@ -523,10 +524,9 @@ struct StreamOut {
   double* const* dst = nullptr;  // per source of the chunk
   int n = 0;
   bool active = false;  // the band launch streams (stream_setup)
-  int K = 0, wlog = 0, trlog = 0, nstr = 0, ntz = 0, nz = 0, nx = 0, qcap = 0, rslots = 0;
+  af::ts::Geometry g;
   std::atomic<int> kernel_done{0};
   std::unique_ptr<std::atomic<int>[]> missing;  // per source: a tile never arrived (copied after)
-  std::chrono::steady_clock::time_point t_done;
 };
 static int stream_setup(alifmm_ctx* ctx, StreamOut* so, int n, int K, int wlog, int fz, int fx);
 static void stream_start(alifmm_ctx* ctx, StreamOut* so);
@@ -661,9 +661,9 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
       P.hs = static_cast<double*>(ctx->hstage);
       P.hq = ctx->hq;
       P.hcons = ctx->hcons;
-      P.qcap = so->qcap;
-      P.rslots = so->rslots;
-      P.tr_log = so->trlog;
+      P.qcap = so->g.qcap;
+      P.rslots = so->g.rslots;
+      P.tr_log = so->g.trlog;
     }
   }
   HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
@@ -1022,97 +1022,26 @@ static int host_buf(void** p, size_t* have, size_t need) {  // coherent pinned m
   return 0;
 }
 
-// Tile geometry and host buffers of a streamed band launch: W x 2^trlog tiles, the fewest rows
-// that keep every member's own tiles within the kernel's 1024 LDS counters (16-bit: <= 32768
-// cells a tile); a ring of 64 tile slots per member.  No geometry, no copy team or
-// no pinned memory: so->active stays false (the fields are copied after the launch).
+// Tile geometry (tile_stream.h) and host buffers of a streamed band launch: a ring of
+// kRingSlots tile slots per member (1 GB at C4).  No geometry, no copy team or no pinned memory:
+// so->active stays false (the fields are copied after the launch).
 static int stream_setup(alifmm_ctx* ctx, StreamOut* so, int n, int K, int wlog, int fz, int fx) {
   so->active = false;
-  if (copy_team(ctx).size() < 2) return ALIFMM_OK;
-  const int W = 1 << wlog, nstr = (fx + W - 1) / W, own = (nstr + K - 1) / K;
-  int trlog = 2;
-  while (trlog < 14 && (long)own * ((fz + (1 << trlog) - 1) >> trlog) > 1024) trlog++;
-  const int ntz = (fz + (1 << trlog) - 1) >> trlog;
-  if ((long)own * ntz > 1024 || ((long)W << trlog) > 32768) return ALIFMM_OK;
-  const size_t members = (size_t)n * K, tile_bytes = ((size_t)W << trlog) * sizeof(double);
-  // 64 slots per member: the kernel may hold two staged, unpublished lists of up to 32 tiles when
-  // it asks for slots for the next ones (fmm_band_k.hip kTdCap); C4: 256 members x 64 x 64 KB = 1 GB
-  const int rslots = 64;
-  const size_t qcap = (size_t)own * ntz;
-  if (host_buf(&ctx->hstage, &ctx->hstage_bytes, members * rslots * tile_bytes) ||
-      host_buf((void**)&ctx->hq, &ctx->hq_bytes, members * qcap * sizeof(unsigned long long)) ||
+  if (copy_team(ctx).size() < 2 || !af::ts::plan(K, wlog, fz, fx, &so->g)) return ALIFMM_OK;
+  const af::ts::Geometry& g = so->g;
+  const size_t members = (size_t)n * K, tile_bytes = ((size_t)1 << g.clog()) * sizeof(double);
+  const size_t qbytes = members * g.qcap * sizeof(unsigned long long);
+  if (host_buf(&ctx->hstage, &ctx->hstage_bytes, members * g.rslots * tile_bytes) ||
+      host_buf((void**)&ctx->hq, &ctx->hq_bytes, qbytes) ||
       host_buf((void**)&ctx->hcons, &ctx->hcons_bytes, members * sizeof(unsigned))) {
     free_stream_bufs(ctx);
     return ALIFMM_OK;
   }
   // (the previous launch that used them has completed)
-  memset(ctx->hq, 0, members * qcap * sizeof(unsigned long long));
+  memset(ctx->hq, 0, qbytes);
   memset(ctx->hcons, 0, members * sizeof(unsigned));
-  so->K = K;
-  so->wlog = wlog;
-  so->trlog = trlog;
-  so->nstr = nstr;
-  so->ntz = ntz;
-  so->nz = fz;
-  so->nx = fx;
-  so->qcap = (int)qcap;
-  so->rslots = rslots;
   so->active = true;
   return ALIFMM_OK;
-}
-
-// copy-team thread w of nw: the queues of members w, w + nw, ... (member m = source * K + k owns
-// the stripes k, k + K, ...); each entry's tile goes from its ring slot to the caller's field, row
-// by row, and the slot is handed back.  Ends when every expected tile has arrived, or once the
-// launch has completed and a pass over the queues finds nothing new (the missing sources are then
-// copied from the device).
-static void stream_worker(alifmm_ctx* ctx, StreamOut* so, int w, int nw) {
-  struct Q {
-    int m, pos, expect;
-  };
-  std::vector<Q> qs;
-  long remaining = 0;
-  for (int m = w; m < so->n * so->K; m += nw) {
-    const int k = m % so->K;
-    const int nown = k < so->nstr ? (so->nstr - k + so->K - 1) / so->K : 0;
-    qs.push_back({m, 0, nown * so->ntz});
-    remaining += (long)nown * so->ntz;
-  }
-  const double* ring = static_cast<const double*>(ctx->hstage);
-  const int W = 1 << so->wlog, TR = 1 << so->trlog, clog = so->wlog + so->trlog;
-  int quiet = 0;
-  while (remaining > 0) {
-    bool any = false;
-    for (auto& q : qs) {
-      while (q.pos < q.expect) {
-        const unsigned long long v = __atomic_load_n(ctx->hq + (size_t)q.m * so->qcap + q.pos, __ATOMIC_ACQUIRE);
-        if ((long)(v >> 32) != (long)q.pos + 1) break;
-        const int t = (int)(unsigned)v, src = q.m / so->K;
-        const int tz = t / so->nstr, st = t - tz * so->nstr;
-        const int z0 = tz * TR, x0 = st * W;
-        const int rows = std::min(TR, so->nz - z0), cols = std::min(W, so->nx - x0);
-        double* d = so->dst[src];
-        const double* sp = ring + (((size_t)q.m * so->rslots + q.pos % so->rslots) << clog);
-        for (int r = 0; r < rows; r++)
-          memcpy(d + (size_t)(z0 + r) * so->nx + x0, sp + (size_t)r * W, (size_t)cols * sizeof(double));
-        q.pos++;
-        __atomic_store_n(ctx->hcons + q.m, (unsigned)q.pos, __ATOMIC_RELEASE);  // the slot is free
-        remaining--;
-        any = true;
-      }
-    }
-    if (any) {
-      quiet = 0;
-      continue;
-    }
-    if (so->kernel_done.load(std::memory_order_acquire)) {
-      if (++quiet > 1) break;
-    } else {
-      for (int i = 0; i < 64; i++) __builtin_ia32_pause();
-    }
-  }
-  for (auto& q : qs)
-    if (q.pos < q.expect) so->missing[q.m / so->K].store(1);
 }
 
 static void stream_start(alifmm_ctx* ctx, StreamOut* so) {
@@ -1121,7 +1050,11 @@ static void stream_start(alifmm_ctx* ctx, StreamOut* so) {
   so->missing.reset(new std::atomic<int>[so->n]);
   for (int i = 0; i < so->n; i++) so->missing[i].store(0);
   const int nw = team.size() - 1;
-  team.start([ctx, so, nw](int t) { stream_worker(ctx, so, t - 1, nw); });
+  const af::ts::Buffers b{static_cast<const double*>(ctx->hstage), ctx->hq, ctx->hcons};
+  team.start([so, b, nw](int t) {
+    af::ts::drain(so->g, so->n, so->dst, b, t - 1, nw,
+                  [so] { return so->kernel_done.load(std::memory_order_acquire) != 0; }, so->missing.get());
+  });
 }
 
 // the launch has completed (or failed): the workers finish the queues, then the team is joined

@@ -44,6 +44,7 @@
 #include "local_ops.h"
 #include "fields.h"
 #include "band_common.h"
+#include "tile_stream.h"
 
 namespace af {
 namespace kb {
@@ -164,8 +165,8 @@ constexpr int kCell = 0x7fffffff;
 
 // host streaming of final tiles (BandParams::hs): completed tiles staged per step (more wait for
 // the flush at the end), own tiles per member with an LDS counter
-constexpr int kTdCap = 32;
-constexpr int kTileMax = 1024;
+constexpr int kTdCap = ts::kListCap;
+constexpr int kTileMax = ts::kOwnTileMax;
 // AF_HS_VEC: 16-byte system-scope stores (1) or 8-byte (0)
 #ifndef AF_HS_VEC
 #define AF_HS_VEC 1
@@ -660,8 +661,8 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
     sh->nR = 0;
     sh->err = 0;
     sh->nrim[0] = sh->nrim[1] = 0;
-    // two lists of up to kTdCap tiles can be staged and not yet published when a third asks for
-    // slots: fewer slots could wait for the host forever (the host gives 2 kTdCap)
+    // a list may be staged and not yet published when the next asks for slots: fewer slots than
+    // two lists could wait for the host forever (tile_stream.h kRingSlots)
     if (hstream && P.rslots < 2 * kTdCap) sh->err = 11;
   }
   __syncthreads();

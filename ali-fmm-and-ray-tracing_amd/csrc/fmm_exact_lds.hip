@@ -515,9 +515,13 @@ AF_DEV long long walk(Lds* L, Heap& h, const DevModel& M, const XG& g, bool stag
 // earlier jobs' addtree / updtree before a fouds18_A() — the sequential order.
 AF_DEV void xpost(int* w, int v) { __hip_atomic_store(w, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP); }
 AF_DEV int xload(int* w) { return __hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP); }
+// polls back off with s_sleep(AF_XL_SLEEP) (0: spin)
+#ifndef AF_XL_SLEEP
+#define AF_XL_SLEEP 1
+#endif
 AF_DEV bool xawait_at_least(int* w, int v) {  // false: timeout (the other role is gone)
   for (long spins = 0; xload(w) < v; spins++) {
-    __builtin_amdgcn_s_sleep(1);
+    if (AF_XL_SLEEP) __builtin_amdgcn_s_sleep(AF_XL_SLEEP);
     if (spins > (1L << 28)) return false;
   }
   return true;
@@ -526,7 +530,7 @@ AF_DEV int xawait_change(int* w, int last) {  // the next value != last, or -2 o
   for (long spins = 0;; spins++) {
     const int v = xload(w);
     if (v != last) return v;
-    __builtin_amdgcn_s_sleep(1);
+    if (AF_XL_SLEEP) __builtin_amdgcn_s_sleep(AF_XL_SLEEP);
     if (spins > (1L << 28)) return -2;
   }
 }

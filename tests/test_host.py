@@ -290,3 +290,29 @@ def test_shutdown_keeps_library_mapped(monkeypatch):
     assert _alifmm.lib() is not None  # still usable after the teardown
     monkeypatch.setenv("ROCPROFILER_TEST_MARKER", "1")
     assert _alifmm._profiler_attached()
+
+
+@pytest.mark.parametrize("args", [
+    "3 2 6 300 333 1",       # K = 2, W = 64, ragged last stripe and tile row
+    "2 16 4 257 500 2",      # K = 16, W = 16: members with no stripe of their own at the edge
+    "1 1 6 64 64 3",         # one member
+    "4 4 6 1000 130 4",
+    "2 2 6 4096 4096 5",     # the C4 geometry (64 x 128 tiles, 1024 own tiles per member)
+])
+def test_stream_protocol_model(args, tmp_path):
+    """The host side of the band kernel's field streaming (csrc/tile_stream.h: tile plan, queue
+    drain, slot hand-back) against a CPU model of the kernel's side (tests/stream_sim.cpp: bursts
+    of completed tiles past a step's list, the end flush): every field arrives intact in reversed,
+    non-consecutive rows, and a ring one list too small is reported as a deadlock."""
+    import subprocess
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    exe = str(tmp_path / "stream_sim")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-pthread",
+                    "-I" + os.path.join(here, "..", "ali-fmm-and-ray-tracing_amd", "csrc"),
+                    os.path.join(here, "stream_sim.cpp"), "-o", exe], check=True)
+    r = subprocess.run([exe] + args.split(), capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout + r.stderr
+    if args.startswith("3 2"):
+        r = subprocess.run([exe] + args.split() + ["40", "2"], capture_output=True, text=True, timeout=120)
+        assert r.returncode == 1 and "deadlock=1" in r.stdout, r.stdout
