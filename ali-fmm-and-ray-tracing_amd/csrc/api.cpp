@@ -197,7 +197,6 @@ int alifmm_set_option(alifmm_ctx* ctx, const char* name, double value) {
   else if (!strcmp(name, "exact_r") && value >= 0 && value <= 48) ctx->exact_r = (int)value;
   else if (!strcmp(name, "exact_lds")) ctx->exact_lds = value != 0;
   else if (!strcmp(name, "stream_out")) ctx->stream_out = value != 0;
-  else if (!strcmp(name, "small_k") && value >= 0 && value <= af::kMaxK) ctx->small_k = (int)value;
   else if (!strcmp(name, "members") && value >= 0 && value <= af::kMaxK && value == (int)value)
     ctx->members = (int)value;
   else if (!strcmp(name, "stripe_log") && (value == 0 || (value >= 3 && value <= 12))) ctx->stripe_log = (int)value;
@@ -215,7 +214,6 @@ int alifmm_get_option(alifmm_ctx* ctx, const char* name, double* value) {
   else if (!strcmp(name, "exact_r")) *value = ctx->exact_r;
   else if (!strcmp(name, "exact_lds")) *value = ctx->exact_lds;
   else if (!strcmp(name, "stream_out")) *value = ctx->stream_out;
-  else if (!strcmp(name, "small_k")) *value = ctx->small_k;
   else if (!strcmp(name, "stream_tail_ms")) *value = ctx->t_stream_tail;      // last travel with a host destination
   else if (!strcmp(name, "stream_fallback")) *value = (double)ctx->stream_fallback;
   else if (!strcmp(name, "prof")) *value = ctx->prof;
@@ -722,8 +720,7 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
   HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
   if (fs != ctx->stream) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_fill, 0));
   HIPCHK(hipMemsetAsync(a.kx, 0, sizeof(af::KX) * n, ctx->stream));
-  HIPCHK(ctx->small_k > 0 && K >= ctx->small_k ? af_launch_band_k_small(&P, ctx->stream)
-                                                : af_launch_band_k(&P, ctx->stream));
+  HIPCHK(af_launch_band_k(&P, ctx->stream));
   // the copy team takes the tiles as they arrive; joined on every return path below
   struct StreamJoin {
     alifmm_ctx* c;

@@ -93,7 +93,6 @@ struct alifmm_ctx {
   int coop = 1;  // band kernel: cooperative launch (1; 0 under rocprofv3) or plain launch after a residency check (0)
   int members = 0;     // band kernel: workgroups per source (0: as many as the device fits, <= 16)
   int stripe_log = 0;  // band kernel: stripe width log2 (0: 6 for K <= 4, 4 for K >= 8)
-  int small_k = 0;     // band kernel: members per source from which the 256-thread build runs (0: never)
   int last_k = 0;      // members per source of the last band launch
   int n_cu = 0;
   long cap_scale = 1;

@@ -46,21 +46,8 @@
 #include "band_common.h"
 #include "tile_stream.h"
 
-// AF_BAND_SMALL (fmm_band_k_small.hip): the same kernel in its own namespace and launcher, built
-// for fewer threads per member (the host picks it for short steps, many members per source)
-#ifndef AF_BAND_SMALL
-#define AF_BAND_SMALL 0
-#endif
-#if AF_BAND_SMALL
-#define AF_KB kbs
-#define AF_BAND_LAUNCH af_launch_band_k_small
-#else
-#define AF_KB kb
-#define AF_BAND_LAUNCH af_launch_band_k
-#endif
-
 namespace af {
-namespace AF_KB {
+namespace kb {
 
 // Workgroups per CU (AF_WG_PER_CU): 1 = one 768-thread member per CU with the whole LDS; 2 = two
 // 384-thread members per CU (of any sources), each with half the LDS, so that one member's
@@ -1429,10 +1416,9 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
   }
 }
 
-}  // namespace AF_KB
+}  // namespace kb
 }  // namespace af
 
-#if !AF_BAND_SMALL
 // band-kernel workgroups one CU holds at once (the host sizes K so that every member is resident)
 extern "C" int af_band_wgs_per_cu() { return AF_WG_PER_CU; }
 
@@ -1444,26 +1430,25 @@ extern "C" long af_band_sb_cells(int nz, int nx) {
 extern "C" long af_band_tb_cells(int nz, int nx) {
   return AF_BRICK ? 16L * ((nz + 3) / 4) * ((nx + 3) / 4) : (long)nz * nx;
 }
-#endif
 
 // nsrc (padded to a multiple of 8) x K workgroups, AF_WG_PER_CU per CU, all resident
-extern "C" hipError_t AF_BAND_LAUNCH(const af::BandParams* P, hipStream_t stream) {
-  const bool lds = P->M.mid && P->M.mslo && P->M.nmat <= af::AF_KB::kMatLds && P->M.nstab <= af::AF_KB::kStabLds &&
-                   361 * P->M.ncol <= af::AF_KB::kPtabLds;
-  const dim3 g(8 * ((P->nsrc + 7) / 8) * P->K), b(af::AF_KB::kThreads);
+extern "C" hipError_t af_launch_band_k(const af::BandParams* P, hipStream_t stream) {
+  const bool lds = P->M.mid && P->M.mslo && P->M.nmat <= af::kb::kMatLds && P->M.nstab <= af::kb::kStabLds &&
+                   361 * P->M.ncol <= af::kb::kPtabLds;
+  const dim3 g(8 * ((P->nsrc + 7) / 8) * P->K), b(af::kb::kThreads);
   af::BandParams Pc = *P;
   void* args[] = {&Pc};
   const void* fn;
   if (P->mode == 0) {
-    fn = lds ? (P->prof ? (const void*)af::AF_KB::fmm_band_k_kernel<0, true, true>
-                        : (const void*)af::AF_KB::fmm_band_k_kernel<0, true, false>)
-             : (P->prof ? (const void*)af::AF_KB::fmm_band_k_kernel<0, false, true>
-                        : (const void*)af::AF_KB::fmm_band_k_kernel<0, false, false>);
+    fn = lds ? (P->prof ? (const void*)af::kb::fmm_band_k_kernel<0, true, true>
+                        : (const void*)af::kb::fmm_band_k_kernel<0, true, false>)
+             : (P->prof ? (const void*)af::kb::fmm_band_k_kernel<0, false, true>
+                        : (const void*)af::kb::fmm_band_k_kernel<0, false, false>);
   } else {
-    fn = lds ? (P->prof ? (const void*)af::AF_KB::fmm_band_k_kernel<1, true, true>
-                        : (const void*)af::AF_KB::fmm_band_k_kernel<1, true, false>)
-             : (P->prof ? (const void*)af::AF_KB::fmm_band_k_kernel<1, false, true>
-                        : (const void*)af::AF_KB::fmm_band_k_kernel<1, false, false>);
+    fn = lds ? (P->prof ? (const void*)af::kb::fmm_band_k_kernel<1, true, true>
+                        : (const void*)af::kb::fmm_band_k_kernel<1, true, false>)
+             : (P->prof ? (const void*)af::kb::fmm_band_k_kernel<1, false, true>
+                        : (const void*)af::kb::fmm_band_k_kernel<1, false, false>);
   }
   if (P->coop) return hipLaunchCooperativeKernel(fn, g, b, args, 0, stream);
   // Plain launch: the members of a source wait for each other every step, so every workgroup must
@@ -1475,7 +1460,7 @@ extern "C" hipError_t AF_BAND_LAUNCH(const af::BandParams* P, hipStream_t stream
   int dev = 0, ncu = 0, per_cu = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e == hipSuccess) e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-  if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, af::AF_KB::kThreads, 0);
+  if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, af::kb::kThreads, 0);
   if (e != hipSuccess) return e;
   if ((long)per_cu * ncu < (long)g.x) return hipErrorCooperativeLaunchTooLarge;
   return hipLaunchKernel(fn, g, b, args, 0, stream);

@@ -156,8 +156,6 @@ hipError_t af_launch_exact(const af::BandParams* P, hipStream_t stream);
 hipError_t af_launch_exact_lds(const af::BandParams* P, hipStream_t stream);
 int af_exact_lds_fits(int sg, int exact_r);  // fmm_exact_lds holds the stage grids of subgrid sg
 hipError_t af_launch_band_k(const af::BandParams* P, hipStream_t stream);
-// the same kernel built with 256-thread members (fmm_band_k_small.hip)
-hipError_t af_launch_band_k_small(const af::BandParams* P, hipStream_t stream);
 int af_band_wgs_per_cu(void);  // band-kernel workgroups resident per CU (fmm_band_k.hip AF_WG_PER_CU)
 // the band kernel's working-field layout: pitch and size (doubles) for an nz x nx main grid
 int af_band_tb_pitch(int nx);
