@@ -56,8 +56,7 @@ int alifmm_set_model(alifmm_ctx* ctx, int nnz, int nnx, const double* veln, cons
  * where the stage grids fit — subgrid <= 9; 0 = the HBM walk, fmm_exact.hip; bit-identical),
  * "coop" (band launch: 1 = cooperative, 0 = plain after a residency check), "cdelta_far" /
  * "r_far" (optional wider band beyond r_far cells; off by default), "stream_out" (subgrid-1 travels
- * with a host destination stream the fields out of the band kernel, alifmm_travel_into; default 1),
- * "small_k" (members per source from which the band kernel's 256-thread build runs; 0 = never). */
+ * with a host destination stream the fields out of the band kernel, alifmm_travel_into; default 1). */
 int alifmm_set_option(alifmm_ctx* ctx, const char* name, double value);
 /* Read an option, or "last_k" (workgroups per source of the last band launch), "n_cu"
  * (compute units of the device), "vmax" (the model's fastest speed [m/s]: the exact prefix
