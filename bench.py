@@ -1,7 +1,9 @@
 """Benchmark: grid-cell updates/s + sources/s on the 4096^2 anisotropic weld-like grid (BASELINE.json,
 config 4: "4096x4096 weld-like grid, 128 Tx sources sharded across 1/2/4/8 MI355X").
 
-One process per GPU (python -m torch.distributed.run ... bench.py --gpus N).  The 128 C4 sources
+One process per GPU: `python bench.py --gpus N` spawns its N ranks itself (launch_ranks; it refuses
+when fewer than N GPUs are visible), or runs as one rank of an outside launcher (python -m
+torch.distributed.run ... bench.py --gpus N, WORLD_SIZE set).  n_gpus = the ranks that ran.  The 128 C4 sources
 (z = 0, x = 16 + 32 k) are dealt block-cyclically over the N ranks, as the
 reference's update_parallel hands whole sources to its workers (Anis_TTF_rays.py:3938-4051), so
 the total work is fixed and the curve over N is STRONG scaling; --weak gives every rank its own
@@ -63,6 +65,79 @@ def parse():
     return ap.parse_args()
 
 
+_COUNT_GPUS = r"""
+import ctypes, sys
+try:
+    h = ctypes.CDLL("libamdhip64.so")
+except OSError:
+    try:
+        h = ctypes.CDLL("/opt/rocm/lib/libamdhip64.so")
+    except OSError:
+        print(0); sys.exit(0)
+n = ctypes.c_int(0)
+print(n.value if h.hipGetDeviceCount(ctypes.byref(n)) == 0 else 0)
+"""
+
+
+def visible_gpus():
+    """HIP devices this job sees, counted in a child process: the launching parent never
+    initialises the GPU (its children are the ranks)."""
+    import subprocess
+
+    try:
+        r = subprocess.run([sys.executable, "-c", _COUNT_GPUS], capture_output=True, text=True, timeout=120)
+        return int(r.stdout.strip().splitlines()[-1])
+    except (subprocess.SubprocessError, ValueError, IndexError):
+        return 0
+
+
+def _free_port():
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` run directly (no WORLD_SIZE in the environment, N > 1): one process per
+    GPU, LOCAL_RANK = RANK = 0 .. N-1 over a gloo group on 127.0.0.1, as the reference's
+    find_all_TTF_rays_parallel / update_parallel spawn their own n_threads workers
+    (Anis_TTF_rays.py:4550-4685, :3938-4051).  Refuses (exit 2) when fewer than N GPUs are visible,
+    unless ALIFMM_BENCH_DEVICE pins every rank to one device (rehearsal) or ALIFMM_BENCH_STUB asks
+    for the GPU-free stub ranks of the CPU tests.  Rank 0 prints the JSON line; the exit status is
+    the first failing rank's (the others are then stopped)."""
+    import signal
+    import subprocess
+
+    if "ALIFMM_BENCH_DEVICE" not in os.environ and "ALIFMM_BENCH_STUB" not in os.environ:
+        have = visible_gpus()
+        if have < n:
+            print("bench.py: --gpus %d but %d GPU(s) visible (set ALIFMM_BENCH_DEVICE=<dev> to rehearse "
+                  "every rank on one device)" % (n, have), file=sys.stderr, flush=True)
+            return 2
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port, ALIFMM_BENCH_LAUNCHED="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                for q in live:  # a failed rank leaves the others blocked in the group: stop them
+                    q.send_signal(signal.SIGTERM)
+        time.sleep(0.2)
+    return rc
+
+
 def max_over_ranks(value, dist=None):
     """Max of a float over all ranks of the default process group (identity without one)."""
     if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
@@ -72,6 +147,16 @@ def max_over_ranks(value, dist=None):
     t = torch.tensor([float(value)], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def _sum_over_ranks(value, dist=None):
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return int(value)
+    import torch
+
+    t = torch.tensor([int(value)], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return int(t.item())
 
 
 def rccl_gather_fields(ctx, n_local, subgrid, rank, world, dist, first_slot=0):
@@ -187,28 +272,56 @@ def cpu_baseline(args, scx, scz, model, vt, dnx, cells):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print("bench.py: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr, flush=True)
+        sys.exit(2)
     dist = None
     if world > 1:
         import torch  # noqa: F401  (before the library: one HIP runtime for both, see rccl_gather_fields)
         import torch.distributed as dist
 
         dist.init_process_group("gloo", rank=rank, world_size=world)
+    stub = "ALIFMM_BENCH_STUB" in os.environ
+    # ranks that reached this point (the group's size is what was asked; this is what ran)
+    ran = _sum_over_ranks(1, dist)
+    if stub:  # CPU tests of the launcher: the source deal without a GPU
+        scx, _, ids = rank_sources(args, rank, world, 1.0)
+        got = [None] * world
+        if dist is not None:
+            dist.all_gather_object(got, [int(i) for i in ids])
+        else:
+            got = [[int(i) for i in ids]]
+        if rank == 0:
+            print(json.dumps({"stub": True, "n_gpus": ran, "sources_per_rank": got}), flush=True)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
 
     import _alifmm
     import sharding
     import workloads as W
 
+    # one GPU per rank (LOCAL_RANK); ALIFMM_BENCH_DEVICE pins every rank to one device, only to
+    # rehearse the multi-process path on a one-GPU box
+    dev = int(os.environ.get("ALIFMM_BENCH_DEVICE", local))
+    have = _alifmm.device_count()
+    if dev >= have:
+        print("bench.py: rank %d needs device %d, %d visible" % (rank, dev, have), file=sys.stderr, flush=True)
+        sys.exit(3)
     n = args.n
     model = W.weldlike_model(n)
     dnx = W.weldlike_dnx()
     vt = W.default_table()
-    # one GPU per rank (LOCAL_RANK); ALIFMM_BENCH_DEVICE pins every rank to one device, only to
-    # rehearse the multi-process path on a one-GPU box
-    dev = int(os.environ.get("ALIFMM_BENCH_DEVICE", local))
     ctx = _alifmm.Context(dev)
+    devices = [dev]
+    if dist is not None:
+        devices = [None] * world
+        dist.all_gather_object(devices, dev)
     if args.cdelta is not None:
         ctx.set_option("cdelta", args.cdelta)
     if args.members is not None:
@@ -322,7 +435,8 @@ def main():
             "metric": "grid-cell updates/sec + sources/sec on 4096^2 anisotropic grid",
             "value": value,
             "unit": "grid-cell updates/s",
-            "n_gpus": world,
+            "n_gpus": ran,
+            "devices": devices,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": dt / args.steps * 1e3,

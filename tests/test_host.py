@@ -316,3 +316,38 @@ def test_stream_protocol_model(args, tmp_path):
     if args.startswith("3 2"):
         r = subprocess.run([exe] + args.split() + ["40", "2"], capture_output=True, text=True, timeout=120)
         assert r.returncode == 1 and "deadlock=1" in r.stdout, r.stdout
+
+
+def _bench(args, env_extra, timeout=240):
+    import subprocess
+    import sys
+
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "ALIFMM_BENCH_DEVICE",
+                                                            "ALIFMM_BENCH_STUB")}
+    env.update(env_extra)
+    return subprocess.run([sys.executable, os.path.join(REPO, "bench.py")] + args, env=env, capture_output=True,
+                          text=True, timeout=timeout)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_launches_its_own_ranks(world):
+    """`python bench.py --gpus N` without an outside launcher spawns N ranks itself (gloo on
+    127.0.0.1), deals C4's 128 sources block-cyclically over them and reports n_gpus = the ranks
+    that ran (stub ranks: the launcher and the deal, no GPU)."""
+    import json
+
+    r = _bench(["--gpus", str(world)], {"ALIFMM_BENCH_STUB": "1"})
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["n_gpus"] == world
+    per = line["sources_per_rank"]
+    assert len(per) == world and sorted(sum(per, [])) == list(range(128))
+    assert max(map(len, per)) - min(map(len, per)) <= 1
+
+
+def test_bench_refuses_more_gpus_than_visible():
+    """--gpus N with fewer than N visible GPUs (none in this container) exits non-zero before any
+    rank starts, unless ALIFMM_BENCH_DEVICE pins the ranks to one device for a rehearsal."""
+    r = _bench(["--gpus", "2", "--steps", "1"], {})
+    assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
+    assert "GPU(s) visible" in r.stderr
