@@ -83,6 +83,9 @@ static const int kMaxRayCand = 256;
 // ray point buffers larger than this are freed at the end of each alifmm_find_rays call
 static const size_t kRayBufKeepBytes = (size_t)1 << 30;
 
+// contexts alive in this process (copy teams share the process's CPU share between them)
+static std::atomic<int> g_live_ctx{0};
+
 extern "C" {
 
 const char* alifmm_version(void) { return "alifmm-mi355x 0.1 (gfx950)"; }
@@ -121,6 +124,7 @@ int alifmm_ctx_create(int device, alifmm_ctx** out) {
   ctx->coop = 1;
   for (char** e = environ; e && *e; e++)
     if (!strncmp(*e, "ROCPROF", 7) || !strncmp(*e, "ROCP_", 5)) ctx->coop = 0;
+  g_live_ctx++;
   *out = ctx;
   return ALIFMM_OK;
 }
@@ -156,6 +160,7 @@ static void destroy_team(alifmm_ctx* ctx);
 
 int alifmm_ctx_destroy(alifmm_ctx* ctx) {
   if (!ctx) return ALIFMM_OK;
+  g_live_ctx--;
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
   destroy_team(ctx);
@@ -216,6 +221,7 @@ int alifmm_get_option(alifmm_ctx* ctx, const char* name, double* value) {
   else if (!strcmp(name, "stream_out")) *value = ctx->stream_out;
   else if (!strcmp(name, "stream_tail_ms")) *value = ctx->t_stream_tail;      // last travel with a host destination
   else if (!strcmp(name, "stream_fallback")) *value = (double)ctx->stream_fallback;
+  else if (!strcmp(name, "exact_redo")) *value = (double)ctx->exact_redo;
   else if (!strcmp(name, "prof")) *value = ctx->prof;
   else if (!strcmp(name, "coop")) *value = ctx->coop;
   else if (!strcmp(name, "members")) *value = ctx->members;
@@ -705,6 +711,7 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
       HIPCHK(hipStreamSynchronize(ctx->stream));
       bool redo = false;
       for (int i = 0; i < n; i++) redo |= chk[i].err == 9;
+      for (int i = 0; i < n; i++) ctx->exact_redo += chk[i].err == 9;
       if (redo) {
         for (int i = 0; i < n; i++) {
           HIPCHK(hipMemsetAsync(hs[i].T, 0xFF, (size_t)cells * 8, ctx->stream));
@@ -726,7 +733,12 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
     alifmm_ctx* c;
     StreamOut* s;
     ~StreamJoin() {
-      if (s) stream_finish(c, s);
+      if (!s) return;
+      // an early return: the kernel may still store into the pinned ring; it must have ended
+      // before the drain stops and the next call resets or frees those buffers
+      (void)hipStreamSynchronize(c->stream);
+      (void)hipGetLastError();
+      stream_finish(c, s);
     }
   } sjoin{ctx, nullptr};
   if (so && so->active) {
@@ -809,6 +821,7 @@ static int travel_impl(alifmm_ctx* ctx, int subgrid, int nsrc, const double* scx
   }
   ctx->t_stream_tail = 0;
   ctx->stream_fallback = 0;
+  ctx->exact_redo = 0;
   HIPCHK(hipEventRecord(ctx->ev[3], ctx->stream));
   // the call's timing events, destroyed on every return path
   struct Ev {
@@ -984,11 +997,14 @@ class CopyTeam {
 
 static CopyTeam& copy_team(alifmm_ctx* ctx) {
   if (!ctx->team) {
+    // the process's CPU share (OMP_NUM_THREADS on the GPU box, else up to 8) split over the live
+    // contexts (one per GPU in update_parallel), at least two threads per team (caller + one)
     int n = (int)std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
     if (const char* e = getenv("OMP_NUM_THREADS")) {
       const int v = atoi(e);
       if (v >= 1) n = std::min(v, 32);
     }
+    n = std::max(2, n / std::max(1, g_live_ctx.load()));
     ctx->team = new CopyTeam(n);
   }
   return *static_cast<CopyTeam*>(ctx->team);

@@ -213,13 +213,17 @@ static int gather_check(alifmm_comm* comm, int root, int subgrid, const int* fir
 
 int alifmm_gather_fields(alifmm_comm* comm, int root, int subgrid, const int* first_slot, const int* count,
                          int dst_slot, double* ms) {
-  if (!comm || !first_slot || !count || root < 0 || root >= comm->nranks || dst_slot < 0)
-    return cfail(comm, ALIFMM_E_ARG, "gather_fields: bad arguments");
+  // only a missing communicator or RCCL library returns at once; every other failed check still
+  // joins the ranks' agreement below with a failing flag (a rank returning alone would leave its
+  // peers blocked in the AllReduce)
+  if (!comm) return ALIFMM_E_ARG;
   Rccl& R = rccl();
   if (!R.ok) return cfail(comm, ALIFMM_E_HIP, "RCCL unavailable: %s", R.why.c_str());
   const int G = comm->nranks;
   std::vector<long> off(G + 1, 0);  // root slot of rank r's first field: dst_slot + off[r]
   int rc = ALIFMM_OK;
+  if (!first_slot || !count || root < 0 || root >= G || dst_slot < 0)
+    rc = cfail(comm, ALIFMM_E_ARG, "gather_fields: bad arguments");
   for (int r = 0; r < G && !rc; r++) {
     if (count[r] < 0 || first_slot[r] < 0) rc = cfail(comm, ALIFMM_E_ARG, "gather_fields: rank %d count/slot", r);
     off[r + 1] = off[r] + std::max(count[r], 0);

@@ -137,6 +137,7 @@ struct alifmm_ctx {
   size_t hcons_bytes = 0;
   double t_stream_tail = 0;  // last travel_into: ms from the band kernel's end to the last tile copied
   long stream_fallback = 0;  // last travel_into: fields copied after the kernel (not streamed)
+  long exact_redo = 0;       // last travel (subgrid > 1): sources the LDS exact walk handed to the HBM walk
 };
 
 static inline int fail(alifmm_ctx* c, int code, const char* fmt, ...) {

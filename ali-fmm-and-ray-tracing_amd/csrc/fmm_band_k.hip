@@ -206,6 +206,7 @@ struct Lds {
   int qpos;      // tiles published (host queue entries written)
   int spos, nst; // tiles staged before this step; tiles staged this step
   int cons;      // tiles the host has taken out of the ring (last read)
+  int hsoff;     // streaming given up (ring_space timed out): no more staging or publishing
   double tmin_g, thr;
   unsigned long long nE2;  // claimed-list lengths: interior (low half), boundary (high half)
   int nA, nF, hi, taken, nD, nR, nRx, live_g, err_g, err, nFb;
@@ -428,9 +429,9 @@ AF_DEV void ring_space(Lds* sh, const TileStream& ts, int i0, int n) {
     sh->cons = (int)__hip_atomic_load(ts.cons, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (i0 + n - sh->cons <= ts.rslots) break;
     __builtin_amdgcn_s_sleep(2);
-    if (spins > (1L << 24)) {  // the host stopped taking tiles
-      sh->err = 11;
-      sh->cons = i0 + n;
+    if (spins > (1L << 24)) {  // the host stopped taking tiles: this member streams no more
+      sh->hsoff = 1;           // (its source's tiles count as missing: the host copies the field
+      return;                  // after the launch), the band itself carries on
     }
   }
 }
@@ -654,7 +655,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
   }
   if (tid == 0) {
     sh->nTd[0] = sh->nTd[1] = 0;
-    sh->qpos = sh->spos = sh->nst = sh->cons = 0;
+    sh->qpos = sh->spos = sh->nst = sh->cons = sh->hsoff = 0;
     sh->hi = 0;
     sh->nF = 0;
     sh->nD = 0;
@@ -792,7 +793,8 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
       sh->spos += sh->nst;
       const int nT = min(sh->nTd[prv], kTdCap);
       sh->nst = nT;
-      if (nT > 0) ring_space(sh, ts, sh->spos, nT);
+      if (nT > 0 && !sh->hsoff) ring_space(sh, ts, sh->spos, nT);
+      if (sh->hsoff) sh->nst = sh->nTd[0] = sh->nTd[1] = 0;
     }
     // ---- P1: local Tmin over the close set (LDS); publish every own close RIM cell (cell, T) for
     // the neighbour members, which keep those with T <= thr; clear the claim hash ----
@@ -835,7 +837,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
 #if !AF_PROF_FBWAIT && !AF_PROF_SPILL
     AF_SUBT(3, tdr)
 #endif
-    if (hstream) {
+    if (hstream && !sh->hsoff) {
       // publish the tiles staged last step (their stores have drained: the wait above), then stage
       // the ones completed last step (slots reserved in P0h)
       if (wv == 0 && sh->nTd[par] > 0) publish_tiles(sh, ts, par, lane);
@@ -1368,7 +1370,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
   // host streaming: every own tile not yet published (incomplete: cells never reached; past a
   // step's list; or staged in the last steps), in windows of kTdCap tiles, each published once
   // its stores have drained
-  if (hstream) {
+  if (hstream && !sh->hsoff) {
     // the last step's staged list: its stores drained (every wave), then published
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -1389,6 +1391,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
       if (nT > 0) {
         if (tid == 0) ring_space(sh, ts, sh->spos, nT);
         __syncthreads();
+        if (sh->hsoff) break;  // (uniform: read after the barrier)
         stage_tiles(sh, nT, 0, sh->spos, ts, Tb, TL, tid);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();

@@ -447,8 +447,12 @@ AF_DEV long long walk(Lds* L, Heap& h, const DevModel& M, const XG& g, bool stag
     ntr = __shfl(ntr, 0);
     const int iz = g.gz(c), ix = g.gx(c);
     if (!stage && ((g.wz0 > 0 && iz - g.wz0 < 3) || (g.wz0 + g.wh < g.nz && g.wz0 + g.wh - 1 - iz < 3) ||
-                   (g.wx0 > 0 && ix - g.wx0 < 3) || (g.wx0 + g.ww < g.nx && g.wx0 + g.ww - 1 - ix < 3)))
-      break;  // the window holds no more of the prefix (the band kernel goes on from the heap)
+                   (g.wx0 > 0 && ix - g.wx0 < 3) || (g.wx0 + g.ww < g.nx && g.wx0 + g.ww - 1 - ix < 3))) {
+      // the window edge before tstop (the root key is still below it): the HBM walk redoes the
+      // source (error 9), so the hand-over is the reference's prefix to tstop
+      if (lane == 0) h.err = 9;
+      break;
+    }  // the window holds no more of the prefix (the band kernel goes on from the heap)
     // lanes 0..3: neighbour x-1, x+1, z-1, z+1; statuses read before downtree (fmm_exact.hip)
     const int kz = lane == 2 ? iz - 1 : lane == 3 ? iz + 1 : iz;
     const int kx = lane == 0 ? ix - 1 : lane == 1 ? ix + 1 : ix;
@@ -559,8 +563,12 @@ AF_DEV long long heap_role(Lds* L, Heap& h, const XG& g, bool stage, int isx_s, 
     c = __shfl(c, 0);
     const int iz = g.gz(c), ix = g.gx(c);
     if (!stage && ((g.wz0 > 0 && iz - g.wz0 < 3) || (g.wz0 + g.wh < g.nz && g.wz0 + g.wh - 1 - iz < 3) ||
-                   (g.wx0 > 0 && ix - g.wx0 < 3) || (g.wx0 + g.ww < g.nx && g.wx0 + g.ww - 1 - ix < 3)))
+                   (g.wx0 > 0 && ix - g.wx0 < 3) || (g.wx0 + g.ww < g.nx && g.wx0 + g.ww - 1 - ix < 3))) {
+      // the window edge before tstop (the root key is still below it): the HBM walk redoes the
+      // source (error 9), so the hand-over is the reference's prefix to tstop
+      if (lane == 0) h.err = 9;
       break;
+    }
     const int kz = lane == 2 ? iz - 1 : lane == 3 ? iz + 1 : iz;
     const int kx = lane == 0 ? ix - 1 : lane == 1 ? ix + 1 : ix;
     const bool inb = lane < 4 && (lane < 2 ? (0 <= kx && kx <= g.nx - 1) : (0 <= kz && kz <= g.nz - 1));

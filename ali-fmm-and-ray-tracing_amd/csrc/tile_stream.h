@@ -13,6 +13,7 @@
 #pragma once
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstring>
 #include <thread>
 #include <vector>
@@ -71,6 +72,15 @@ inline void relax_cpu() {
 #endif
 }
 
+// an idle pass over the queues: spin briefly, then yield, then sleep.  A member publishes a tile
+// every ~0.4 ms at C4 and its ring holds 64, so a 50 us nap loses nothing; it keeps a context per
+// GPU (update_parallel: one process, up to 8 teams) from spinning ~120 threads on a 16-CPU share
+inline void idle_wait(int idle) {
+  if (idle < 32) relax_cpu();
+  else if (idle < 64) std::this_thread::yield();
+  else std::this_thread::sleep_for(std::chrono::microseconds(50));
+}
+
 // Copy thread w of nw: the queues of members w, w + nw, ... of a launch of nsrc sources; each
 // entry's tile goes from its slot into dst[source], row by row, and the slot is handed back.
 // Ends when every expected tile has arrived, or once kernel_done() and a pass over the queues
@@ -89,7 +99,7 @@ void drain(const Geometry& g, int nsrc, double* const* dst, const Buffers& b, in
     remaining += qs.back().expect;
   }
   const int W = g.W(), TR = g.TR();
-  int quiet = 0;
+  int quiet = 0, idle = 0;
   while (remaining > 0) {
     bool any = false;
     for (auto& q : qs) {
@@ -111,13 +121,13 @@ void drain(const Geometry& g, int nsrc, double* const* dst, const Buffers& b, in
       }
     }
     if (any) {
-      quiet = 0;
+      quiet = idle = 0;
       continue;
     }
     if (kernel_done()) {
       if (++quiet > 1) break;
     } else {
-      relax_cpu();
+      idle_wait(idle++);
     }
   }
   for (auto& q : qs)

@@ -59,6 +59,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-return", action="store_true", help="skip the result-return measurement")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end ALI_FMM.update() measurement")
+    ap.add_argument("--no-c3", action="store_true", help="skip the BASELINE config 3 line (N = 1)")
     ap.add_argument("--gather", action="store_true", help="N > 1: also time an RCCL gather of all fields to rank 0")
     ap.add_argument("--members", type=int, default=None, help="band-kernel workgroups per source (0: auto)")
     ap.add_argument("--cdelta", type=float, default=None)
@@ -232,6 +233,45 @@ def _host_cpus():
     except OSError:
         pass
     return usable, quota, len(cores) or os.cpu_count(), os.cpu_count()
+
+
+def c3_line(ctx, W):
+    """BASELINE config 3 (2048^2 Voronoi grains, anisotropic, one interior source; all CUs on the
+    one source: K band members) after the timed C4 steps: init / band kernel times (in-library HIP
+    events, best of 3 after a warm-up), cell-sweeps and the band kernel's roofline at SURVEY
+    §8(d)'s 18.1 B per sweep; the field against the reference's own (tests/golden/c3_2048,
+    decimated x8) as a sanity figure (tests/test_gpu_parity.py holds the parity check)."""
+    ctx.release_fields()
+    vt = W.default_table()
+    ctx.set_model(*W.c3_model(), vt, vt, 1e-3)
+    x, z = W.c3_source()
+    ctx.travel([x], [z], copy_out=False)
+    best = None
+    for _ in range(3):
+        ctx.travel([x], [z], copy_out=False)
+        t = ctx.last_timing()
+        best = t if best is None or t[2] < best[2] else best
+    st = ctx.source_stats(0)
+    sweeps = int(st[1])
+    out = {"workload": "C3: 2048x2048 Voronoi grains (rng 1234, 128 seeds), velpn 0, one source (x=%d, z=%d)"
+                       % (round(x / 1e-3), round(z / 1e-3)),
+           "init_ms": best[0], "band_ms": best[1], "total_ms": best[2], "band_workgroups": int(ctx.get_option("last_k")),
+           "band_steps": int(st[0][3]), "cell_sweeps": sweeps,
+           "roofline": {"bound": "hbm", "kernel": "fmm_band_k_kernel", "bytes_per_cell_sweep": BYTES_PER_SWEEP,
+                        "achieved": BYTES_PER_SWEEP * sweeps / (best[1] * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s"}}
+    out["roofline"]["frac"] = out["roofline"]["achieved"] / HBM_PEAK_GBS
+    try:
+        R = np.load(os.path.join(REPO, "tests", "golden", "c3_2048.npz"))["field_dec8"]
+        D = ctx.get_field(0, 1)[::8, ::8]
+        zz, xx = np.mgrid[0:D.shape[0], 0:D.shape[1]]
+        m = np.hypot(zz - z / 1e-3 / 8, xx - x / 1e-3 / 8) > 1
+        rel = np.abs(D[m] - R[m]) / R[m]
+        out.update({"field_vs_reference_rel_max_dec8": float(rel.max()), "field_vs_reference_rel_mean_dec8": float(rel.mean())})
+    except OSError:
+        pass
+    ctx.release_fields()
+    return out
 
 
 def cpu_baseline(args, scx, scz, model, vt, dnx, cells):
@@ -427,6 +467,9 @@ def main():
         del F
         for c in M._ctxs.values():
             c.close()
+    c3 = None
+    if world == 1 and not args.no_c3:
+        c3 = c3_line(ctx, W)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args, scx, scz, model, vt, dnx, cells)
@@ -467,6 +510,7 @@ def main():
                                         if valu and band_avg_s > 0 else None)},
             "result_return": ret,
             "update_end_to_end": e2e,
+            "c3": c3,
             "cpu_baseline": cpu,
         }
         if cpu:

@@ -550,6 +550,29 @@ def test_sharded_contexts_bit_identical(A, monkeypatch):
                 np.testing.assert_array_equal(a, b)
 
 
+@pytest.mark.gpu
+def test_sharded_contexts_bit_identical_c4(A, monkeypatch):
+    """The same on BASELINE C4 (4096^2 weld-like, sources at z = 0): six of the 128 bench sources
+    through update() on one context and through update_parallel() dealt over two contexts
+    (ALIFMM_DEVICE_MAP=0,0 — the 2-GPU deal on one device) give bit-identical fields, although the
+    two runs use different band-member counts per source (6 sources on one context vs 3 per
+    context)."""
+    veln, velpn, vm, sd = W.weldlike_model()
+    dnx = W.weldlike_dnx()
+    sx, sz = W.c4_sources(128)
+    sel = [0, 1, 40, 64, 100, 127]
+    sx, sz = sx[sel], sz[sel]
+    M1 = A.ALI_FMM(veln, velpn, vm, sx, sz, stif_den=sd, dnx=dnx)
+    F1 = M1.update(veln, velpn, vm, stif_den=sd, subgrid_size=1)
+    monkeypatch.setenv("ALIFMM_DEVICE_MAP", "0,0")
+    M2 = A.ALI_FMM(veln, velpn, vm, sx, sz, stif_den=sd, dnx=dnx)
+    assert M2._devices(8) == [0, 1]
+    F2 = M2.update_parallel(veln, velpn, vm, stif_den=sd, subgrid_size=1, n_threads=2)
+    assert F1.shape == (6, 4096, 4096)
+    np.testing.assert_array_equal(F2, F1)
+    assert np.isfinite(F1).all()
+
+
 @pytest.mark.parametrize("n", [61, 81])
 def test_many_materials_paths(ctx, envelope, n):
     """Models past the kernels' LDS material tables: per-cell random orientations give n^2 distinct
