@@ -36,6 +36,10 @@ constexpr int kThreads = 256;  // 4 waves clear and hand over; wave 0 walks
 #ifndef AF_XL_DIAG
 #define AF_XL_DIAG 0  // diagnostic build: cycle counters of the walk (walk(), BandSrc::ph / sub)
 #endif
+// a stale speculative entry's stencil stage re-run across the wavefront (1) or on its lane (0)
+#ifndef AF_XL_PARSEL
+#define AF_XL_PARSEL 1
+#endif
 #ifndef AF_XL_TWO_ROLE
 #define AF_XL_TWO_ROLE 1  // heap wavefront + relax wavefront (1), or one wavefront doing both (0)
 #endif
@@ -371,17 +375,30 @@ AF_DEV double relax_value(Lds* L, const DevModel& M, const XG& g, Spec& sp, int 
   if (hm) {
     const int e = __ffsll((long long)hm) - 1;
     int pth = 0;
-    if (lane == e && sp.dirty) {
-      NbFieldT nb;
-      stencil_from_lds(L, sp, nb, lane);
-      const UpdSel s2 = update_nb_select(nb, sp.z, sp.x, g.nz, g.nx);
-      pth = 1;
-      if (!s2.same(sp.sel)) {
-        sp.v = update_nb_finish(M, sp.cm, sp.z, sp.x, g.dnx, s2);
-        sp.sel = s2;
-        pth = 2;
+    if (__builtin_amdgcn_readlane((int)sp.dirty, e)) {
+      // the patched stencil's stage again, spread over the wavefront (lane k < 12: slot k of the
+      // entry's stencil; lanes 0..7 a square stencil each), on the entry's lane where update()
+      // runs its triangular stage
+      const unsigned vm_e = (unsigned)__builtin_amdgcn_readlane((int)sp.vm, e);
+      const int z_e = __builtin_amdgcn_readlane(sp.z, e), x_e = __builtin_amdgcn_readlane(sp.x, e);
+      const double tk = lane < 12 ? L->stn[lane][e] : 0.0;
+      const bool vk = lane < 12 && ((vm_e >> lane) & 1u);
+      UpdSel s2;
+      const bool par = AF_XL_PARSEL && update_select_lanes(tk, vk, z_e, x_e, g.nz, g.nx, lane, s2);
+      if (lane == e) {
+        if (!par) {
+          NbFieldT nb;
+          stencil_from_lds(L, sp, nb, lane);
+          s2 = update_nb_select(nb, sp.z, sp.x, g.nz, g.nx);
+        }
+        pth = 1;
+        if (!s2.same(sp.sel)) {
+          sp.v = update_nb_finish(M, sp.cm, sp.z, sp.x, g.dnx, s2);
+          sp.sel = s2;
+          pth = 2;
+        }
+        sp.dirty = false;
       }
-      sp.dirty = false;
     }
     path = __builtin_amdgcn_readlane(pth, e);
     return rlane(sp.v, e);

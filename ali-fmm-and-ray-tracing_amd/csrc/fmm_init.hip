@@ -30,6 +30,17 @@ constexpr int kInitStab = 64;         // stiffness rows staged in LDS
 #ifndef AF_INIT_DIAG
 #define AF_INIT_DIAG 0
 #endif
+// the heap role runs on its whole wavefront: addtree / updtree sift-ups (AF_INIT_PARSIFT) and the
+// pop's neighbour classification (AF_INIT_PARCLS) spread over the lanes (0: one lane's loops)
+#ifndef AF_INIT_PARSIFT
+#define AF_INIT_PARSIFT 1
+#endif
+#ifndef AF_INIT_PARCLS
+#define AF_INIT_PARCLS 1
+#endif
+#ifndef AF_INIT_PARDOWN
+#define AF_INIT_PARDOWN 1
+#endif
 #if AF_INIT_DIAG
 #define AF_DG_T0(v) const long long v = clock64();
 #define AF_DG_ADD(L, k, v) (L)->dg[k] += clock64() - (v);
@@ -88,6 +99,53 @@ struct Heap {
   AF_DEV int bx(int k) const { return L->hcell[k] & 255; }
   AF_DEV double tb(int k) const { return L->hkey[k]; }
   AF_DEV static int parent(int t) { return (int)rint((double)t / 2.0); }  // half-even (:123)
+  // the same in integers: t / 2 rounded half to even
+  AF_DEV static int parent_i(int t) { return (t >> 1) + ((t & (t >> 1)) & 1); }
+  // sift_up on the heap role's whole wavefront (every lane calls it, wave-uniform arguments): lane
+  // i reads the i-th ancestor's key and node in one LDS round trip, a ballot of "tv < key" finds
+  // how far the entry rises (the first ancestor it does not beat stops it, as in the loop), and
+  // the ancestors it passes move down one place each in one round of stores.  Heap indices and
+  // statuses end as the loop leaves them; a node with two entries (ndup) takes the loop (the
+  // order of its two status writes decides which index it keeps).
+  AF_DEV void sift_up_par(int iz, int ix, int tpc) {
+    const int lane = threadIdx.x & 63;
+    const unsigned short mc = (unsigned short)((iz << 8) | ix);
+    const double tv = L->hkey[tpc];
+    int anc = 0, depth = 0;
+    for (int t = parent_i(tpc); t > 0; t = parent_i(t)) {
+      anc = lane == depth ? t : anc;
+      depth++;
+    }
+    const bool have = lane < depth;
+    const double k = have ? L->hkey[anc] : 0.0;
+    const int cc = have ? (int)L->hcell[anc] : 0;
+    const unsigned long long m = __ballot(have && tv < k);
+    const int j = __builtin_ctzll(~m);
+    if (j == 0) {
+      if (lane == 0) {
+        L->hcell[tpc] = mc;
+        L->hkey[tpc] = tv;
+      }
+      return;
+    }
+    int below = __shfl_up(anc, 1);
+    if (lane == 0) below = tpc;
+    if (lane < j) {
+      L->hcell[below] = (unsigned short)cc;
+      L->hkey[below] = k;
+      L->S[(cc >> 8) * nx + (cc & 255)] = (short)below;
+    }
+    const int fin = __builtin_amdgcn_readlane(anc, j - 1);
+    if (lane == 0) {
+      L->S[iz * nx + ix] = (short)fin;
+      L->hcell[fin] = mc;
+      L->hkey[fin] = tv;
+    }
+  }
+  AF_DEV void sift(int iz, int ix, int tpc) {
+    if (AF_INIT_PARSIFT && ndup == 0) sift_up_par(iz, ix, tpc);
+    else sift_up(iz, ix, tpc);
+  }
   // The moving entry stays in registers while it sifts: one round of LDS reads per level (the
   // other entry's key and node), the status writes in the reference's order.
   AF_DEV void sift_up(int iz, int ix, int tpc) {
@@ -121,13 +179,13 @@ struct Heap {
     L->S[iz * nx + ix] = (short)ntr;
     L->hcell[ntr] = (unsigned short)((iz << 8) | ix);
     L->hkey[ntr] = L->T[iz * nx + ix];
-    sift_up(iz, ix, ntr);
+    sift(iz, ix, ntr);
   }
   // updtree :141-175
   AF_DEV void upd(int iz, int ix) {
     const int tpc = L->S[iz * nx + ix];
     L->hkey[tpc] = L->T[iz * nx + ix];
-    sift_up(iz, ix, tpc);
+    sift(iz, ix, tpc);
   }
   // a node's ttn changed: every heap entry of a node with two entries takes the new value
   AF_DEV void sync(int iz, int ix) {
@@ -138,6 +196,80 @@ struct Heap {
     const double t = L->T[iz * nx + ix];
     for (int k = 1; k <= ntr; k++)
       if (L->hcell[k] == c) L->hkey[k] = t;
+  }
+  // downtree on the heap role's whole wavefront (every lane calls it): the last entry sinks along
+  // the path of smaller children from the root (the right child only when strictly smaller), which
+  // does not depend on the sinking key, until a child does not beat it.  The path is followed five
+  // levels at a time: lanes 0..61 read the keys of the 62 nodes of the next five levels below the
+  // current node in one LDS round trip and the wavefront walks them with readlane; then the path
+  // entries move up one level each in one round of stores.  Same heap and statuses as down();
+  // nodes with two entries (ndup) take down().
+  AF_DEV void down_par() {
+    if (ntr == 1) {
+      ntr -= 1;
+      return;
+    }
+    const int lane = threadIdx.x & 63;
+    const unsigned short mc = L->hcell[ntr];
+    const double km = L->hkey[ntr];
+    ntr -= 1;
+    // lane j < 62 of a chunk: level l = 1..5 below q, node q * 2^l + r
+    const int jl = lane + 2, lvl = 31 - __builtin_clz(jl), r = jl - (1 << lvl);
+    int q = 1, moves = 0, path = 0;
+    double pk = 0.0;  // key of path node `moves` (lane = move index)
+    bool go = true;
+    while (go) {
+      const int node = (q << lvl) + r;
+      const double key = (lane < 62 && node <= ntr) ? L->hkey[node] : 0.0;
+#pragma unroll 1
+      for (int l = 0; l < 5; l++) {
+        // children of the current node q (level l + 1 below the chunk's root)
+        const int c1 = 2 * q;
+        if (c1 > ntr) {
+          go = false;
+          break;
+        }
+        const int base = (1 << (l + 1)) - 2;                   // chunk lane of level l + 1's first node
+        const int o1 = base + (c1 - (((c1 >> (l + 1)) << (l + 1))));  // c1 - q0 * 2^(l+1)
+        const double k1 = lane_d(key, o1);
+        int t = c1;
+        double kc = k1;
+        if (c1 < ntr) {
+          const double k2 = lane_d(key, o1 + 1);
+          if (k1 > k2) {
+            t = c1 + 1;
+            kc = k2;
+          }
+        }
+        if (!(kc < km)) {
+          go = false;
+          break;
+        }
+        path = lane == moves ? t : path;
+        pk = lane == moves ? kc : pk;
+        moves++;
+        q = t;
+      }
+    }
+    // move i: the entry at path[i] goes up to its parent on the path (1 for the first)
+    int up = __shfl_up(path, 1);
+    if (lane == 0) up = 1;
+    const int cc = lane < moves ? (int)L->hcell[path] : 0;
+    if (lane < moves) {
+      L->hcell[up] = (unsigned short)cc;
+      L->hkey[up] = pk;
+      L->S[(cc >> 8) * nx + (cc & 255)] = (short)up;
+    }
+    const int fin = moves ? __builtin_amdgcn_readlane(path, moves - 1) : 1;
+    if (lane == 0) {
+      L->S[(mc >> 8) * nx + (mc & 255)] = (short)fin;
+      L->hcell[fin] = mc;
+      L->hkey[fin] = km;
+    }
+  }
+  AF_DEV void pop_down() {
+    if (AF_INIT_PARDOWN && ndup == 0) down_par();
+    else down();
   }
   // downtree :178-237 (the moving entry in registers, as in sift_up)
   AF_DEV void down() {
@@ -266,6 +398,11 @@ AF_DEV int job_pack(int z, int x, int kind) { return (z << 8) | x | (kind << 16)
 AF_DEV void post(int* w, int v) { __hip_atomic_store(w, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP); }
 // the waiting role backs off between polls (s_sleep) so that it does not take issue slots and
 // LDS cycles from the working one
+// the relax role's re-check of a changed speculative entry: lane-parallel stencil stage (1) or
+// one lane (0)
+#ifndef AF_INIT_PARSEL
+#define AF_INIT_PARSEL 1
+#endif
 #ifndef AF_INIT_SLEEP
 #define AF_INIT_SLEEP 1
 #endif
@@ -300,13 +437,13 @@ AF_DEV bool pop_two_role(Heap& h, int& seq, int& jobs, int n) {
   InitLds* L = h.L;
   h.pops++;
   if (n == 0) {  // nothing to relax
-    h.down();
+    h.pop_down();
     return true;
   }
   L->njob = n;
   post(&L->cmd, ++seq);
   AF_DG_T0(td)
-  h.down();
+  h.pop_down();
   AF_DG_ADD(L, 1, td)
   for (int k = 0; k < n; k++) {
     AF_DG_T0(tw)
@@ -333,11 +470,23 @@ struct RelaxWin {
 };
 
 // v of lane l (l wave-uniform)
-AF_DEV double readlane_d(double v, int l) {
-  const long long b = __double_as_longlong(v);
-  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)b, l);
-  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(b >> 32), l);
-  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+AF_DEV double readlane_d(double v, int l) { return lane_d(v, l); }
+
+// lane k < 12: NbField slot k of (iz, ix) on an LDS grid (rows z0..z1, columns x0..x1, pitch w),
+// the value and validity NbFieldT::load_lds gives that slot; other lanes: (0, false)
+AF_DEV void lane_slot_lds(const double* T, const short* S, int z0, int x0, int z1, int x1, int w, int iz, int ix,
+                          int lane, double& t, bool& v) {
+  // (dz + 2) and (dx + 2) of slots 0..11, 4 bits each (NbFieldT::load_lds's order)
+  constexpr unsigned long long kDZ = nib12(2, 2, 2, 2, 0, 1, 3, 4, 1, 1, 3, 3);
+  constexpr unsigned long long kDX = nib12(0, 1, 3, 4, 2, 2, 2, 2, 1, 3, 1, 3);
+  const int k = lane < 12 ? lane : 0;
+  const int zz = iz + (int)((kDZ >> (4 * k)) & 15ull) - 2, xx = ix + (int)((kDX >> (4 * k)) & 15ull) - 2;
+  const bool in = lane < 12 && zz >= z0 && zz <= z1 && xx >= x0 && xx <= x1;
+  const int c = in ? (zz - z0) * w + (xx - x0) : 0;
+  const double tv = T[c];
+  const int sv = S[c];
+  t = in ? tv : 0.0;
+  v = in && sv >= 0;
 }
 
 // The relax role (wavefront 1).  A pop's neighbours are relaxed in order, each seeing the earlier
@@ -385,18 +534,30 @@ AF_DEV void relax_role(InitLds* L, const DevModel& M, const MatView& mv, const M
       double v;
       if (hm) {
         const int e = __ffsll((long long)hm) - 1;
-        if (lane == e && (my_dirty || my_nnz != qnnz)) {
-          NbFieldT nb;
-          nb.load_lds(L->T, L->S, R.z0, R.x0, R.z1, R.x1, R.w, iz, ix);
-          const UpdSel s2 = update_nb_select(nb, iz, ix, qnnz, R.nnx);
-          if (!s2.same(my_sel)) {
-            const double* pre;
-            const CellMat cm = init_mat<LDSMAT>(M, L, mv, mw, iz, ix, &pre);
-            my_val = update_nb_finish(M, cm, iz, ix, R.dnx, s2);
-            my_sel = s2;
+        // a changed stencil (or bounds mode): the stage again, on the state of this turn — spread
+        // over the wavefront (lanes 0..11 load a slot each, lanes 0..7 a square stencil each);
+        // on one lane where update() runs its triangular stage
+        if (__builtin_amdgcn_readlane((int)(my_dirty || my_nnz != qnnz), e)) {
+          double tk;
+          bool vk;
+          lane_slot_lds(L->T, L->S, R.z0, R.x0, R.z1, R.x1, R.w, iz, ix, lane, tk, vk);
+          UpdSel s2;
+          const bool par = AF_INIT_PARSEL && update_select_lanes(tk, vk, iz, ix, qnnz, R.nnx, lane, s2);
+          if (lane == e) {
+            if (!par) {
+              NbFieldT nb;
+              nb.load_lds(L->T, L->S, R.z0, R.x0, R.z1, R.x1, R.w, iz, ix);
+              s2 = update_nb_select(nb, iz, ix, qnnz, R.nnx);
+            }
+            if (!s2.same(my_sel)) {
+              const double* pre;
+              const CellMat cm = init_mat<LDSMAT>(M, L, mv, mw, iz, ix, &pre);
+              my_val = update_nb_finish(M, cm, iz, ix, R.dnx, s2);
+              my_sel = s2;
+            }
+            my_dirty = false;
+            my_nnz = qnnz;
           }
-          my_dirty = false;
-          my_nnz = qnnz;
         }
         v = readlane_d(my_val, e);
         if (lane == 0) { AF_DG_ADD(L, 5, tv) }
@@ -462,36 +623,52 @@ template <bool LDSMAT>
 AF_DEV void stage_loop(Heap& h, const DevModel& M, const StageCfg& c, int tid) {
   InitLds* L = h.L;
   const int nz = h.nz, nx = h.nx;
-  if (tid == 0) {
+  if (tid < 64) {  // heap role: wavefront 0 (uniform; single stores by lane 0)
     int seq = 0, jobs = 0;
     bool finished = false;
     while (h.ntr > 0 && !finished && !h.err) {
       AF_DG_T0(tc)
       const int ix = h.bx(1), iz = h.bz(1);
-      L->S[iz * nx + ix] = 0;
+      if (tid == 0) L->S[iz * nx + ix] = 0;
       int n = 0;
-      for (int s = 0; s < 2; s++) {
-        const int i = s == 0 ? ix - 1 : ix + 1;
-        if (0 <= i && i <= nx - 1) {
-          const int st = L->S[iz * nx + i];
-          if (st == -1 || st > 0) {
-            L->job[n] = job_pack(iz, i, st == -1 ? kJobAdd : (kJobUpd | (c.quirk ? kJobQuirk : 0)));
-            n++;
+      if (AF_INIT_PARCLS) {
+        // lane d < 4: neighbour d in the reference's order (x - 1, x + 1, z - 1, z + 1)
+        const int d = tid & 3;
+        const int zz = d < 2 ? iz : (d == 2 ? iz - 1 : iz + 1), xx = d < 2 ? (d == 0 ? ix - 1 : ix + 1) : ix;
+        const bool inb = tid < 4 && (d < 2 ? (0 <= xx && xx <= nx - 1) : (0 <= zz && zz <= nz - 1));
+        const int st = inb ? (int)L->S[zz * nx + xx] : 0;
+        const bool job = inb && (st == -1 || st > 0);
+        const bool fin = tid < 4 && !inb && (d < 2 ? abs(c.isx - xx) : abs(c.isz - zz)) == c.max_dist + 1;
+        const unsigned long long jm = __ballot(job);
+        if (__ballot(fin)) finished = true;
+        if (job)
+          L->job[__popcll(jm & ((1ull << tid) - 1ull))] =
+              job_pack(zz, xx, st == -1 ? kJobAdd : (kJobUpd | (d < 2 && c.quirk ? kJobQuirk : 0)));
+        n = __popcll(jm);
+      } else {
+        for (int s = 0; s < 2; s++) {
+          const int i = s == 0 ? ix - 1 : ix + 1;
+          if (0 <= i && i <= nx - 1) {
+            const int st = L->S[iz * nx + i];
+            if (st == -1 || st > 0) {
+              L->job[n] = job_pack(iz, i, st == -1 ? kJobAdd : (kJobUpd | (c.quirk ? kJobQuirk : 0)));
+              n++;
+            }
+          } else if (abs(c.isx - i) == c.max_dist + 1) {
+            finished = true;
           }
-        } else if (abs(c.isx - i) == c.max_dist + 1) {
-          finished = true;
         }
-      }
-      for (int s = 0; s < 2; s++) {
-        const int i = s == 0 ? iz - 1 : iz + 1;
-        if (0 <= i && i <= nz - 1) {
-          const int st = L->S[i * nx + ix];
-          if (st == -1 || st > 0) {
-            L->job[n] = job_pack(i, ix, st == -1 ? kJobAdd : kJobUpd);
-            n++;
+        for (int s = 0; s < 2; s++) {
+          const int i = s == 0 ? iz - 1 : iz + 1;
+          if (0 <= i && i <= nz - 1) {
+            const int st = L->S[i * nx + ix];
+            if (st == -1 || st > 0) {
+              L->job[n] = job_pack(i, ix, st == -1 ? kJobAdd : kJobUpd);
+              n++;
+            }
+          } else if (abs(c.isz - i) == c.max_dist + 1) {
+            finished = true;
           }
-        } else if (abs(c.isz - i) == c.max_dist + 1) {
-          finished = true;
         }
       }
       AF_DG_ADD(L, 3, tc)
@@ -543,7 +720,7 @@ AF_DEV void main_prefix(Heap& h, const DevModel& M, const InitJob& J, int wz0, i
   const int ww = h.nx;
   const int nnz = M.nz0, nnx = M.nx0;
   const MatView ident{1, 0, 0, 1, 0, 0, 1, 0, 0, 0, 0};
-  if (tid == 0) {
+  if (tid < 64) {  // heap role: wavefront 0 (uniform)
     int seq = 0, jobs = 0;
     while (h.ntr > 0 && !h.err) {
       const int lx = h.bx(1), lz = h.bz(1);
@@ -650,7 +827,7 @@ __global__ __launch_bounds__(128) void fmm_init_kernel(DevModel M0, InitJob* job
         }
       }
       __syncthreads();
-      if (lane == 0) {
+      if (lane < 64) {  // (the heap's sift-ups use the whole wavefront 0)
         // window edges -> heap, in the reference's order (:1601-1612)
         const int s1 = side1;
         if (isz_s - s1 >= 0)
@@ -662,7 +839,7 @@ __global__ __launch_bounds__(128) void fmm_init_kernel(DevModel M0, InitJob* job
         if (isx_s + s1 <= nx - 1)
           for (int i = max(0, isz_s - s1); i <= min(nz - 1, isz_s + s1); i++) h.add(i, isx_s + s1);
       }
-    } else if (lane == 0) {
+    } else if (lane < 64) {
       // hand-over from the decimated previous stage, in row-major order (:1719-1753)
       int dz = (pnz - 1) / 3 + 1, dx = (pnx - 1) / 3 + 1;
       for (int k = 0; k < dz * dx; k++) {
@@ -716,7 +893,7 @@ __global__ __launch_bounds__(128) void fmm_init_kernel(DevModel M0, InitJob* job
       if (LDSMAT && pw.w) load_smid(M, L, pw, lane, nl);
       __syncthreads();
       Heap h{L, wh, ww, 0, 0};
-      if (lane == 0) {
+      if (lane < 64) {
         int dz = (pnz - 1) / 3 + 1, dx = (pnx - 1) / 3 + 1;
         for (int k = 0; k < dz * dx; k++) {
           int i = 3 * (k / dx), j = 3 * (k % dx);

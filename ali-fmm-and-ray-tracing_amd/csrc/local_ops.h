@@ -778,6 +778,89 @@ AF_DEV UpdSel update_nb_select(const F& f, AF_UPD_IDX iz, AF_UPD_IDX ix, AF_UPD_
     return r;
 }
 
+// eight 4-bit fields, the first lowest
+constexpr unsigned nib8(unsigned a, unsigned b, unsigned c, unsigned d, unsigned e, unsigned f, unsigned g,
+                        unsigned h) {
+    return a | b << 4 | c << 8 | d << 12 | e << 16 | f << 20 | g << 24 | h << 28;
+}
+static_assert(nib8(4, 3, 7, 0, 8, 9, 11, 10) == 0xab980734u, "nibble packing");
+// twelve 4-bit fields, the first lowest
+constexpr unsigned long long nib12(unsigned a, unsigned b, unsigned c, unsigned d, unsigned e, unsigned f,
+                                   unsigned g, unsigned h, unsigned i, unsigned j, unsigned k, unsigned l) {
+    return (unsigned long long)nib8(a, b, c, d, e, f, g, h) | (unsigned long long)(i | j << 4 | k << 8 | l << 12) << 32;
+}
+
+// value of lane l (l wave-uniform)
+AF_DEV double lane_d(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)b, l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// update_nb_select() spread over a wavefront (every lane calls it, wave-uniform arguments): lane
+// k < 12 holds NbField slot k's value tk and validity vk; lane k < 8 forms square stencil k's
+// |T_a - T_b| and a three-round min-reduction that keeps the lowest index on ties picks the
+// stencil, which is the reference's first-minimum scan with strict '<' (:994-1033).  The result is
+// update_nb_select()'s, on every lane.  False (r untouched) where update() runs its triangular
+// stage (a grid-edge cell, or no valid square stencil): the caller then runs update_nb_select().
+AF_DEV bool update_select_lanes(double tk, bool vk, AF_UPD_IDX iz, AF_UPD_IDX ix, AF_UPD_IDX nnz, AF_UPD_IDX nnx,
+                                int lane, UpdSel& r) {
+    using I = AF_UPD_IDX;
+    if (ix == 0 || ix == nnx - 1 || iz == 0 || iz == nnz - 1) return false;
+    // interior: every position of the 12 is inside the operator's bounds (update_nb_select's inb)
+    const bool r2 = ix < nnx - 2, l2 = ix > 1, u2 = iz > 1, d2 = iz < nnz - 2;
+    const unsigned inb = 2u | 4u | 32u | 64u | 256u | 512u | 1024u | 2048u | (l2 ? 1u : 0u) | (r2 ? 8u : 0u) |
+                         (u2 ? 16u : 0u) | (d2 ? 128u : 0u);
+    const unsigned em = (unsigned)__ballot(lane < 12 && vk) & inb;
+    // slots of stencil k packed 4 bits per stencil: apex, a, b (update_nb_select's AP / SA / SB)
+    constexpr unsigned kAP = nib8(4, 3, 7, 0, 8, 9, 11, 10), kSA = nib8(8, 9, 10, 8, 1, 5, 6, 1),
+                       kSB = nib8(9, 11, 11, 10, 5, 2, 2, 6);
+    const int k = lane & 7;
+    const int sa = (int)((kSA >> (4 * k)) & 15u), sb = (int)((kSB >> (4 * k)) & 15u), ap = (int)((kAP >> (4 * k)) & 15u);
+    const double ta = __shfl(tk, sa), tb = __shfl(tk, sb);
+    const unsigned msk = (1u << ap) | (1u << sa) | (1u << sb);
+    const double d = fabs(ta - tb);
+    double key = (lane < 8 && (em & msk) == msk && d < 1000000.0) ? d : INFINITY;
+    int idx = lane < 8 ? lane : 64;
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) {
+        const double ok = __shfl_xor(key, o);
+        const int oi = __shfl_xor(idx, o);
+        if (ok < key || (ok == key && oi < idx)) {
+            key = ok;
+            idx = oi;
+        }
+    }
+    if (!(lane_d(key, 0) < INFINITY)) return false;
+    const int sno = __builtin_amdgcn_readfirstlane(idx);
+    const int pa_s = (int)((kSA >> (4 * sno)) & 15u), pb_s = (int)((kSB >> (4 * sno)) & 15u);
+    const int p_s = (int)((kAP >> (4 * sno)) & 15u);
+    const double yap = lane_d(tk, p_s), ya = lane_d(tk, pa_s), yb = lane_d(tk, pb_s);
+    // slot -> (dz + 2) * 8 + (dx + 2), 6 bits per slot (update_nb_select's OFF)
+    constexpr unsigned long long kOff = (16ull) | (17ull << 6) | (19ull << 12) | (20ull << 18) | (2ull << 24) |
+                                        (10ull << 30) | (26ull << 36) | (34ull << 42) | (9ull << 48) |
+                                        (11ull << 54);
+    auto off = [&](int s) -> int { return s < 10 ? (int)((kOff >> (6 * s)) & 63ull) : (s == 10 ? 25 : 27); };
+    const bool lo = ya < yb;
+    const int p1 = off(p_s), p2 = off(lo ? pa_s : pb_s), p3 = off(lo ? pb_s : pa_s);
+    r.w.x1 = ix + (p1 & 7) - 2;
+    r.w.z1 = iz + (p1 >> 3) - 2;
+    r.w.x2 = ix + (p2 & 7) - 2;
+    r.w.z2 = iz + (p2 >> 3) - 2;
+    r.w.x3 = ix + (p3 & 7) - 2;
+    r.w.z3 = iz + (p3 >> 3) - 2;
+    r.w.y1 = yap;
+    r.w.y2 = lo ? ya : yb;
+    r.w.y3 = lo ? yb : ya;
+    r.w.have = true;
+    r.wt = r.w.y2;
+    r.angle = 0.0;
+    r.dist = -1.0;
+    (void)sizeof(I);
+    return true;
+}
+
 AF_DEV double update_nb_finish(const DevModel& M, const CellMat& cm, AF_UPD_IDX iz, AF_UPD_IDX ix, double dnx,
                                const UpdSel& r) {
     return upd_finish(M, cm, ix, iz, r.w, r.wt, r.angle, r.dist, dnx);
