@@ -33,18 +33,20 @@ constexpr int kInitStab = 64;         // stiffness rows staged in LDS
 // the heap role runs on its whole wavefront: addtree / updtree sift-ups (AF_INIT_PARSIFT) and the
 // pop's neighbour classification (AF_INIT_PARCLS) spread over the lanes (0: one lane's loops)
 #ifndef AF_INIT_PARSIFT
-#define AF_INIT_PARSIFT 1
+#define AF_INIT_PARSIFT 0
 #endif
 #ifndef AF_INIT_PARCLS
 #define AF_INIT_PARCLS 1
 #endif
 #ifndef AF_INIT_PARDOWN
-#define AF_INIT_PARDOWN 1
+#define AF_INIT_PARDOWN 0
 #endif
 #if AF_INIT_DIAG
 #define AF_DG_T0(v) const long long v = clock64();
 #define AF_DG_ADD(L, k, v) (L)->dg[k] += clock64() - (v);
+#define AF_DG_CNT(L, k) (L)->dg[k] += 1;
 #else
+#define AF_DG_CNT(L, k)
 #define AF_DG_T0(v)
 #define AF_DG_ADD(L, k, v)
 #endif
@@ -538,6 +540,7 @@ AF_DEV void relax_role(InitLds* L, const DevModel& M, const MatView& mv, const M
         // over the wavefront (lanes 0..11 load a slot each, lanes 0..7 a square stencil each);
         // on one lane where update() runs its triangular stage
         if (__builtin_amdgcn_readlane((int)(my_dirty || my_nnz != qnnz), e)) {
+          AF_DG_T0(trc)
           double tk;
           bool vk;
           lane_slot_lds(L->T, L->S, R.z0, R.x0, R.z1, R.x1, R.w, iz, ix, lane, tk, vk);
@@ -558,6 +561,13 @@ AF_DEV void relax_role(InitLds* L, const DevModel& M, const MatView& mv, const M
             my_dirty = false;
             my_nnz = qnnz;
           }
+          if (lane == 0) {
+            AF_DG_ADD(L, 7, trc)
+            AF_DG_CNT(L, 8)
+            if (!par) { AF_DG_CNT(L, 10) }
+          }
+        } else if (lane == 0) {
+          AF_DG_CNT(L, 9)
         }
         v = readlane_d(my_val, e);
         if (lane == 0) { AF_DG_ADD(L, 5, tv) }

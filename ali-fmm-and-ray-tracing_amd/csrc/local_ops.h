@@ -790,6 +790,21 @@ constexpr unsigned long long nib12(unsigned a, unsigned b, unsigned c, unsigned 
     return (unsigned long long)nib8(a, b, c, d, e, f, g, h) | (unsigned long long)(i | j << 4 | k << 8 | l << 12) << 32;
 }
 
+// DPP moves (gfx9 controls: quad_perm 0x00-0xff, row_mirror 0x140, row_half_mirror 0x141)
+template <int CTRL>
+AF_DEV int dpp_i(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false);
+}
+template <int CTRL>
+AF_DEV double dpp_d(double v) {
+    const long long b = __double_as_longlong(v);
+    const unsigned lo = (unsigned)dpp_i<CTRL>((int)b), hi = (unsigned)dpp_i<CTRL>((int)(b >> 32));
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+#ifndef AF_SEL_DPP
+#define AF_SEL_DPP 1
+#endif
+
 // value of lane l (l wave-uniform)
 AF_DEV double lane_d(double v, int l) {
     const long long b = __double_as_longlong(v);
@@ -823,6 +838,18 @@ AF_DEV bool update_select_lanes(double tk, bool vk, AF_UPD_IDX iz, AF_UPD_IDX ix
     const double d = fabs(ta - tb);
     double key = (lane < 8 && (em & msk) == msk && d < 1000000.0) ? d : INFINITY;
     int idx = lane < 8 ? lane : 64;
+#if AF_SEL_DPP
+    // lanes 0..7: partners by DPP (quad xor 1, quad xor 2, half-row mirror), no LDS round trip
+    auto step = [&](double ok, int oi) {
+        if (ok < key || (ok == key && oi < idx)) {
+            key = ok;
+            idx = oi;
+        }
+    };
+    step(dpp_d<0xB1>(key), dpp_i<0xB1>(idx));
+    step(dpp_d<0x4E>(key), dpp_i<0x4E>(idx));
+    step(dpp_d<0x141>(key), dpp_i<0x141>(idx));
+#else
 #pragma unroll
     for (int o = 1; o < 8; o <<= 1) {
         const double ok = __shfl_xor(key, o);
@@ -832,6 +859,7 @@ AF_DEV bool update_select_lanes(double tk, bool vk, AF_UPD_IDX iz, AF_UPD_IDX ix
             idx = oi;
         }
     }
+#endif
     if (!(lane_d(key, 0) < INFINITY)) return false;
     const int sno = __builtin_amdgcn_readfirstlane(idx);
     const int pa_s = (int)((kSA >> (4 * sno)) & 15u), pb_s = (int)((kSB >> (4 * sno)) & 15u);

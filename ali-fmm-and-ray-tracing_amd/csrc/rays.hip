@@ -58,9 +58,12 @@ __global__ __launch_bounds__(64 * kRayWaves) __attribute__((amdgpu_waves_per_eu(
     if constexpr (LDSMAT) return MatLds{P.M, smat, sstab, sgtab};
     else return MatGlobal{P.M};
   }();
-  const int lane = threadIdx.x & (G - 1), w = threadIdx.x >> 6, grp = (threadIdx.x & 63) / G;
+  // a group of G lanes per ray: G a power of two, or 9 (subgrid 1: the 9 axis-plane candidates,
+  // 7 rays per wavefront, lane 63 idle); gbase = the group's first lane in the wavefront
+  constexpr bool kPow2 = (G & (G - 1)) == 0;
+  const int wl = threadIdx.x & 63, w = threadIdx.x >> 6, grp = wl / G, lane = wl - grp * G, gbase = grp * G;
   const int ray = (blockIdx.x * kRayWaves + w) * kGroups + grp;
-  if (ray >= P.nrays) return;
+  if (grp >= kGroups || ray >= P.nrays) return;
   const RayJob J = P.jobs[ray];
   const int sg = P.sg;
   const long sd = 3L * sg + 1, sd2 = 2L * sg + 1;
@@ -192,9 +195,20 @@ __global__ __launch_bounds__(64 * kRayWaves) __attribute__((amdgpu_waves_per_eu(
         }
       }
     }
-    for (int o = G / 2; o > 0; o >>= 1) {  // stays inside the aligned group of G lanes
-      Key other{__shfl_xor(best.v, o), __shfl_xor(best.order, o), __shfl_xor(best.pos, o)};
-      if (key_less(other, best)) best = other;
+    if (kPow2) {
+      for (int o = G / 2; o > 0; o >>= 1) {  // stays inside the aligned group of G lanes
+        Key other{__shfl_xor(best.v, o), __shfl_xor(best.order, o), __shfl_xor(best.pos, o)};
+        if (key_less(other, best)) best = other;
+      }
+    } else {
+      // lane i takes lane i + o of its group (o = 1, 2, 4, 8): lane 0 ends with the group's
+      // minimum (the order is total: the selection does not depend on the tree), then broadcasts
+      for (int o = 1; o < G; o <<= 1) {
+        const int src = lane + o < G ? wl + o : wl;
+        Key other{__shfl(best.v, src), __shfl(best.order, src), __shfl(best.pos, src)};
+        if (key_less(other, best)) best = other;
+      }
+      best = Key{__shfl(best.v, gbase), __shfl(best.order, gbase), __shfl(best.pos, gbase)};
     }
     const double min_i = best.pos;
     double nx_, ny_;
@@ -241,7 +255,7 @@ __global__ __launch_bounds__(64 * kRayWaves) __attribute__((amdgpu_waves_per_eu(
     double seg = 0.0;
     if (k < npts - 1) seg = tbp(P.M, ms, gld(rxo + k), gld(rxo + k + 1), gld(ryo + k), gld(ryo + k + 1), P.dnx, sg);
     const int m = (int)min((long)G, npts - 1 - k0);
-    for (int l = 0; l < m; l++) tt += __shfl(seg, l, G);
+    for (int l = 0; l < m; l++) tt += kPow2 ? __shfl(seg, l, G) : __shfl(seg, gbase + l);
   }
   if (lane == 0) {
     P.times[ray] = tt;
@@ -277,11 +291,16 @@ extern "C" int af_ray_waves_per_simd() { return AF_RAY_WPE; }
 
 // lanes per ray (a power of two): candidates of one search plane across lanes; AF_RAY_GMIN 8 puts
 // 8 rays in a wavefront at subgrid 1 (9 axis-plane candidates then take two rounds)
+// subgrid 1: groups of exactly the 9 candidates (1) instead of 16 lanes (0)
+#ifndef AF_RAY_G9
+#define AF_RAY_G9 1
+#endif
 #ifndef AF_RAY_GMIN
 #define AF_RAY_GMIN 16
 #endif
 extern "C" int af_ray_group_lanes(int sg) {
   const int ncand = 6 * sg + 3;  // axis planes; diagonal planes have <= 5*sg+3
+  if (AF_RAY_G9 && ncand == 9) return 9;  // subgrid 1: 7 rays of 9 lanes per wavefront
   return ncand <= AF_RAY_GMIN ? AF_RAY_GMIN : ncand <= 16 ? 16 : ncand <= 32 ? 32 : 64;
 }
 
@@ -293,7 +312,10 @@ extern "C" hipError_t af_launch_rays(const af::RayParams* P, hipStream_t stream)
   // index the records)
   const bool lds = P->M.mid && P->M.mtab && P->M.nmat <= af::kRayMatLds && P->M.nstab <= af::kRayStabLds &&
                    361 * P->M.ncol <= af::kRayGtabLds;
-  if (G == 8) {
+  if (G == 9) {
+    if (lds) hipLaunchKernelGGL((af::find_ray_kernel<9, true>), grid, block, 0, stream, *P);
+    else hipLaunchKernelGGL((af::find_ray_kernel<9, false>), grid, block, 0, stream, *P);
+  } else if (G == 8) {
     if (lds) hipLaunchKernelGGL((af::find_ray_kernel<8, true>), grid, block, 0, stream, *P);
     else hipLaunchKernelGGL((af::find_ray_kernel<8, false>), grid, block, 0, stream, *P);
   } else if (G == 16) {

@@ -25,7 +25,9 @@ P = np.array([ctx.init_profile(i) for i in range(ns)], dtype=np.float64)
 m = P.mean(axis=0)
 pops = float(m[4:8].sum())
 names = ["heap_wait_relax", "heap_down", "heap_addupd", "heap_classify", "relax_wait_pop", "relax_entry",
-         "relax_pass", "-"]
+         "relax_pass", "relax_recheck"]
 out = {"sources": ns, "init_ms": ti, "pops": pops, "walk_us_per_pop": ti * 1e3 / pops,
        "cycles_per_pop": {n: round(m[8 + k] / pops, 1) for k, n in enumerate(names) if n != "-"}}
+# diagnostic builds put counts in the stage-tick slots: re-checks, clean entries, re-checks on one lane
+out["per_pop"] = {n: round(m[k] / pops, 3) for k, n in enumerate(("rechecks", "clean_entries", "serial_rechecks"))}
 print(json.dumps(out))
