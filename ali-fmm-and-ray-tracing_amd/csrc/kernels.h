@@ -119,6 +119,7 @@ struct RayParams {
   int* ray_len;
   double* times;
   int* flags;     // bit0 early exit ("Travel time to receiver increasing"), bit1 capacity, bit2 empty plane
+  int glanes;     // lanes per ray (af_ray_group_lanes)
 };
 
 struct LocalOpsParams {
@@ -166,7 +167,7 @@ long af_band_sb_cells(int nz, int nx);
 hipError_t af_launch_scale(double* T, long n, double sg, hipStream_t stream);
 hipError_t af_launch_rays(const af::RayParams* P, hipStream_t stream);
 int af_ray_waves_per_simd();
-int af_ray_group_lanes(int sg);
+int af_ray_group_lanes(int sg, int packed);
 hipError_t af_launch_pack_rays(const double* rx, const double* ry, const int* len, const long long* off, int nrays,
                                int max_pts, double* packed, hipStream_t stream);
 hipError_t af_launch_local_ops(const af::LocalOpsParams* P, hipStream_t stream);

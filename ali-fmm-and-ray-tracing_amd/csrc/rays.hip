@@ -298,14 +298,17 @@ extern "C" int af_ray_waves_per_simd() { return AF_RAY_WPE; }
 #ifndef AF_RAY_GMIN
 #define AF_RAY_GMIN 16
 #endif
-extern "C" int af_ray_group_lanes(int sg) {
+// packed: the launch has rays enough to fill the device at 7 rays per wavefront (9-lane groups at
+// subgrid 1); else 16 lanes (4 rays per wavefront: twice the wavefronts for a smaller launch)
+extern "C" int af_ray_group_lanes(int sg, int packed) {
   const int ncand = 6 * sg + 3;  // axis planes; diagonal planes have <= 5*sg+3
-  if (AF_RAY_G9 && ncand == 9) return 9;  // subgrid 1: 7 rays of 9 lanes per wavefront
+  if (AF_RAY_G9 && packed && ncand == 9) return 9;  // subgrid 1: 7 rays of 9 lanes per wavefront
   return ncand <= AF_RAY_GMIN ? AF_RAY_GMIN : ncand <= 16 ? 16 : ncand <= 32 ? 32 : 64;
 }
 
 extern "C" hipError_t af_launch_rays(const af::RayParams* P, hipStream_t stream) {
-  const int G = af_ray_group_lanes(P->sg);
+  const int G = P->glanes > 0 ? P->glanes : af_ray_group_lanes(P->sg, 0);
+  if (G != 9 && G != 8 && G != 16 && G != 32 && G != 64) return hipErrorInvalidValue;
   const int per_block = af::kRayWaves * (64 / G);
   const dim3 grid((P->nrays + per_block - 1) / per_block), block(64 * af::kRayWaves);
   // material records, stiffness rows and the group table in LDS when they fit (the per-cell ids
