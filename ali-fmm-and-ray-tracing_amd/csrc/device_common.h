@@ -267,10 +267,12 @@ AF_DEV void wad(I ix, I iz, I x1, I x2, I x3, I z1, I z2, I z3, double y1, doubl
 // time_between_points :2835-2989 (coarse material, numba negative-index wrap)
 template <class MS>
 AF_DEV double tbp(const DevModel& M, const MS& ms, double x1, double x2, double y1, double y2, double dnx, int sg) {
-  x1 = x1 / (double)sg;
-  x2 = x2 / (double)sg;
-  y1 = y1 / (double)sg;
-  y2 = y2 / (double)sg;
+  if (sg != 1) {  // (x / 1.0 is x)
+    x1 = x1 / (double)sg;
+    x2 = x2 / (double)sg;
+    y1 = y1 / (double)sg;
+    y2 = y2 / (double)sg;
+  }
   double section_time = 0.0;
   double start_x = x1, end_x = x2, start_y = y1, end_y = y2, prev_x = x1, prev_y = y1;
   double angle = (x1 == x2) ? 0.0 : AF_ATAN((y2 - y1) / (x2 - x1)) * kRad2Deg;

@@ -44,6 +44,7 @@ __global__ __launch_bounds__(64 * kRayWaves) __attribute__((amdgpu_waves_per_eu(
   constexpr int kGroups = 64 / G;             // rays per wavefront
   constexpr int kTT = kMaxCand / kGroups;      // candidate slots per ray
   __shared__ double TTs[kRayWaves][kMaxCand];
+  __shared__ double RTs[kRayWaves][kMaxCand];  // rec_TTF at the candidates (the step's new point reads it)
   __shared__ MatRec smat[LDSMAT ? kRayMatLds : 1];
   __shared__ double sstab[LDSMAT ? 5 * kRayStabLds : 1];
   __shared__ double sgtab[LDSMAT ? kRayGtabLds : 1];
@@ -71,6 +72,7 @@ __global__ __launch_bounds__(64 * kRayWaves) __attribute__((amdgpu_waves_per_eu(
   double* rxo = P.ray_x + (long)ray * P.max_pts;
   double* ryo = P.ray_y + (long)ray * P.max_pts;
   double* TT = &TTs[w][grp * kTT];
+  double* RTc = &RTs[w][grp * kTT];
   long cap = 5L * (P.M.nz0 + P.M.nx0);
   if (cap > P.max_pts) cap = P.max_pts;
   const double recx = J.rx, recy = J.ry;
@@ -84,6 +86,8 @@ __global__ __launch_bounds__(64 * kRayWaves) __attribute__((amdgpu_waves_per_eu(
     ryo[0] = J.sy;
   }
 #define RT(r, c) gld(J.ttf + (long)(r) * P.fnx + (long)(c))
+  // rec_TTF at the rounded last point (:3406): carried from step to step
+  double rt_last = RT(pyround(last_y), pyround(last_x));
   while ((last_x - recx) * (last_x - recx) + (last_y - recy) * (last_y - recy) > (1.6 * sg) * (1.6 * sg)) {
     if ((last_x - recx) * (last_x - recx) + (last_y - recy) * (last_y - recy) < (double)(4 * sg) * (4 * sg)) {
       lvx = recx - last_x;
@@ -150,21 +154,26 @@ __global__ __launch_bounds__(64 * kRayWaves) __attribute__((amdgpu_waves_per_eu(
     for (long i0 = 0; i0 < n; i0 += G) {
       long i = i0 + lane;
       if (i < n) {
-        double t;
+        double t, rt;
         if (dir == 0) {
           long xv = i + base0;
-          t = RT(xv, c_value) + tbp(P.M, ms, last_x, (double)c_value, last_y, (double)xv, P.dnx, sg);
+          rt = RT(xv, c_value);
+          t = rt + tbp(P.M, ms, last_x, (double)c_value, last_y, (double)xv, P.dnx, sg);
         } else if (dir == 1) {
           long xc = base0 + i, yc = -xc + c_value;
-          t = RT(yc, xc) + tbp(P.M, ms, last_x, (double)xc, last_y, (double)yc, P.dnx, sg);
+          rt = RT(yc, xc);
+          t = rt + tbp(P.M, ms, last_x, (double)xc, last_y, (double)yc, P.dnx, sg);
         } else if (dir == 2) {
           long yv = i + base0;
-          t = RT(c_value, yv) + tbp(P.M, ms, last_x, (double)yv, last_y, (double)c_value, P.dnx, sg);
+          rt = RT(c_value, yv);
+          t = rt + tbp(P.M, ms, last_x, (double)yv, last_y, (double)c_value, P.dnx, sg);
         } else {
           long xc = base0 + i, yc = xc + c_value;
-          t = RT(yc, xc) + tbp(P.M, ms, last_x, (double)xc, last_y, (double)yc, P.dnx, sg);
+          rt = RT(yc, xc);
+          t = rt + tbp(P.M, ms, last_x, (double)xc, last_y, (double)yc, P.dnx, sg);
         }
         TT[i] = t;
+        RTc[i] = rt;
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -225,10 +234,20 @@ __global__ __launch_bounds__(64 * kRayWaves) __attribute__((amdgpu_waves_per_eu(
       nx_ = (double)base0 + min_i;
       ny_ = nx_ + (double)c_value;
     }
-    if (RT(pyround(last_y), pyround(last_x)) < RT(pyround(ny_), pyround(nx_))) {
+    // rec_TTF at the rounded new point: a candidate's (read in the candidate pass) when the point
+    // rounds onto the search plane, which it does except at exact .5 ties on diagonal planes
+    const long nrz = pyround(ny_), nrx = pyround(nx_);
+    long ci = -1;
+    if (dir == 0) ci = nrx == c_value ? nrz - base0 : -1;
+    else if (dir == 2) ci = nrz == c_value ? nrx - base0 : -1;
+    else if (dir == 1) ci = nrz == c_value - nrx ? nrx - base0 : -1;
+    else ci = nrz == nrx + c_value ? nrx - base0 : -1;
+    const double rt_new = (ci >= 0 && ci < n) ? RTc[ci] : RT(nrz, nrx);
+    if (rt_last < rt_new) {
       flags |= 1;  // "Travel time to receiver increasing: Finishing ray early" (:3406-3407)
       break;
     }
+    rt_last = rt_new;
     if (lane == 0) {
       rxo[ray_len] = nx_;
       ryo[ray_len] = ny_;
