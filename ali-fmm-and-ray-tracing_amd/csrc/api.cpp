@@ -196,6 +196,7 @@ int alifmm_set_option(alifmm_ctx* ctx, const char* name, double value) {
   else if (!strcmp(name, "r0") && value >= 0) ctx->r0 = value;
   else if (!strcmp(name, "cdelta_far") && value >= 0) ctx->cdelta_far = value;
   else if (!strcmp(name, "r_far") && value >= 0) ctx->r_far = value;
+  else if (!strcmp(name, "far_sg") && value >= 0 && value == (int)value) ctx->far_sg = (int)value;
   else if (!strcmp(name, "batch") && value >= 1) ctx->batch = (int)value;
   else if (!strcmp(name, "prof")) ctx->prof = value != 0;
   else if (!strcmp(name, "coop")) ctx->coop = value != 0;
@@ -215,6 +216,7 @@ int alifmm_get_option(alifmm_ctx* ctx, const char* name, double* value) {
   else if (!strcmp(name, "r0")) *value = ctx->r0;
   else if (!strcmp(name, "cdelta_far")) *value = ctx->cdelta_far;
   else if (!strcmp(name, "r_far")) *value = ctx->r_far;
+  else if (!strcmp(name, "far_sg")) *value = ctx->far_sg;
   else if (!strcmp(name, "batch")) *value = ctx->batch;
   else if (!strcmp(name, "exact_r")) *value = ctx->exact_r;
   else if (!strcmp(name, "exact_lds")) *value = ctx->exact_lds;
@@ -642,7 +644,7 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
   P.cdelta = ctx->cdelta;
   P.vmax = ctx->vmax;
   P.r0 = ctx->r0;
-  P.cdelta_far = ctx->cdelta_far;
+  P.cdelta_far = sg <= ctx->far_sg ? ctx->cdelta_far : 0.0;
   P.r_far = ctx->r_far;
   P.capL = (int)capL;
   P.capC = (int)capC;

@@ -78,7 +78,10 @@ struct alifmm_ctx {
   double* d_ptab = nullptr;
   // options
   double cdelta = 0.5, r0 = 40.0;
-  double cdelta_far = 0.0, r_far = 0.0;  // band width beyond r_far nodes (0: off)
+  // band width 0.6 beyond r_far = 256 nodes (ramped in over 256 .. 512; profiles/r5i: 16 sources
+  // 169 -> 148 ms, 128 sources unchanged, parity envelope within 15 % of the uniform 0.5 band)
+  double cdelta_far = 0.6, r_far = 256.0;
+  int far_sg = 1;  // largest subgrid the far band applies to (subgrid 9 weld rays: profiles/r5j)
   int exact_r = 20;
   void* team = nullptr;  // api.cpp CopyTeam: host copy threads of the pinned staging ring
   int exact_lds = 1;  // subgrid > 1: the LDS exact walk (fmm_exact_lds.hip) when it fits (0: fmm_exact.hip)

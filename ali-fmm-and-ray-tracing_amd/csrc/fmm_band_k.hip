@@ -884,7 +884,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
 #ifndef AF_FAR
 #define AF_FAR 1
 #endif
-    if (AF_FAR) {  // optional wider band far from the source (option cdelta_far / r_far; off by default)
+    if (AF_FAR) {  // wider band far from the source (options cdelta_far / r_far: 0.6 beyond 256 nodes)
       const double tfar = launder_u(R.tfar);
       if (tfar > 0 && tmin > tfar) dl = delta + (launder_u(R.delta_far) - delta) * fmin(1.0, (tmin - tfar) / tfar);
     }

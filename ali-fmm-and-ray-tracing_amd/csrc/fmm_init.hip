@@ -41,6 +41,11 @@ constexpr int kInitStab = 64;         // stiffness rows staged in LDS
 #ifndef AF_INIT_PARDOWN
 #define AF_INIT_PARDOWN 0
 #endif
+// serial sift-ups and downtree with their stores after the walk along the path (1) or level by
+// level (0)
+#ifndef AF_INIT_DEFER
+#define AF_INIT_DEFER 0
+#endif
 #if AF_INIT_DIAG
 #define AF_DG_T0(v) const long long v = clock64();
 #define AF_DG_ADD(L, k, v) (L)->dg[k] += clock64() - (v);
@@ -144,9 +149,112 @@ struct Heap {
       L->hkey[fin] = tv;
     }
   }
+  // sift_up with its stores deferred to the end (ndup == 0): the levels' loads then do not queue
+  // behind the previous level's stores in the wavefront's in-order LDS stream.  The moved entries
+  // are kept in registers (fully unrolled: kLv levels cover the kInitHeap heap); same heap and
+  // statuses as sift_up.
+  static constexpr int kLv = 10;
+  static_assert((1 << kLv) >= kInitHeap, "levels of the heap");
+  AF_DEV void sift_up_defer(int iz, int ix, int tpc) {
+    const unsigned short mc = (unsigned short)((iz << 8) | ix);
+    const double tv = L->hkey[tpc];
+    int tpp = parent_i(tpc), nm = 0;
+    unsigned short mvc[kLv];
+    double mvk[kLv];
+    int mvp[kLv];
+    bool go = true;
+#pragma unroll
+    for (int l = 0; l < kLv; l++) {
+      mvc[l] = 0;
+      mvk[l] = 0.0;
+      mvp[l] = 0;
+      if (go && tpp > 0) {
+        const double kp = L->hkey[tpp];
+        const unsigned short cp = L->hcell[tpp];
+        if (tv < kp) {
+          mvc[l] = cp;
+          mvk[l] = kp;
+          mvp[l] = tpc;
+          nm = l + 1;
+          tpc = tpp;
+          tpp = parent_i(tpc);
+        } else {
+          go = false;
+        }
+      } else {
+        go = false;
+      }
+    }
+#pragma unroll
+    for (int l = 0; l < kLv; l++) {
+      if (l < nm) {
+        L->hcell[mvp[l]] = mvc[l];
+        L->hkey[mvp[l]] = mvk[l];
+        L->S[(mvc[l] >> 8) * nx + (mvc[l] & 255)] = (short)mvp[l];
+      }
+    }
+    if (nm) L->S[iz * nx + ix] = (short)tpc;
+    L->hcell[tpc] = mc;
+    L->hkey[tpc] = tv;
+  }
   AF_DEV void sift(int iz, int ix, int tpc) {
     if (AF_INIT_PARSIFT && ndup == 0) sift_up_par(iz, ix, tpc);
+    else if (AF_INIT_DEFER && ndup == 0) sift_up_defer(iz, ix, tpc);
     else sift_up(iz, ix, tpc);
+  }
+  // downtree with its stores deferred to the end (ndup == 0), as sift_up_defer
+  AF_DEV void down_defer() {
+    if (ntr == 1) {
+      ntr -= 1;
+      return;
+    }
+    const unsigned short mc = L->hcell[ntr];
+    const double km = L->hkey[ntr];
+    ntr -= 1;
+    int tpp = 1, tpc = 2, nm = 0;
+    unsigned short mvc[kLv];
+    double mvk[kLv];
+    int mvp[kLv];
+    bool go = true;
+#pragma unroll
+    for (int l = 0; l < kLv; l++) {
+      mvc[l] = 0;
+      mvk[l] = 0.0;
+      mvp[l] = 0;
+      if (go && tpc <= ntr) {
+        const double k1 = L->hkey[tpc], k2 = tpc < ntr ? L->hkey[tpc + 1] : 0.0;
+        const unsigned short c1 = L->hcell[tpc], c2 = tpc < ntr ? L->hcell[tpc + 1] : 0;
+        const bool right = tpc < ntr && k1 > k2;
+        const int t = right ? tpc + 1 : tpc;
+        const double kc = right ? k2 : k1;
+        const unsigned short cc = right ? c2 : c1;
+        if (kc < km) {
+          mvc[l] = cc;
+          mvk[l] = kc;
+          mvp[l] = tpp;
+          nm = l + 1;
+          tpp = t;
+          tpc = 2 * tpp;
+          if (t == ntr) go = false;  // (the last node: no children)
+        } else {
+          go = false;
+        }
+        if (tpc > ntr) go = false;
+      } else {
+        go = false;
+      }
+    }
+#pragma unroll
+    for (int l = 0; l < kLv; l++) {
+      if (l < nm) {
+        L->hcell[mvp[l]] = mvc[l];
+        L->hkey[mvp[l]] = mvk[l];
+        L->S[(mvc[l] >> 8) * nx + (mvc[l] & 255)] = (short)mvp[l];
+      }
+    }
+    L->S[(mc >> 8) * nx + (mc & 255)] = (short)tpp;
+    L->hcell[tpp] = mc;
+    L->hkey[tpp] = km;
   }
   // The moving entry stays in registers while it sifts: one round of LDS reads per level (the
   // other entry's key and node), the status writes in the reference's order.
@@ -271,6 +379,7 @@ struct Heap {
   }
   AF_DEV void pop_down() {
     if (AF_INIT_PARDOWN && ndup == 0) down_par();
+    else if (AF_INIT_DEFER && ndup == 0) down_defer();
     else down();
   }
   // downtree :178-237 (the moving entry in registers, as in sift_up)

@@ -55,14 +55,17 @@ int alifmm_set_model(alifmm_ctx* ctx, int nnz, int nnx, const double* veln, cons
  * 256), "exact_lds" (subgrid > 1: 1 = the exact walk with its state in LDS, fmm_exact_lds.hip,
  * where the stage grids fit — subgrid <= 9; 0 = the HBM walk, fmm_exact.hip; bit-identical),
  * "coop" (band launch: 1 = cooperative, 0 = plain after a residency check), "cdelta_far" /
- * "r_far" (optional wider band beyond r_far cells; off by default), "stream_out" (subgrid-1 travels
+ * "r_far" (band width beyond Tmin = r_far * dnx / vmax, ramped in over r_far .. 2 r_far; default
+ * 0.6 from 256 cells; cdelta_far 0 = one width everywhere), "far_sg" (the largest subgrid the
+ * far band applies to, default 1), "stream_out" (subgrid-1 travels
  * with a host destination stream the fields out of the band kernel, alifmm_travel_into; default 1). */
 int alifmm_set_option(alifmm_ctx* ctx, const char* name, double value);
 /* Read an option, or "last_k" (workgroups per source of the last band launch), "n_cu"
  * (compute units of the device), "vmax" (the model's fastest speed [m/s]: the exact prefix
  * covers T <= exact_r * dnx / vmax), "stream_tail_ms" and "stream_fallback" (last travel with a host
  * destination: ms from the band kernel's end to the last streamed tile copied; fields copied after
- * the launch instead of streamed). */
+ * the launch instead of streamed), "exact_redo" (last travel, subgrid > 1: sources the LDS exact
+ * walk handed to the HBM walk). */
 int alifmm_get_option(alifmm_ctx* ctx, const char* name, double* value);
 
 /* Shape of a travel-time field for subgrid size sg: (sg*(nnz-1)+1, sg*(nnx-1)+1). */

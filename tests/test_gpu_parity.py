@@ -596,7 +596,8 @@ def test_many_materials_paths(ctx, envelope, n):
     T = ctx.get_field(0, 1)
     B, _ = O.band_travel(dnx * sx, dnx * sz, veln, velpn, vm, sd, vt, vt, ctx.get_option("vmax"),
                          cdelta=ctx.get_option("cdelta"), exact_init=True, r0=ctx.get_option("r0"),
-                         exact_r=ctx.get_option("exact_r"), dnx=dnx)
+                         exact_r=ctx.get_option("exact_r"), dnx=dnx, cdelta_far=ctx.get_option("cdelta_far"),
+                         r_far=ctx.get_option("r_far"))
     dm = float(np.max(np.abs(T - B) / np.maximum(B, 1e-300)))
     envelope["many_materials_vs_band_model_%d" % n] = dm
     assert dm <= 1e-9, (n, dm)

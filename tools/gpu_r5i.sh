@@ -16,3 +16,5 @@ import numpy as np
 for s in ('', '_share'):
     a,b=np.load('gpurun_out/r5i/rold%s.npz'%s),np.load('gpurun_out/r5i/rnew%s.npz'%s)
     print(s or 'full', 'identical' if all(np.array_equal(a[k],b[k]) for k in a.files) else 'DIFFER')" > gpurun_out/r5i/ident.txt
+bash tools/ab_run.sh "idef0 idef1" python -u tools/kbench.py x 128 16 > gpurun_out/r5i/init_defer.txt &&
+bash tools/ab_run.sh "idef0 idef1" python -u tools/c3_bench.py >> gpurun_out/r5i/init_defer.txt
