@@ -88,6 +88,9 @@ AF_DEV double pymod(double a, double b) {
 }
 // round(): half-even (numba lowers to llvm.rint).
 AF_DEV long pyround(double x) { return (long)rint(x); }
+// the same for values known to fit in int (grid coordinates): two instructions instead of the
+// 64-bit conversion's sequence
+AF_DEV int pyround_i(double x) { return (int)rint(x); }
 
 // ---------------------------------------------------------------------------------------------
 // Distinct per-cell material (veln, vel_map, velpn, stiffness row): the band kernel stages the
@@ -284,8 +287,8 @@ AF_DEV double tbp(const DevModel& M, const MS& ms, double x1, double x2, double 
   bool fin_x = false, fin_y = false;
   int dir_x = (start_x < end_x) ? 1 : -1;
   int dir_y = (start_y < end_y) ? 1 : -1;
-  double next_x = (double)pyround(start_x) + dir_x * 0.5;
-  double next_y = (double)pyround(start_y) + dir_y * 0.5;
+  double next_x = rint(start_x) + dir_x * 0.5;  // (double)pyround(x) is rint(x)
+  double next_y = rint(start_y) + dir_y * 0.5;
   int last_id = -1;
   double slown = 0.0;
   while (!(fin_x && fin_y)) {
@@ -323,8 +326,8 @@ AF_DEV double tbp(const DevModel& M, const MS& ms, double x1, double x2, double 
         next_x += dir_x;
       }
     }
-    long x_pos = pyround((prev_x + nxv) / 2);
-    long y_pos = pyround((prev_y + nyv) / 2);
+    int x_pos = pyround_i((prev_x + nxv) / 2);
+    int y_pos = pyround_i((prev_y + nyv) / 2);
     if (x_pos < 0) x_pos += M.nx0;
     if (y_pos < 0) y_pos += M.nz0;
     // the slowness depends on the cell only through its material record (the angle is fixed for

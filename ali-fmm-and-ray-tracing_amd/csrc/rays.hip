@@ -67,8 +67,8 @@ __global__ __launch_bounds__(64 * kRayWaves) __attribute__((amdgpu_waves_per_eu(
   if (grp >= kGroups || ray >= P.nrays) return;
   const RayJob J = P.jobs[ray];
   const int sg = P.sg;
-  const long sd = 3L * sg + 1, sd2 = 2L * sg + 1;
-  const long nnx = P.fnz, nnz = P.fnx;  // reference naming (:3151-3152)
+  const int sd = 3 * sg + 1, sd2 = 2 * sg + 1;
+  const int nnx = P.fnz, nnz = P.fnx;  // reference naming (:3151-3152)
   double* rxo = P.ray_x + (long)ray * P.max_pts;
   double* ryo = P.ray_y + (long)ray * P.max_pts;
   double* TT = &TTs[w][grp * kTT];
@@ -87,7 +87,7 @@ __global__ __launch_bounds__(64 * kRayWaves) __attribute__((amdgpu_waves_per_eu(
   }
 #define RT(r, c) gld(J.ttf + (long)(r) * P.fnx + (long)(c))
   // rec_TTF at the rounded last point (:3406): carried from step to step
-  double rt_last = RT(pyround(last_y), pyround(last_x));
+  double rt_last = RT(pyround_i(last_y), pyround_i(last_x));
   while ((last_x - recx) * (last_x - recx) + (last_y - recy) * (last_y - recy) > (1.6 * sg) * (1.6 * sg)) {
     if ((last_x - recx) * (last_x - recx) + (last_y - recy) * (last_y - recy) < (double)(4 * sg) * (4 * sg)) {
       lvx = recx - last_x;
@@ -101,25 +101,26 @@ __global__ __launch_bounds__(64 * kRayWaves) __attribute__((amdgpu_waves_per_eu(
     int dir = 0;
     for (int q = 1; q < 4; q++)
       if (cand[q] > cand[dir]) dir = q;
-    long rlx = pyround(last_x), rly = pyround(last_y);
-    long c_value = 0, base0 = 0, n = 0;
+    // grid coordinates in int (fields stay below 32768 nodes a side)
+    int rlx = pyround_i(last_x), rly = pyround_i(last_y);
+    int c_value = 0, base0 = 0, n = 0;
     bool stop = false;
     if (dir == 0) {
       c_value = rlx + (lvx > 0 ? sg : -sg);
       if (c_value < 0 || c_value >= nnz) stop = true;
-      long mn = max(0L, rly - sd), mx = min(nnx - 1, rly + sd);
+      int mn = max(0, rly - sd), mx = min(nnx - 1, rly + sd);
       base0 = mn;
       n = mx - mn + 1;
     } else if (dir == 1) {
       c_value = rlx + rly;
-      long mn, mx;
+      int mn, mx;
       if (lvx > 0) {
         c_value += sg;
-        mn = max(max(0L, c_value - (nnx - 1)), rlx - sd2);
+        mn = max(max(0, c_value - (nnx - 1)), rlx - sd2);
         mx = min(min(nnz - 1, c_value), c_value - rly + sd2);
       } else {
         c_value -= sg;
-        mn = max(max(0L, c_value - (nnx - 1)), c_value - rly - sd2);
+        mn = max(max(0, c_value - (nnx - 1)), c_value - rly - sd2);
         mx = min(min(nnz - 1, c_value), rlx + sd2);
       }
       base0 = mn;
@@ -127,19 +128,19 @@ __global__ __launch_bounds__(64 * kRayWaves) __attribute__((amdgpu_waves_per_eu(
     } else if (dir == 2) {
       c_value = rly + (lvy > 0 ? sg : -sg);
       if (c_value < 0 || c_value >= nnx) stop = true;
-      long mn = max(0L, rlx - sd), mx = min(nnz - 1, rlx + sd);
+      int mn = max(0, rlx - sd), mx = min(nnz - 1, rlx + sd);
       base0 = mn;
       n = mx - mn + 1;
     } else {
       c_value = rly - rlx;
-      long mn, mx;
+      int mn, mx;
       if (lvx < 0) {
         c_value += sg;
-        mn = max(max(0L, -c_value), rly - c_value - sd2);
+        mn = max(max(0, -c_value), rly - c_value - sd2);
         mx = min(min(nnz - 1, (nnx - 1) - c_value), rlx + sd2);
       } else {
         c_value -= sg;
-        mn = max(max(0L, -c_value), rlx - sd2);
+        mn = max(max(0, -c_value), rlx - sd2);
         mx = min(min(nnz - 1, (nnx - 1) - c_value), rly - c_value + sd2);
       }
       base0 = mn;
@@ -151,24 +152,24 @@ __global__ __launch_bounds__(64 * kRayWaves) __attribute__((amdgpu_waves_per_eu(
       break;
     }
     // candidates across lanes
-    for (long i0 = 0; i0 < n; i0 += G) {
-      long i = i0 + lane;
+    for (int i0 = 0; i0 < n; i0 += G) {
+      int i = i0 + lane;
       if (i < n) {
         double t, rt;
         if (dir == 0) {
-          long xv = i + base0;
+          int xv = i + base0;
           rt = RT(xv, c_value);
           t = rt + tbp(P.M, ms, last_x, (double)c_value, last_y, (double)xv, P.dnx, sg);
         } else if (dir == 1) {
-          long xc = base0 + i, yc = -xc + c_value;
+          int xc = base0 + i, yc = -xc + c_value;
           rt = RT(yc, xc);
           t = rt + tbp(P.M, ms, last_x, (double)xc, last_y, (double)yc, P.dnx, sg);
         } else if (dir == 2) {
-          long yv = i + base0;
+          int yv = i + base0;
           rt = RT(c_value, yv);
           t = rt + tbp(P.M, ms, last_x, (double)yv, last_y, (double)c_value, P.dnx, sg);
         } else {
-          long xc = base0 + i, yc = xc + c_value;
+          int xc = base0 + i, yc = xc + c_value;
           rt = RT(yc, xc);
           t = rt + tbp(P.M, ms, last_x, (double)xc, last_y, (double)yc, P.dnx, sg);
         }
@@ -182,8 +183,8 @@ __global__ __launch_bounds__(64 * kRayWaves) __attribute__((amdgpu_waves_per_eu(
     Key best;
     if (TT[0] < TT[n - 1]) best = Key{TT[0], 0, 0.0};
     else best = Key{TT[n - 1], 0, (double)(n - 1)};
-    for (long j0 = 1; j0 < n - 1; j0 += G) {
-      long j = j0 + lane;
+    for (int j0 = 1; j0 < n - 1; j0 += G) {
+      int j = j0 + lane;
       if (j < n - 1) {
         double t1 = TT[j - 1], t2 = TT[j], t3 = TT[j + 1];
         if (t1 >= t2 && t2 <= t3) {
@@ -236,8 +237,8 @@ __global__ __launch_bounds__(64 * kRayWaves) __attribute__((amdgpu_waves_per_eu(
     }
     // rec_TTF at the rounded new point: a candidate's (read in the candidate pass) when the point
     // rounds onto the search plane, which it does except at exact .5 ties on diagonal planes
-    const long nrz = pyround(ny_), nrx = pyround(nx_);
-    long ci = -1;
+    const int nrz = pyround_i(ny_), nrx = pyround_i(nx_);
+    int ci = -1;
     if (dir == 0) ci = nrx == c_value ? nrz - base0 : -1;
     else if (dir == 2) ci = nrz == c_value ? nrx - base0 : -1;
     else if (dir == 1) ci = nrz == c_value - nrx ? nrx - base0 : -1;
