@@ -234,6 +234,9 @@ struct MatLds {
   const double* stab;
   const double* gt;
   AF_DEV int id(int z, int x) const {
+#ifdef AF_RAY_DIAG_NOID  // diagnostic build only (wrong rays): the cost of the material-id loads
+    return 0;
+#endif
     const long c = (long)z * M.nx0 + x;
     return M.mid8 ? (int)gld(M.mid8 + c) : gld(M.mid + c);
   }
