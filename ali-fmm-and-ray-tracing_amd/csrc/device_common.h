@@ -270,19 +270,9 @@ AF_DEV void wad(I ix, I iz, I x1, I x2, I x3, I z1, I z2, I z3, double y1, doubl
   dist = fabs(dz * (double)(x2 - ix) - dx * (double)(z2 - iz)) / sqrt(dx * dx + dz * dz);
 }
 
-// Material ids of a window of coarse cells (the ray tracer's step: the cells its candidates'
-// segments cross), read once into LDS: rows z0 .. z0 + kIdWin - 1, columns x0 .. ; -1 where the
-// window leaves the grid (and a cell outside the window) reads the model as before
-constexpr int kIdWin = 11;
-struct IdWin {
-  const int* id;  // kIdWin x kIdWin, row-major (null: no window)
-  int z0, x0;
-};
-
 // time_between_points :2835-2989 (coarse material, numba negative-index wrap)
 template <class MS>
-AF_DEV double tbp(const DevModel& M, const MS& ms, double x1, double x2, double y1, double y2, double dnx, int sg,
-                  const IdWin& win = IdWin{nullptr, 0, 0}) {
+AF_DEV double tbp(const DevModel& M, const MS& ms, double x1, double x2, double y1, double y2, double dnx, int sg) {
   if (sg != 1) {  // (x / 1.0 is x)
     x1 = x1 / (double)sg;
     x2 = x2 / (double)sg;
@@ -346,10 +336,7 @@ AF_DEV double tbp(const DevModel& M, const MS& ms, double x1, double x2, double 
     // the slowness depends on the cell only through its material record (the angle is fixed for
     // the segment), so consecutive pieces in the same material reuse it: the same value, without
     // the group-velocity evaluation (the per-cell material id identifies the record exactly)
-    int id = -1;
-    const unsigned wz = (unsigned)(y_pos - win.z0), wx = (unsigned)(x_pos - win.x0);
-    if (win.id && wz < (unsigned)kIdWin && wx < (unsigned)kIdWin) id = win.id[wz * kIdWin + wx];
-    if (id < 0) id = ms.id((int)y_pos, (int)x_pos);
+    const int id = ms.id((int)y_pos, (int)x_pos);
     if (id < 0 || id != last_id) {
       CellMat cm = ms.cm(id, (int)y_pos, (int)x_pos);
       double eff = pymod(cm.veln - angle, 180);

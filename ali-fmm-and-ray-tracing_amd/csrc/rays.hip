@@ -35,11 +35,6 @@ struct Key {
 AF_DEV bool key_less(const Key& a, const Key& b) { return a.v < b.v || (a.v == b.v && a.order < b.order); }
 
 // wavefronts per SIMD the kernel is compiled for (232 VGPRs at 2; 3 or 4 force fewer registers)
-// subgrid 1: material ids of the step's window read into LDS once per step (1) or per segment
-// piece from the model (0)
-#ifndef AF_RAY_IDWIN
-#define AF_RAY_IDWIN 1
-#endif
 #ifndef AF_RAY_WPE
 #define AF_RAY_WPE 2
 #endif
@@ -50,10 +45,6 @@ __global__ __launch_bounds__(64 * kRayWaves) __attribute__((amdgpu_waves_per_eu(
   constexpr int kTT = kMaxCand / kGroups;      // candidate slots per ray
   __shared__ double TTs[kRayWaves][kMaxCand];
   __shared__ double RTs[kRayWaves][kMaxCand];  // rec_TTF at the candidates (the step's new point reads it)
-  // subgrid 1: per ray, the material ids of the 11 x 11 coarse cells around the step's point (the
-  // candidates' segments stay inside it): one batch of independent loads per step instead of a
-  // dependent load per segment piece
-  __shared__ int IDs[kRayWaves][kGroups][AF_RAY_IDWIN ? kIdWin * kIdWin : 1];
   __shared__ MatRec smat[LDSMAT ? kRayMatLds : 1];
   __shared__ double sstab[LDSMAT ? 5 * kRayStabLds : 1];
   __shared__ double sgtab[LDSMAT ? kRayGtabLds : 1];
@@ -160,18 +151,6 @@ __global__ __launch_bounds__(64 * kRayWaves) __attribute__((amdgpu_waves_per_eu(
       flags |= 4;
       break;
     }
-    IdWin win{nullptr, 0, 0};
-    if (AF_RAY_IDWIN && sg == 1) {
-      int* wid = IDs[w][grp];
-      const int z0 = rly - kIdWin / 2, x0 = rlx - kIdWin / 2;
-      for (int k = lane; k < kIdWin * kIdWin; k += G) {
-        const int z = z0 + k / kIdWin, x = x0 + k % kIdWin;
-        wid[k] = (z >= 0 && z < P.M.nz0 && x >= 0 && x < P.M.nx0) ? ms.id(z, x) : -1;
-      }
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      win = IdWin{wid, z0, x0};
-    }
     // candidates across lanes
     for (int i0 = 0; i0 < n; i0 += G) {
       int i = i0 + lane;
@@ -180,19 +159,19 @@ __global__ __launch_bounds__(64 * kRayWaves) __attribute__((amdgpu_waves_per_eu(
         if (dir == 0) {
           int xv = i + base0;
           rt = RT(xv, c_value);
-          t = rt + tbp(P.M, ms, last_x, (double)c_value, last_y, (double)xv, P.dnx, sg, win);
+          t = rt + tbp(P.M, ms, last_x, (double)c_value, last_y, (double)xv, P.dnx, sg);
         } else if (dir == 1) {
           int xc = base0 + i, yc = -xc + c_value;
           rt = RT(yc, xc);
-          t = rt + tbp(P.M, ms, last_x, (double)xc, last_y, (double)yc, P.dnx, sg, win);
+          t = rt + tbp(P.M, ms, last_x, (double)xc, last_y, (double)yc, P.dnx, sg);
         } else if (dir == 2) {
           int yv = i + base0;
           rt = RT(c_value, yv);
-          t = rt + tbp(P.M, ms, last_x, (double)yv, last_y, (double)c_value, P.dnx, sg, win);
+          t = rt + tbp(P.M, ms, last_x, (double)yv, last_y, (double)c_value, P.dnx, sg);
         } else {
           int xc = base0 + i, yc = xc + c_value;
           rt = RT(yc, xc);
-          t = rt + tbp(P.M, ms, last_x, (double)xc, last_y, (double)yc, P.dnx, sg, win);
+          t = rt + tbp(P.M, ms, last_x, (double)xc, last_y, (double)yc, P.dnx, sg);
         }
         TT[i] = t;
         RTc[i] = rt;
