@@ -36,10 +36,6 @@ constexpr int kThreads = 256;  // 4 waves clear and hand over; wave 0 walks
 #ifndef AF_XL_DIAG
 #define AF_XL_DIAG 0  // diagnostic build: cycle counters of the walk (walk(), BandSrc::ph / sub)
 #endif
-// heap sifts with their stores deferred to the end of the path (1) or level by level (0)
-#ifndef AF_XL_DEFER
-#define AF_XL_DEFER 0
-#endif
 // a stale speculative entry's stencil stage re-run across the wavefront (1) or on its lane (0)
 #ifndef AF_XL_PARSEL
 #define AF_XL_PARSEL 1
@@ -165,58 +161,7 @@ struct Heap {
     L->ht[(e >> 18) & (kHT - 1)] = kLive | ((unsigned)pos << 18) | (e & kNodeM);
     if (e & kDupF) sset(L, (int)(e & kNodeM), kSClose);
   }
-  // sift_up / pop_rest with their stores after the walk along the path (no entry carries kDupF:
-  // the heap-index writes then go to distinct hash slots, so their order is free): the levels'
-  // loads do not queue behind the previous level's stores in the wavefront's in-order LDS stream
-  static constexpr int kLv = 12;
-  static_assert((1 << kLv) >= kHeap, "levels of the heap");
-  AF_DEV void sift_up_defer(int tpc, double km) {
-    const unsigned em = L->ent[tpc];
-    int tpp = parent(tpc), nm = 0;
-    unsigned mve[kLv];
-    double mvk[kLv];
-    int mvp[kLv];
-    bool go = true;
-#pragma unroll
-    for (int l = 0; l < kLv; l++) {
-      mve[l] = 0u;
-      mvk[l] = 0.0;
-      mvp[l] = 0;
-      if (go && tpp > 0) {
-        const double kp = L->key[tpp];
-        unsigned ep = L->ent[tpp];
-        asm volatile("" : "+v"(ep));
-        if (km < kp) {
-          mve[l] = ep;
-          mvk[l] = kp;
-          mvp[l] = tpc;
-          nm = l + 1;
-          tpc = tpp;
-          tpp = parent(tpc);
-        } else {
-          go = false;
-        }
-      } else {
-        go = false;
-      }
-    }
-#pragma unroll
-    for (int l = 0; l < kLv; l++) {
-      if (l < nm) {
-        L->ent[mvp[l]] = mve[l];
-        L->key[mvp[l]] = mvk[l];
-        setpos(mve[l], mvp[l]);
-      }
-    }
-    if (nm) setpos(em, tpc);
-    L->ent[tpc] = em;
-    L->key[tpc] = km;
-  }
   AF_DEV void sift_up(int tpc, double km) {
-    if (AF_XL_DEFER && livedup == 0) {
-      sift_up_defer(tpc, km);
-      return;
-    }
     const unsigned em = L->ent[tpc];
     int tpp = parent(tpc);
     while (tpp > 0) {
@@ -298,54 +243,6 @@ struct Heap {
     }
     const unsigned em = L->ent[ntr];
     const double km = L->key[ntr];
-    if (AF_XL_DEFER && livedup == 0) {
-      ntr -= 1;
-      int tpp = 1, tpc = 2, nm = 0;
-      unsigned mve[kLv];
-      double mvk[kLv];
-      int mvp[kLv];
-      bool go = true;
-#pragma unroll
-      for (int l = 0; l < kLv; l++) {
-        mve[l] = 0u;
-        mvk[l] = 0.0;
-        mvp[l] = 0;
-        if (go && tpc <= ntr) {
-          const double k1 = L->key[tpc], k2 = tpc < ntr ? L->key[tpc + 1] : 0.0;
-          unsigned e1 = L->ent[tpc], e2 = tpc < ntr ? L->ent[tpc + 1] : 0u;
-          asm volatile("" : "+v"(e1), "+v"(e2));
-          const bool right = tpc < ntr && k1 > k2;
-          const int t = right ? tpc + 1 : tpc;
-          const double kc = right ? k2 : k1;
-          const unsigned ec = right ? e2 : e1;
-          if (kc < km) {
-            mve[l] = ec;
-            mvk[l] = kc;
-            mvp[l] = tpp;
-            nm = l + 1;
-            tpp = t;
-            tpc = 2 * tpp;
-          } else {
-            go = false;
-          }
-          if (tpc > ntr) go = false;
-        } else {
-          go = false;
-        }
-      }
-#pragma unroll
-      for (int l = 0; l < kLv; l++) {
-        if (l < nm) {
-          L->ent[mvp[l]] = mve[l];
-          L->key[mvp[l]] = mvk[l];
-          setpos(mve[l], mvp[l]);
-        }
-      }
-      setpos(em, tpp);
-      L->ent[tpp] = em;
-      L->key[tpp] = km;
-      return;
-    }
     setpos(em, 1);
     ntr -= 1;
     int tpp = 1, tpc = 2;

@@ -30,21 +30,13 @@ constexpr int kInitStab = 64;         // stiffness rows staged in LDS
 #ifndef AF_INIT_DIAG
 #define AF_INIT_DIAG 0
 #endif
-// the heap role runs on its whole wavefront: addtree / updtree sift-ups (AF_INIT_PARSIFT) and the
-// pop's neighbour classification (AF_INIT_PARCLS) spread over the lanes (0: one lane's loops)
-#ifndef AF_INIT_PARSIFT
-#define AF_INIT_PARSIFT 0
-#endif
+// the heap role runs on its whole wavefront: the pop's neighbour classification spread over the
+// lanes (AF_INIT_PARCLS; 0: one lane's loops).  Its sift-ups and downtree stay one lane's loops:
+// lane-parallel versions (the ancestors / the min-child path read in one LDS round trip, ballot
+// and readlane chains) and stores deferred to the end of a sift measured slower (profiles/r5d,
+// profiles/r5i_init_deferred_stores_not_kept.txt)
 #ifndef AF_INIT_PARCLS
 #define AF_INIT_PARCLS 1
-#endif
-#ifndef AF_INIT_PARDOWN
-#define AF_INIT_PARDOWN 0
-#endif
-// serial sift-ups and downtree with their stores after the walk along the path (1) or level by
-// level (0)
-#ifndef AF_INIT_DEFER
-#define AF_INIT_DEFER 0
 #endif
 #if AF_INIT_DIAG
 #define AF_DG_T0(v) const long long v = clock64();
@@ -106,156 +98,7 @@ struct Heap {
   AF_DEV int bx(int k) const { return L->hcell[k] & 255; }
   AF_DEV double tb(int k) const { return L->hkey[k]; }
   AF_DEV static int parent(int t) { return (int)rint((double)t / 2.0); }  // half-even (:123)
-  // the same in integers: t / 2 rounded half to even
-  AF_DEV static int parent_i(int t) { return (t >> 1) + ((t & (t >> 1)) & 1); }
-  // sift_up on the heap role's whole wavefront (every lane calls it, wave-uniform arguments): lane
-  // i reads the i-th ancestor's key and node in one LDS round trip, a ballot of "tv < key" finds
-  // how far the entry rises (the first ancestor it does not beat stops it, as in the loop), and
-  // the ancestors it passes move down one place each in one round of stores.  Heap indices and
-  // statuses end as the loop leaves them; a node with two entries (ndup) takes the loop (the
-  // order of its two status writes decides which index it keeps).
-  AF_DEV void sift_up_par(int iz, int ix, int tpc) {
-    const int lane = threadIdx.x & 63;
-    const unsigned short mc = (unsigned short)((iz << 8) | ix);
-    const double tv = L->hkey[tpc];
-    int anc = 0, depth = 0;
-    for (int t = parent_i(tpc); t > 0; t = parent_i(t)) {
-      anc = lane == depth ? t : anc;
-      depth++;
-    }
-    const bool have = lane < depth;
-    const double k = have ? L->hkey[anc] : 0.0;
-    const int cc = have ? (int)L->hcell[anc] : 0;
-    const unsigned long long m = __ballot(have && tv < k);
-    const int j = __builtin_ctzll(~m);
-    if (j == 0) {
-      if (lane == 0) {
-        L->hcell[tpc] = mc;
-        L->hkey[tpc] = tv;
-      }
-      return;
-    }
-    int below = __shfl_up(anc, 1);
-    if (lane == 0) below = tpc;
-    if (lane < j) {
-      L->hcell[below] = (unsigned short)cc;
-      L->hkey[below] = k;
-      L->S[(cc >> 8) * nx + (cc & 255)] = (short)below;
-    }
-    const int fin = __builtin_amdgcn_readlane(anc, j - 1);
-    if (lane == 0) {
-      L->S[iz * nx + ix] = (short)fin;
-      L->hcell[fin] = mc;
-      L->hkey[fin] = tv;
-    }
-  }
-  // sift_up with its stores deferred to the end (ndup == 0): the levels' loads then do not queue
-  // behind the previous level's stores in the wavefront's in-order LDS stream.  The moved entries
-  // are kept in registers (fully unrolled: kLv levels cover the kInitHeap heap); same heap and
-  // statuses as sift_up.
-  static constexpr int kLv = 10;
-  static_assert((1 << kLv) >= kInitHeap, "levels of the heap");
-  AF_DEV void sift_up_defer(int iz, int ix, int tpc) {
-    const unsigned short mc = (unsigned short)((iz << 8) | ix);
-    const double tv = L->hkey[tpc];
-    int tpp = parent_i(tpc), nm = 0;
-    unsigned short mvc[kLv];
-    double mvk[kLv];
-    int mvp[kLv];
-    bool go = true;
-#pragma unroll
-    for (int l = 0; l < kLv; l++) {
-      mvc[l] = 0;
-      mvk[l] = 0.0;
-      mvp[l] = 0;
-      if (go && tpp > 0) {
-        const double kp = L->hkey[tpp];
-        const unsigned short cp = L->hcell[tpp];
-        if (tv < kp) {
-          mvc[l] = cp;
-          mvk[l] = kp;
-          mvp[l] = tpc;
-          nm = l + 1;
-          tpc = tpp;
-          tpp = parent_i(tpc);
-        } else {
-          go = false;
-        }
-      } else {
-        go = false;
-      }
-    }
-#pragma unroll
-    for (int l = 0; l < kLv; l++) {
-      if (l < nm) {
-        L->hcell[mvp[l]] = mvc[l];
-        L->hkey[mvp[l]] = mvk[l];
-        L->S[(mvc[l] >> 8) * nx + (mvc[l] & 255)] = (short)mvp[l];
-      }
-    }
-    if (nm) L->S[iz * nx + ix] = (short)tpc;
-    L->hcell[tpc] = mc;
-    L->hkey[tpc] = tv;
-  }
-  AF_DEV void sift(int iz, int ix, int tpc) {
-    if (AF_INIT_PARSIFT && ndup == 0) sift_up_par(iz, ix, tpc);
-    else if (AF_INIT_DEFER && ndup == 0) sift_up_defer(iz, ix, tpc);
-    else sift_up(iz, ix, tpc);
-  }
-  // downtree with its stores deferred to the end (ndup == 0), as sift_up_defer
-  AF_DEV void down_defer() {
-    if (ntr == 1) {
-      ntr -= 1;
-      return;
-    }
-    const unsigned short mc = L->hcell[ntr];
-    const double km = L->hkey[ntr];
-    ntr -= 1;
-    int tpp = 1, tpc = 2, nm = 0;
-    unsigned short mvc[kLv];
-    double mvk[kLv];
-    int mvp[kLv];
-    bool go = true;
-#pragma unroll
-    for (int l = 0; l < kLv; l++) {
-      mvc[l] = 0;
-      mvk[l] = 0.0;
-      mvp[l] = 0;
-      if (go && tpc <= ntr) {
-        const double k1 = L->hkey[tpc], k2 = tpc < ntr ? L->hkey[tpc + 1] : 0.0;
-        const unsigned short c1 = L->hcell[tpc], c2 = tpc < ntr ? L->hcell[tpc + 1] : 0;
-        const bool right = tpc < ntr && k1 > k2;
-        const int t = right ? tpc + 1 : tpc;
-        const double kc = right ? k2 : k1;
-        const unsigned short cc = right ? c2 : c1;
-        if (kc < km) {
-          mvc[l] = cc;
-          mvk[l] = kc;
-          mvp[l] = tpp;
-          nm = l + 1;
-          tpp = t;
-          tpc = 2 * tpp;
-          if (t == ntr) go = false;  // (the last node: no children)
-        } else {
-          go = false;
-        }
-        if (tpc > ntr) go = false;
-      } else {
-        go = false;
-      }
-    }
-#pragma unroll
-    for (int l = 0; l < kLv; l++) {
-      if (l < nm) {
-        L->hcell[mvp[l]] = mvc[l];
-        L->hkey[mvp[l]] = mvk[l];
-        L->S[(mvc[l] >> 8) * nx + (mvc[l] & 255)] = (short)mvp[l];
-      }
-    }
-    L->S[(mc >> 8) * nx + (mc & 255)] = (short)tpp;
-    L->hcell[tpp] = mc;
-    L->hkey[tpp] = km;
-  }
+  AF_DEV void sift(int iz, int ix, int tpc) { sift_up(iz, ix, tpc); }
   // The moving entry stays in registers while it sifts: one round of LDS reads per level (the
   // other entry's key and node), the status writes in the reference's order.
   AF_DEV void sift_up(int iz, int ix, int tpc) {
@@ -307,81 +150,7 @@ struct Heap {
     for (int k = 1; k <= ntr; k++)
       if (L->hcell[k] == c) L->hkey[k] = t;
   }
-  // downtree on the heap role's whole wavefront (every lane calls it): the last entry sinks along
-  // the path of smaller children from the root (the right child only when strictly smaller), which
-  // does not depend on the sinking key, until a child does not beat it.  The path is followed five
-  // levels at a time: lanes 0..61 read the keys of the 62 nodes of the next five levels below the
-  // current node in one LDS round trip and the wavefront walks them with readlane; then the path
-  // entries move up one level each in one round of stores.  Same heap and statuses as down();
-  // nodes with two entries (ndup) take down().
-  AF_DEV void down_par() {
-    if (ntr == 1) {
-      ntr -= 1;
-      return;
-    }
-    const int lane = threadIdx.x & 63;
-    const unsigned short mc = L->hcell[ntr];
-    const double km = L->hkey[ntr];
-    ntr -= 1;
-    // lane j < 62 of a chunk: level l = 1..5 below q, node q * 2^l + r
-    const int jl = lane + 2, lvl = 31 - __builtin_clz(jl), r = jl - (1 << lvl);
-    int q = 1, moves = 0, path = 0;
-    double pk = 0.0;  // key of path node `moves` (lane = move index)
-    bool go = true;
-    while (go) {
-      const int node = (q << lvl) + r;
-      const double key = (lane < 62 && node <= ntr) ? L->hkey[node] : 0.0;
-#pragma unroll 1
-      for (int l = 0; l < 5; l++) {
-        // children of the current node q (level l + 1 below the chunk's root)
-        const int c1 = 2 * q;
-        if (c1 > ntr) {
-          go = false;
-          break;
-        }
-        const int base = (1 << (l + 1)) - 2;                   // chunk lane of level l + 1's first node
-        const int o1 = base + (c1 - (((c1 >> (l + 1)) << (l + 1))));  // c1 - q0 * 2^(l+1)
-        const double k1 = lane_d(key, o1);
-        int t = c1;
-        double kc = k1;
-        if (c1 < ntr) {
-          const double k2 = lane_d(key, o1 + 1);
-          if (k1 > k2) {
-            t = c1 + 1;
-            kc = k2;
-          }
-        }
-        if (!(kc < km)) {
-          go = false;
-          break;
-        }
-        path = lane == moves ? t : path;
-        pk = lane == moves ? kc : pk;
-        moves++;
-        q = t;
-      }
-    }
-    // move i: the entry at path[i] goes up to its parent on the path (1 for the first)
-    int up = __shfl_up(path, 1);
-    if (lane == 0) up = 1;
-    const int cc = lane < moves ? (int)L->hcell[path] : 0;
-    if (lane < moves) {
-      L->hcell[up] = (unsigned short)cc;
-      L->hkey[up] = pk;
-      L->S[(cc >> 8) * nx + (cc & 255)] = (short)up;
-    }
-    const int fin = moves ? __builtin_amdgcn_readlane(path, moves - 1) : 1;
-    if (lane == 0) {
-      L->S[(mc >> 8) * nx + (mc & 255)] = (short)fin;
-      L->hcell[fin] = mc;
-      L->hkey[fin] = km;
-    }
-  }
-  AF_DEV void pop_down() {
-    if (AF_INIT_PARDOWN && ndup == 0) down_par();
-    else if (AF_INIT_DEFER && ndup == 0) down_defer();
-    else down();
-  }
+  AF_DEV void pop_down() { down(); }
   // downtree :178-237 (the moving entry in registers, as in sift_up)
   AF_DEV void down() {
     if (ntr == 1) { ntr -= 1; return; }
