@@ -573,6 +573,44 @@ def test_sharded_contexts_bit_identical_c4(A, monkeypatch):
     assert np.isfinite(F1).all()
 
 
+def test_far_band_vs_band_model(ctx, envelope):
+    """The default far band (band width 0.6 beyond Tmin = 256 dnx / vmax, ramped in up to 512;
+    subgrid 1) on a 401^2 anisotropic grain model whose front runs ~540 nodes from a corner
+    source: the field equals the CPU band model's (oracle/band_model.c with the same schedule) to
+    <= 1e-9 — the device applies the schedule the model states —, differs from the one-width band
+    (the far band did engage), and stays within the small-grid bar vs the heap oracle (6e-3 / 2e-4;
+    the CPU band model measures 7.8e-4 / 3.9e-5 here, the one-width band 7.2e-4 / 3.8e-5)."""
+    import _alifmm
+
+    n, dnx = 401, 1e-3
+    veln = W.voronoi_small(n, seed=5)
+    velpn = np.zeros((n, n), dtype=np.int64)
+    vm = np.ones((n, n))
+    sd = W.stif_field(n, n)
+    vt = W.default_table()
+    sx, sz = 20, 20
+    assert ctx.get_option("cdelta_far") == 0.6 and ctx.get_option("r_far") == 256
+    ctx.set_model(veln, velpn, vm, sd, vt, vt, dnx)
+    ctx.travel([dnx * sx], [dnx * sz], copy_out=False)
+    T = ctx.get_field(0, 1)
+    B, _ = O.band_travel(dnx * sx, dnx * sz, veln, velpn, vm, sd, vt, vt, ctx.get_option("vmax"),
+                         cdelta=ctx.get_option("cdelta"), exact_init=True, r0=ctx.get_option("r0"),
+                         exact_r=ctx.get_option("exact_r"), dnx=dnx, cdelta_far=0.6, r_far=256.0)
+    dm = float(np.max(np.abs(T - B) / np.maximum(B, 1e-300)))
+    envelope["far_band_vs_band_model_401"] = dm
+    assert dm <= 1e-9, dm
+    c2 = _alifmm.Context(0)
+    try:
+        c2.set_option("cdelta_far", 0.0)
+        c2.set_model(veln, velpn, vm, sd, vt, vt, dnx)
+        c2.travel([dnx * sx], [dnx * sz], copy_out=False)
+        assert not np.array_equal(c2.get_field(0, 1), T)
+    finally:
+        c2.close()
+    R = O.travel(dnx * sx, dnx * sz, veln, velpn, vm, sd, vt, vt, dnx=dnx)
+    _check_field(envelope, "far_band_401", T, R, (sx, sz), tol=(6e-3, 2e-4))
+
+
 @pytest.mark.parametrize("n", [61, 81])
 def test_many_materials_paths(ctx, envelope, n):
     """Models past the kernels' LDS material tables: per-cell random orientations give n^2 distinct
