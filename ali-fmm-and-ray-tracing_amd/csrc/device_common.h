@@ -271,30 +271,45 @@ AF_DEV void wad(I ix, I iz, I x1, I x2, I x3, I z1, I z2, I z3, double y1, doubl
 }
 
 // time_between_points :2835-2989 (coarse material, numba negative-index wrap)
-template <class MS>
-AF_DEV double tbp(const DevModel& M, const MS& ms, double x1, double x2, double y1, double y2, double dnx, int sg) {
-  if (sg != 1) {  // (x / 1.0 is x)
-    x1 = x1 / (double)sg;
-    x2 = x2 / (double)sg;
-    y1 = y1 / (double)sg;
-    y2 = y2 / (double)sg;
+// The walk over the segment's pieces (crossings of the half-integer cell edges): the geometry of
+// piece k does not depend on the material, only the slowness does.
+struct TbpWalk {
+  double start_x, start_y, end_x, end_y, mm, cc;
+  double next_x, next_y, prev_x, prev_y;
+  int dir_x, dir_y;
+  bool fin_x, fin_y;
+  // the segment (x1, y1) -> (x2, y2) in subgrid-sg coordinates; *angle: its direction [deg]
+  AF_DEV void setup(double x1, double x2, double y1, double y2, int sg, double& angle) {
+    if (sg != 1) {  // (x / 1.0 is x)
+      x1 = x1 / (double)sg;
+      x2 = x2 / (double)sg;
+      y1 = y1 / (double)sg;
+      y2 = y2 / (double)sg;
+    }
+    start_x = x1;
+    end_x = x2;
+    start_y = y1;
+    end_y = y2;
+    angle = (x1 == x2) ? 0.0 : AF_ATAN((y2 - y1) / (x2 - x1)) * kRad2Deg;
+    mm = 0;
+    cc = 0;
+    if (end_x != start_x) {
+      mm = (end_y - start_y) / (end_x - start_x);
+      cc = start_y - mm * start_x;
+    }
+    dir_x = (start_x < end_x) ? 1 : -1;
+    dir_y = (start_y < end_y) ? 1 : -1;
   }
-  double section_time = 0.0;
-  double start_x = x1, end_x = x2, start_y = y1, end_y = y2, prev_x = x1, prev_y = y1;
-  double angle = (x1 == x2) ? 0.0 : AF_ATAN((y2 - y1) / (x2 - x1)) * kRad2Deg;
-  double mm = 0, cc = 0;
-  if (end_x != start_x) {
-    mm = (end_y - start_y) / (end_x - start_x);
-    cc = start_y - mm * start_x;
+  AF_DEV void begin() {
+    fin_x = fin_y = false;
+    next_x = rint(start_x) + dir_x * 0.5;  // (double)pyround(x) is rint(x)
+    next_y = rint(start_y) + dir_y * 0.5;
+    prev_x = start_x;
+    prev_y = start_y;
   }
-  bool fin_x = false, fin_y = false;
-  int dir_x = (start_x < end_x) ? 1 : -1;
-  int dir_y = (start_y < end_y) ? 1 : -1;
-  double next_x = rint(start_x) + dir_x * 0.5;  // (double)pyround(x) is rint(x)
-  double next_y = rint(start_y) + dir_y * 0.5;
-  int last_id = -1;
-  double slown = 0.0;
-  while (!(fin_x && fin_y)) {
+  AF_DEV bool done() const { return fin_x && fin_y; }
+  // the next piece's end point (nxv, nyv); the piece runs from (prev_x, prev_y)
+  AF_DEV void piece(double& nxv, double& nyv) {
     if (((next_x > end_x && dir_x == 1) || (next_x < end_x && dir_x == -1)) && !fin_x) {
       fin_x = true;
       next_x = end_x;
@@ -303,7 +318,6 @@ AF_DEV double tbp(const DevModel& M, const MS& ms, double x1, double x2, double 
       fin_y = true;
       next_y = end_y;
     }
-    double nxv, nyv;
     if (end_x == start_x) {
       nxv = start_x;
       nyv = next_y;
@@ -329,26 +343,55 @@ AF_DEV double tbp(const DevModel& M, const MS& ms, double x1, double x2, double 
         next_x += dir_x;
       }
     }
-    int x_pos = pyround_i((prev_x + nxv) / 2);
-    int y_pos = pyround_i((prev_y + nyv) / 2);
+  }
+  // the piece's coarse cell (midpoint, rounded; negative indices wrap like numba's)
+  AF_DEV void cell(const DevModel& M, double nxv, double nyv, int& y_pos, int& x_pos) const {
+    x_pos = pyround_i((prev_x + nxv) / 2);
+    y_pos = pyround_i((prev_y + nyv) / 2);
     if (x_pos < 0) x_pos += M.nx0;
     if (y_pos < 0) y_pos += M.nz0;
+  }
+  // the piece's time at slowness slown (time_between_points' summand)
+  AF_DEV double piece_time(double nxv, double nyv, double dnx, double slown) const {
+    double ddx = prev_x - nxv, ddy = prev_y - nyv;
+    double distance = dnx * sqrt(ddx * ddx + ddy * ddy);
+    return distance * slown;
+  }
+};
+
+// slowness of material record cm along a segment at angle [deg]
+template <class MS>
+AF_DEV double tbp_slowness(const DevModel& M, const MS& ms, const CellMat& cm, double angle) {
+  double eff = pymod(cm.veln - angle, 180);
+  double velocity = group_vel_cell(M, cm, eff, ms.gtab());
+  return 1.0 / velocity;
+}
+
+template <class MS>
+AF_DEV double tbp(const DevModel& M, const MS& ms, double x1, double x2, double y1, double y2, double dnx, int sg) {
+  double section_time = 0.0;
+  TbpWalk w;
+  double angle;
+  w.setup(x1, x2, y1, y2, sg, angle);
+  w.begin();
+  int last_id = -1;
+  double slown = 0.0;
+  while (!w.done()) {
+    double nxv, nyv;
+    w.piece(nxv, nyv);
+    int y_pos, x_pos;
+    w.cell(M, nxv, nyv, y_pos, x_pos);
     // the slowness depends on the cell only through its material record (the angle is fixed for
     // the segment), so consecutive pieces in the same material reuse it: the same value, without
     // the group-velocity evaluation (the per-cell material id identifies the record exactly)
-    const int id = ms.id((int)y_pos, (int)x_pos);
+    const int id = ms.id(y_pos, x_pos);
     if (id < 0 || id != last_id) {
-      CellMat cm = ms.cm(id, (int)y_pos, (int)x_pos);
-      double eff = pymod(cm.veln - angle, 180);
-      double velocity = group_vel_cell(M, cm, eff, ms.gtab());
-      slown = 1.0 / velocity;
+      slown = tbp_slowness(M, ms, ms.cm(id, y_pos, x_pos), angle);
       last_id = id;
     }
-    double ddx = prev_x - nxv, ddy = prev_y - nyv;
-    double distance = dnx * sqrt(ddx * ddx + ddy * ddy);
-    section_time += distance * slown;
-    prev_x = nxv;
-    prev_y = nyv;
+    section_time += w.piece_time(nxv, nyv, dnx, slown);
+    w.prev_x = nxv;
+    w.prev_y = nyv;
   }
   return section_time;
 }

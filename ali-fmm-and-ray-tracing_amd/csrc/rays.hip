@@ -38,6 +38,101 @@ AF_DEV bool key_less(const Key& a, const Key& b) { return a.v < b.v || (a.v == b
 #ifndef AF_RAY_WPE
 #define AF_RAY_WPE 2
 #endif
+// Material runs: time_between_points() evaluates the group velocity once per run of pieces in one
+// material; the lanes of a wavefront reach their runs' evaluations at different pieces, so the
+// one-lane loop re-issues the evaluation for every piece index at which any lane changes material.
+// tbp_wave walks every active lane's segment first (runs: material id and first piece), spreads
+// the runs' evaluations over the active lanes (rounds of one evaluation per lane), then walks the
+// pieces again and sums them in the reference's order.  The same values: a run's slowness depends
+// on its material record and the segment's angle only.
+#ifndef AF_RAY_BATCH
+#define AF_RAY_BATCH 1
+#endif
+constexpr int kRuns = 4;  // runs per segment handled this way (more: the one-lane loop)
+struct RayScratch {       // per wavefront
+  double slo[64 * kRuns];
+  double ang[64];
+  int item[64 * kRuns];
+};
+
+template <class MS>
+AF_DEV double tbp_wave(const DevModel& M, const MS& ms, RayScratch& S, bool valid, double x1, double x2, double y1,
+                       double y2, double dnx, int sg, int wl) {
+  TbpWalk w;
+  double angle = 0.0;
+  unsigned ids = 0, starts = 0;  // run r: material id in byte r, first piece in byte r
+  int nr = 0;
+  if (valid) {
+    w.setup(x1, x2, y1, y2, sg, angle);
+    w.begin();
+    int last = -1;
+    for (int k = 0; !w.done(); k++) {
+      double nxv, nyv;
+      w.piece(nxv, nyv);
+      int yp, xp;
+      w.cell(M, nxv, nyv, yp, xp);
+      const int id = ms.id(yp, xp);
+      if (id != last) {
+        if (nr < kRuns && k < 256) {
+          ids |= (unsigned)id << (8 * nr);
+          starts |= (unsigned)k << (8 * nr);
+        } else {
+          nr = kRuns;  // (k >= 256: over as well)
+        }
+        nr++;
+        last = id;
+      }
+      w.prev_x = nxv;
+      w.prev_y = nyv;
+    }
+  }
+  const bool over = nr > kRuns;
+  const int nb = over ? 0 : nr;
+  S.ang[wl] = angle;
+  const unsigned long long lt = (1ull << wl) - 1ull;
+  int ntot = 0;
+#pragma unroll
+  for (int r = 0; r < kRuns; r++) {
+    const unsigned long long m = __ballot(nb > r);
+    if (nb > r) S.item[ntot + __popcll(m & lt)] = (wl << 10) | (r << 8) | (int)((ids >> (8 * r)) & 255u);
+    ntot += __popcll(m);
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  const unsigned long long act = __ballot(true);
+  const int rank = __popcll(act & lt), nact = __popcll(act);
+  for (int b = 0; b < ntot; b += nact) {
+    const int j = b + rank;
+    if (j < ntot) {
+      const int it = S.item[j];
+      const int l = it >> 10, r = (it >> 8) & 3, id = it & 255;
+      S.slo[l * kRuns + r] = tbp_slowness(M, ms, ms.cm(id, 0, 0), S.ang[l]);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  if (!valid) return 0.0;
+  if (over) return tbp(M, ms, x1, x2, y1, y2, dnx, sg);
+  double section_time = 0.0;
+  w.begin();
+  int r = 0;
+  double slown = S.slo[wl * kRuns];
+  int next_start = nr > 1 ? (int)((starts >> 8) & 255u) : -1;
+  for (int k = 0; !w.done(); k++) {
+    double nxv, nyv;
+    w.piece(nxv, nyv);
+    if (k == next_start) {
+      r++;
+      slown = S.slo[wl * kRuns + r];
+      next_start = r + 1 < nr ? (int)((starts >> (8 * (r + 1))) & 255u) : -1;
+    }
+    section_time += w.piece_time(nxv, nyv, dnx, slown);
+    w.prev_x = nxv;
+    w.prev_y = nyv;
+  }
+  return section_time;
+}
+
 template <int G, bool LDSMAT>
 __global__ __launch_bounds__(64 * kRayWaves) __attribute__((amdgpu_waves_per_eu(AF_RAY_WPE))) void find_ray_kernel(
     RayParams P) {
@@ -48,6 +143,7 @@ __global__ __launch_bounds__(64 * kRayWaves) __attribute__((amdgpu_waves_per_eu(
   __shared__ MatRec smat[LDSMAT ? kRayMatLds : 1];
   __shared__ double sstab[LDSMAT ? 5 * kRayStabLds : 1];
   __shared__ double sgtab[LDSMAT ? kRayGtabLds : 1];
+  __shared__ RayScratch RS[LDSMAT && AF_RAY_BATCH ? kRayWaves : 1];
   crm::lds_init();
   if (LDSMAT) {
     for (int k = threadIdx.x; k < P.M.nmat; k += blockDim.x) smat[k] = P.M.mtab[k];
@@ -153,27 +249,32 @@ __global__ __launch_bounds__(64 * kRayWaves) __attribute__((amdgpu_waves_per_eu(
     }
     // candidates across lanes
     for (int i0 = 0; i0 < n; i0 += G) {
-      int i = i0 + lane;
-      if (i < n) {
-        double t, rt;
-        if (dir == 0) {
-          int xv = i + base0;
-          rt = RT(xv, c_value);
-          t = rt + tbp(P.M, ms, last_x, (double)c_value, last_y, (double)xv, P.dnx, sg);
-        } else if (dir == 1) {
-          int xc = base0 + i, yc = -xc + c_value;
-          rt = RT(yc, xc);
-          t = rt + tbp(P.M, ms, last_x, (double)xc, last_y, (double)yc, P.dnx, sg);
-        } else if (dir == 2) {
-          int yv = i + base0;
-          rt = RT(c_value, yv);
-          t = rt + tbp(P.M, ms, last_x, (double)yv, last_y, (double)c_value, P.dnx, sg);
-        } else {
-          int xc = base0 + i, yc = xc + c_value;
-          rt = RT(yc, xc);
-          t = rt + tbp(P.M, ms, last_x, (double)xc, last_y, (double)yc, P.dnx, sg);
-        }
-        TT[i] = t;
+      const int i = i0 + lane;
+      const bool ok = i < n;
+      // candidate i's grid point (column xa, row ya): rec_TTF there + the straight segment's time
+      int xa, ya;
+      if (dir == 0) {
+        xa = c_value;
+        ya = i + base0;
+      } else if (dir == 1) {
+        xa = base0 + i;
+        ya = -xa + c_value;
+      } else if (dir == 2) {
+        xa = i + base0;
+        ya = c_value;
+      } else {
+        xa = base0 + i;
+        ya = xa + c_value;
+      }
+      const double rt = ok ? RT(ya, xa) : 0.0;
+      double tb;
+      if constexpr (LDSMAT && AF_RAY_BATCH) {
+        tb = tbp_wave(P.M, ms, RS[w], ok, last_x, (double)xa, last_y, (double)ya, P.dnx, sg, wl);
+      } else {
+        tb = ok ? tbp(P.M, ms, last_x, (double)xa, last_y, (double)ya, P.dnx, sg) : 0.0;
+      }
+      if (ok) {
+        TT[i] = rt + tb;
         RTc[i] = rt;
       }
     }
@@ -272,8 +373,15 @@ __global__ __launch_bounds__(64 * kRayWaves) __attribute__((amdgpu_waves_per_eu(
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");  // lane 0's point stores, visible to the group
   for (long k0 = 0; k0 < npts - 1; k0 += G) {
     const long k = k0 + lane;
+    const bool ok = k < npts - 1;
     double seg = 0.0;
-    if (k < npts - 1) seg = tbp(P.M, ms, gld(rxo + k), gld(rxo + k + 1), gld(ryo + k), gld(ryo + k + 1), P.dnx, sg);
+    if constexpr (LDSMAT && AF_RAY_BATCH) {
+      const double xa = ok ? gld(rxo + k) : 0.0, xb = ok ? gld(rxo + k + 1) : 0.0;
+      const double ya = ok ? gld(ryo + k) : 0.0, yb = ok ? gld(ryo + k + 1) : 0.0;
+      seg = tbp_wave(P.M, ms, RS[w], ok, xa, xb, ya, yb, P.dnx, sg, wl);
+    } else {
+      if (ok) seg = tbp(P.M, ms, gld(rxo + k), gld(rxo + k + 1), gld(ryo + k), gld(ryo + k + 1), P.dnx, sg);
+    }
     const int m = (int)min((long)G, npts - 1 - k0);
     for (int l = 0; l < m; l++) tt += kPow2 ? __shfl(seg, l, G) : __shfl(seg, gbase + l);
   }
