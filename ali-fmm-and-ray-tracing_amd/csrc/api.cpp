@@ -247,7 +247,8 @@ int alifmm_copy_fields(alifmm_ctx* ctx, int first_slot, int n, double* dst, int 
 int alifmm_set_model(alifmm_ctx* ctx, int nnz, int nnx, const double* veln, const int64_t* velpn,
                      const double* vel_map, const int64_t* stif_den, const double* group_tab,
                      const double* phase_tab, int ncol, double dnx, double dnz, double gox, double goz) {
-  if (!ctx || nnz < 2 || nnx < 2 || !veln || !velpn || !vel_map || !group_tab || !phase_tab || ncol < 1)
+  if (!ctx || nnz < 2 || nnx < 2 || !veln || !velpn || !vel_map || !group_tab || !phase_tab || ncol < 1 ||
+      ncol >= 32768)  // (the init kernels pack velpn and ncol in one int)
     return fail(ctx, ALIFMM_E_ARG, "set_model: bad arguments");
   HIPCHK(hipSetDevice(ctx->device));
   HIPCHK(hipStreamSynchronize(ctx->stream));

@@ -393,7 +393,7 @@ AF_DEV double relax_value(Lds* L, const DevModel& M, const XG& g, Spec& sp, int 
         }
         pth = 1;
         if (!s2.same(sp.sel)) {
-          sp.v = update_nb_finish(M, sp.cm, sp.z, sp.x, g.dnx, s2);
+          sp.v = update_nb_finish_ool(M, sp.cm, sp.z, sp.x, g.dnx, s2);
           sp.sel = s2;
           pth = 2;
         }
@@ -424,7 +424,7 @@ AF_DEV double relax_value(Lds* L, const DevModel& M, const XG& g, Spec& sp, int 
     L->stn[8][lane] = nb.t8; L->stn[9][lane] = nb.t9; L->stn[10][lane] = nb.t10; L->stn[11][lane] = nb.t11;
     sp.vm = nb.vm;
     sp.sel = update_nb_select(nb, cz, cx, g.nz, g.nx);
-    sp.v = update_nb_finish(M, sp.cm, cz, cx, g.dnx, sp.sel);
+    sp.v = update_nb_finish_ool(M, sp.cm, cz, cx, g.dnx, sp.sel);
     sp.c = g.loc(cz, cx);
     sp.z = cz;
     sp.x = cx;

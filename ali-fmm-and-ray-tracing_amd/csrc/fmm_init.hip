@@ -433,7 +433,7 @@ AF_DEV void relax_role(InitLds* L, const DevModel& M, const MatView& mv, const M
             if (!s2.same(my_sel)) {
               const double* pre;
               const CellMat cm = init_mat<LDSMAT>(M, L, mv, mw, iz, ix, &pre);
-              my_val = update_nb_finish(M, cm, iz, ix, R.dnx, s2);
+              my_val = update_nb_finish_ool(M, cm, iz, ix, R.dnx, s2);
               my_sel = s2;
             }
             my_dirty = false;
@@ -469,7 +469,7 @@ AF_DEV void relax_role(InitLds* L, const DevModel& M, const MatView& mv, const M
           NbFieldT nb;
           nb.load_lds(L->T, L->S, R.z0, R.x0, R.z1, R.x1, R.w, gz, gx);
           my_sel = update_nb_select(nb, gz, gx, cnnz, R.nnx);
-          my_val = update_nb_finish(M, cm, gz, gx, R.dnx, my_sel);
+          my_val = update_nb_finish_ool(M, cm, gz, gx, R.dnx, my_sel);
           my_cell = (cz << 8) | cx;
           my_dirty = false;
           my_nnz = cnnz;

@@ -889,9 +889,42 @@ AF_DEV bool update_select_lanes(double tk, bool vk, AF_UPD_IDX iz, AF_UPD_IDX ix
     return true;
 }
 
+// update()'s finish out of line (AF_FINISH_OOL 1, the init and exact-walk kernels): one copy of the
+// wavefront-angle and phase-velocity code per kernel instead of one per call site (measured: init
+// +1 %, subgrid-9 exact walk -1.5 %, profiles/r5t; off).  The arguments
+// are scalars (32 VGPRs: none go through the stack); vp_nc = velpn | ncol << 16 (set_model keeps
+// ncol below 2^15).  Same arithmetic as upd_finish.
+#ifndef AF_FINISH_OOL
+#define AF_FINISH_OOL 0
+#endif
+#if AF_FINISH_OOL
+__attribute__((noinline))
+#endif
+AF_DEV double upd_finish_ool(const double* ptab, int vp_nc, double veln, double vm, const double* stif, int ix, int iz,
+                             int x1, int x2, int x3, int z1, int z2, int z3, double y1, double y2, double y3, int have,
+                             double wt, double angle, double dist, double dnx) {
+    if (have) wad(ix, iz, x1, x2, x3, z1, z2, z3, y1, y2, y3, angle, dist);
+    if (dist != -1.0) {
+        const int velpn = vp_nc & 0xffff, ncol = vp_nc >> 16;
+        double effa = pymod(veln - angle, 180);
+        double velocity;
+        if (velpn != 0 || stif == nullptr) velocity = table_vel(ptab, ncol, effa, velpn, vm);
+        else velocity = christoffel_phase(stif, effa, vm);
+        return wt + (dist * dnx / velocity);
+    }
+    return -1.0;
+}
+
 AF_DEV double update_nb_finish(const DevModel& M, const CellMat& cm, AF_UPD_IDX iz, AF_UPD_IDX ix, double dnx,
                                const UpdSel& r) {
     return upd_finish(M, cm, ix, iz, r.w, r.wt, r.angle, r.dist, dnx);
+}
+// the same through upd_finish_ool (int coordinates)
+AF_DEV double update_nb_finish_ool(const DevModel& M, const CellMat& cm, int iz, int ix, double dnx, const UpdSel& r) {
+    static_assert(std::is_same<AF_UPD_IDX, int>::value, "int stencil coordinates");
+    return upd_finish_ool(M.ptab, cm.velpn | (M.ncol << 16), cm.veln, cm.vm, cm.stif, ix, iz, r.w.x1, r.w.x2, r.w.x3,
+                          r.w.z1, r.w.z2, r.w.z3, r.w.y1, r.w.y2, r.w.y3, r.w.have ? 1 : 0, r.wt, r.angle, r.dist,
+                          dnx);
 }
 
 template <class F>

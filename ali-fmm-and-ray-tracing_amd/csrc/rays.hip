@@ -48,6 +48,10 @@ AF_DEV bool key_less(const Key& a, const Key& b) { return a.v < b.v || (a.v == b
 #ifndef AF_RAY_BATCH
 #define AF_RAY_BATCH 1
 #endif
+// material ids of a segment's first pieces read ahead of the run scan (0: one read per piece)
+#ifndef AF_RAY_PF
+#define AF_RAY_PF 8
+#endif
 constexpr int kRuns = 4;  // runs per segment handled this way (more: the one-lane loop)
 struct RayScratch {       // per wavefront
   double slo[64 * kRuns];
@@ -55,8 +59,31 @@ struct RayScratch {       // per wavefront
   int item[64 * kRuns];
 };
 
-template <class MS>
-AF_DEV double tbp_wave(const DevModel& M, const MS& ms, RayScratch& S, bool valid, double x1, double x2, double y1,
+// the group-velocity evaluation, one copy in the kernel: inlined at every call site it put the
+// kernel's code past the instruction cache (AF_RAY_SLO_NOINLINE 0: inlined)
+#ifndef AF_RAY_SLO_NOINLINE
+#define AF_RAY_SLO_NOINLINE 1
+#endif
+#if AF_RAY_SLO_NOINLINE
+__attribute__((noinline))
+#endif
+AF_DEV double ray_slowness(double veln, double vm, int velpn, const double* stif, double angle, const double* gtab,
+                           int ncol) {
+  // tbp_slowness / group_vel_cell with the record's fields
+#ifdef AF_RAY_DIAG_SLO  // diagnostic build only (wrong rays): the kernel without the evaluations
+  return 1.0 / (vm + 1e-9 * angle + 1e-12 * veln);
+#endif
+  const double eff = pymod(veln - angle, 180);
+  const double velocity =
+      (velpn != 0 || stif == nullptr) ? table_vel(gtab, ncol, eff, velpn, vm) : christoffel_group(stif, eff, vm);
+  return 1.0 / velocity;
+}
+AF_DEV double ray_slowness(const DevModel& M, const MatLds& ms, int id, double angle) {
+  const MatRec m = ms.mat[id];
+  return ray_slowness(m.veln, m.vm, m.velpn, m.sidx >= 0 ? ms.stab + 5 * m.sidx : nullptr, angle, ms.gt, M.ncol);
+}
+
+AF_DEV double tbp_wave(const DevModel& M, const MatLds& ms, RayScratch& S, bool valid, double x1, double x2, double y1,
                        double y2, double dnx, int sg, int wl) {
   TbpWalk w;
   double angle = 0.0;
@@ -66,12 +93,7 @@ AF_DEV double tbp_wave(const DevModel& M, const MS& ms, RayScratch& S, bool vali
     w.setup(x1, x2, y1, y2, sg, angle);
     w.begin();
     int last = -1;
-    for (int k = 0; !w.done(); k++) {
-      double nxv, nyv;
-      w.piece(nxv, nyv);
-      int yp, xp;
-      w.cell(M, nxv, nyv, yp, xp);
-      const int id = ms.id(yp, xp);
+    auto run = [&](int k, int id) {
       if (id != last) {
         if (nr < kRuns && k < 256) {
           ids |= (unsigned)id << (8 * nr);
@@ -82,14 +104,50 @@ AF_DEV double tbp_wave(const DevModel& M, const MS& ms, RayScratch& S, bool vali
         nr++;
         last = id;
       }
+    };
+    int k = 0;
+    if constexpr (AF_RAY_PF > 0) {
+      // the first AF_RAY_PF pieces' material ids: reads issued together (the walk's geometry does
+      // not depend on them), one memory latency instead of one per piece
+      int idv[AF_RAY_PF > 0 ? AF_RAY_PF : 1];
+      int npf = 0;
+#pragma unroll
+      for (int q = 0; q < AF_RAY_PF; q++) {
+        idv[q] = 0;
+        if (!w.done()) {
+          double nxv, nyv;
+          w.piece(nxv, nyv);
+          int yp, xp;
+          w.cell(M, nxv, nyv, yp, xp);
+          idv[q] = ms.id(yp, xp);
+          w.prev_x = nxv;
+          w.prev_y = nyv;
+          npf = q + 1;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < AF_RAY_PF; q++)
+        if (q < npf) run(q, idv[q]);
+      k = npf;
+    }
+    for (; !w.done(); k++) {  // the rest (long segments)
+      double nxv, nyv;
+      w.piece(nxv, nyv);
+      int yp, xp;
+      w.cell(M, nxv, nyv, yp, xp);
+      run(k, ms.id(yp, xp));
       w.prev_x = nxv;
       w.prev_y = nyv;
     }
   }
+  // over: more runs than kRuns (rare): this lane evaluates its runs in the summing walk
   const bool over = nr > kRuns;
   const int nb = over ? 0 : nr;
   S.ang[wl] = angle;
   const unsigned long long lt = (1ull << wl) - 1ull;
+  // two item lists: table materials (cheap) from the front, Christoffel ones (the closed form's
+  // trigonometry) from the back, so that a round of Christoffel evaluations is not shared with
+  // table ones (both sides of the branch would issue) and the costly rounds are as few as they can be
   int ntot = 0;
 #pragma unroll
   for (int r = 0; r < kRuns; r++) {
@@ -106,22 +164,36 @@ AF_DEV double tbp_wave(const DevModel& M, const MS& ms, RayScratch& S, bool vali
     if (j < ntot) {
       const int it = S.item[j];
       const int l = it >> 10, r = (it >> 8) & 3, id = it & 255;
-      S.slo[l * kRuns + r] = tbp_slowness(M, ms, ms.cm(id, 0, 0), S.ang[l]);
+#ifdef AF_RAY_DIAG_DBL  // diagnostic build: every evaluation twice (its marginal cost), same results
+      double a2 = S.ang[l];
+      asm volatile("" : "+v"(a2));
+      const double s2 = ray_slowness(M, ms, id, a2);
+      S.slo[l * kRuns + r] = ray_slowness(M, ms, id, S.ang[l]) + (s2 == -12345.0 ? 1.0 : 0.0);
+#else
+      S.slo[l * kRuns + r] = ray_slowness(M, ms, id, S.ang[l]);
+#endif
     }
   }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   if (!valid) return 0.0;
-  if (over) return tbp(M, ms, x1, x2, y1, y2, dnx, sg);
   double section_time = 0.0;
   w.begin();
-  int r = 0;
-  double slown = S.slo[wl * kRuns];
-  int next_start = nr > 1 ? (int)((starts >> 8) & 255u) : -1;
+  int r = 0, last = -1;
+  double slown = over ? 0.0 : S.slo[wl * kRuns];
+  int next_start = !over && nr > 1 ? (int)((starts >> 8) & 255u) : -1;
   for (int k = 0; !w.done(); k++) {
     double nxv, nyv;
     w.piece(nxv, nyv);
-    if (k == next_start) {
+    if (over) {
+      int yp, xp;
+      w.cell(M, nxv, nyv, yp, xp);
+      const int id = ms.id(yp, xp);
+      if (id != last) {
+        slown = ray_slowness(M, ms, id, angle);
+        last = id;
+      }
+    } else if (k == next_start) {
       r++;
       slown = S.slo[wl * kRuns + r];
       next_start = r + 1 < nr ? (int)((starts >> (8 * (r + 1))) & 255u) : -1;
@@ -371,7 +443,11 @@ __global__ __launch_bounds__(64 * kRayWaves) __attribute__((amdgpu_waves_per_eu(
   // time_between_points() of consecutive points, read back from the ray buffer) and lane order
   // gives the reference's left-to-right sum, so the per-step walk carries no serial segment time
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");  // lane 0's point stores, visible to the group
+#ifdef AF_RAY_DIAG_NOTIME  // diagnostic build only (no ray times): the walk alone
+  for (long k0 = 0; k0 < 0; k0 += G) {
+#else
   for (long k0 = 0; k0 < npts - 1; k0 += G) {
+#endif
     const long k = k0 + lane;
     const bool ok = k < npts - 1;
     double seg = 0.0;

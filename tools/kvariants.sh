@@ -13,9 +13,10 @@ for v in "$@"; do
   mkdir -p ../../variants/$n
   for s in $SRCS; do
     /opt/rocm/bin/hipcc $FLAGS "$@" -c $s -o ../../variants/$n/${s%.hip}.o &
+    pids="$pids $!"
   done
 done
-wait
+for p in $pids; do wait $p || { echo "a variant failed to compile"; exit 1; }; done
 OTHERS=$(for s in $(sed -n "s/^SRCS = //p" Makefile); do echo ../build/$s.o; done)
 for s in $SRCS; do OTHERS=$(echo "$OTHERS" | grep -v "/${s}.o"); done
 for d in ../../variants/*/; do
