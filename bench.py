@@ -410,6 +410,7 @@ def main():
         for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json"))):
             t = json.load(open(f))
             if (t.get("libalifmm_sha256") == lib_sha and t.get("traffic_bytes_per_launch")
+                    and t.get("kernel", "fmm_band_k_kernel") == "fmm_band_k_kernel"
                     and t.get("sources_per_gpu") == ns and t.get("grid") == [n, n]):
                 traffic_bytes = t["traffic_bytes_per_launch"]
                 if t.get("valu_insts_per_launch"):
