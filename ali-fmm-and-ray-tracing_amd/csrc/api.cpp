@@ -86,6 +86,91 @@ static const size_t kRayBufKeepBytes = (size_t)1 << 30;
 // contexts alive in this process (copy teams share the process's CPU share between them)
 static std::atomic<int> g_live_ctx{0};
 
+// ---- set_model's per-cell passes over the host threads ----
+// the process's CPU share (OMP_NUM_THREADS on the GPU box, else the hardware's, at most 32)
+static int host_threads() {
+  int n = (int)std::max(1u, std::thread::hardware_concurrency());
+  if (const char* e = getenv("OMP_NUM_THREADS")) {
+    const int v = atoi(e);
+    if (v >= 1) n = v;
+  }
+  return std::min(n, 32);
+}
+// fn(chunk, lo, hi) over nch contiguous chunks of [0, n), one thread each
+static void for_chunks(size_t n, int nch, const std::function<void(int, size_t, size_t)>& fn) {
+  if (nch <= 1 || n < 65536) {
+    fn(0, 0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int c = 0; c < nch; c++) th.emplace_back(fn, c, n * c / nch, n * (c + 1) / nch);
+  for (auto& t : th) t.join();
+}
+// Distinct keys of cells [0, n) (key(i)), numbered in order of first occurrence — the serial scan's
+// numbering: each chunk numbers its own keys (runs of equal keys skip the map), then the chunks'
+// keys are merged in chunk order and the ids remapped.  ids[i]: the cell's key id; order: the keys
+// by id.  False when a chunk or the merge finds more than max_keys keys (ids then unusable).
+template <class Key, class KeyFn>
+static bool unique_ids(size_t n, int nth, KeyFn key, std::vector<int>& ids, std::vector<Key>& order,
+                       size_t max_keys) {
+  const int nch = n < 65536 ? 1 : nth;
+  std::vector<std::vector<Key>> local(nch);
+  std::vector<char> over(nch, 0);
+  ids.resize(n);
+  for_chunks(n, nch, [&](int c, size_t lo, size_t hi) {
+    std::map<Key, int> uniq;
+    Key last{};
+    int last_id = -1;
+    for (size_t i = lo; i < hi; i++) {
+      const Key k = key(i);
+      if (last_id >= 0 && k == last) {
+        ids[i] = last_id;
+        continue;
+      }
+      auto it = uniq.find(k);
+      int id;
+      if (it == uniq.end()) {
+        id = (int)local[c].size();
+        if ((size_t)id >= max_keys) {
+          over[c] = 1;
+          return;
+        }
+        uniq.emplace(k, id);
+        local[c].push_back(k);
+      } else {
+        id = it->second;
+      }
+      ids[i] = id;
+      last = k;
+      last_id = id;
+    }
+  });
+  for (int c = 0; c < nch; c++)
+    if (over[c]) return false;
+  std::map<Key, int> glob;
+  std::vector<std::vector<int>> remap(nch);
+  for (int c = 0; c < nch; c++) {
+    for (const Key& k : local[c]) {
+      auto it = glob.find(k);
+      int g;
+      if (it == glob.end()) {
+        g = (int)order.size();
+        if ((size_t)g >= max_keys) return false;
+        glob.emplace(k, g);
+        order.push_back(k);
+      } else {
+        g = it->second;
+      }
+      remap[c].push_back(g);
+    }
+  }
+  for_chunks(n, nch, [&](int c, size_t lo, size_t hi) {
+    const std::vector<int>& r = remap[c];
+    for (size_t i = lo; i < hi; i++) ids[i] = r[ids[i]];
+  });
+  return true;
+}
+
 extern "C" {
 
 const char* alifmm_version(void) { return "alifmm-mi355x 0.1 (gfx950)"; }
@@ -255,40 +340,38 @@ int alifmm_set_model(alifmm_ctx* ctx, int nnz, int nnx, const double* veln, cons
   // everything that can reject the model is checked before the resident model is released, so a
   // rejected call leaves the previous model usable
   const size_t n = (size_t)nnz * nnx;
+  const int nth = host_threads();
   std::vector<int> vp(n);
-  for (size_t i = 0; i < n; i++) {
-    if (velpn[i] < 0 || velpn[i] >= ncol) return fail(ctx, ALIFMM_E_ARG, "velpn[%zu]=%lld outside the table", i,
-                                                      (long long)velpn[i]);
-    vp[i] = (int)velpn[i];
+  {
+    std::vector<size_t> bad(std::max(1, nth), SIZE_MAX);  // per chunk: the first bad cell
+    for_chunks(n, nth, [&](int c, size_t lo, size_t hi) {
+      for (size_t i = lo; i < hi; i++) {
+        if (velpn[i] < 0 || velpn[i] >= ncol) {
+          bad[c] = i;
+          return;
+        }
+        vp[i] = (int)velpn[i];
+      }
+    });
+    for (size_t b : bad)
+      if (b != SIZE_MAX)
+        return fail(ctx, ALIFMM_E_ARG, "velpn[%zu]=%lld outside the table", b, (long long)velpn[b]);
   }
-  // unique stiffness rows
+  // unique stiffness rows (numbered in order of first occurrence)
   std::vector<int> sidx;
   std::vector<double> stab;
   if (stif_den) {
-    sidx.resize(n);
-    std::map<std::array<int64_t, 5>, int> uniq;
-    std::array<int64_t, 5> last{};
-    int last_id = -1;
-    for (size_t i = 0; i < n; i++) {
-      std::array<int64_t, 5> row;
-      for (int k = 0; k < 5; k++) row[k] = stif_den[5 * i + k];
-      if (last_id >= 0 && row == last) {  // runs of equal rows: no map lookup
-        sidx[i] = last_id;
-        continue;
-      }
-      auto it = uniq.find(row);
-      int id;
-      if (it == uniq.end()) {
-        id = (int)uniq.size();
-        uniq.emplace(row, id);
-        for (int k = 0; k < 5; k++) stab.push_back((double)row[k]);
-      } else {
-        id = it->second;
-      }
-      sidx[i] = id;
-      last = row;
-      last_id = id;
-    }
+    std::vector<std::array<int64_t, 5>> rows;
+    unique_ids<std::array<int64_t, 5>>(
+        n, nth,
+        [&](size_t i) {
+          std::array<int64_t, 5> row;
+          for (int k = 0; k < 5; k++) row[k] = stif_den[5 * i + k];
+          return row;
+        },
+        sidx, rows, SIZE_MAX);
+    for (const auto& row : rows)
+      for (int k = 0; k < 5; k++) stab.push_back((double)row[k]);
   }
   // maximum group velocity over the model (band width scale)
   double vmax = 0;
@@ -326,50 +409,47 @@ int alifmm_set_model(alifmm_ctx* ctx, int nnz, int nnx, const double* veln, cons
   }
   // distinct (veln, vel_map, velpn, stiffness row) records -> per-cell material ids
   {
-    std::map<std::array<int64_t, 4>, int> uniq;
     std::vector<af::MatRec> recs;
-    std::vector<int> mid(n);
-    std::array<int64_t, 4> last{};
-    int last_id = -1;
-    bool ok = true;
-    for (size_t i = 0; i < n && ok; i++) {
-      std::array<int64_t, 4> key;
-      memcpy(&key[0], &veln[i], 8);
-      memcpy(&key[1], &vel_map[i], 8);
-      key[2] = vp[i];
-      key[3] = stif_den ? sidx[i] : -1;
-      if (last_id >= 0 && key == last) {
-        mid[i] = last_id;
-        continue;
-      }
-      auto it = uniq.find(key);
-      int id;
-      if (it == uniq.end()) {
-        id = (int)recs.size();
-        if (id >= kMaxMatIds) { ok = false; break; }
-        uniq.emplace(key, id);
-        recs.push_back(af::MatRec{veln[i], vel_map[i], vp[i], stif_den ? sidx[i] : -1});
-      } else {
-        id = it->second;
-      }
-      mid[i] = id;
-      last = key;
-      last_id = id;
+    std::vector<int> mid;
+    std::vector<std::array<int64_t, 4>> keys;
+    const bool ok = unique_ids<std::array<int64_t, 4>>(
+        n, nth,
+        [&](size_t i) {
+          std::array<int64_t, 4> key;
+          memcpy(&key[0], &veln[i], 8);
+          memcpy(&key[1], &vel_map[i], 8);
+          key[2] = vp[i];
+          key[3] = stif_den ? sidx[i] : -1;
+          return key;
+        },
+        mid, keys, (size_t)kMaxMatIds);
+    for (const auto& key : keys) {
+      af::MatRec m;
+      memcpy(&m.veln, &key[0], 8);
+      memcpy(&m.vm, &key[1], 8);
+      m.velpn = (int)key[2];
+      m.sidx = (int)key[3];
+      recs.push_back(m);
     }
     if (ok) {
       HIPCHK(dalloc(&ctx->d_mid, n));
       HIPCHK(dalloc(&ctx->d_mtab, recs.size()));
       HIPCHK(hipMemcpy(ctx->d_mid, mid.data(), n * 4, hipMemcpyHostToDevice));
       if (recs.size() <= 256) {  // byte ids: 4x fewer lines per material gather in the band kernels
-        std::vector<unsigned char> m8(mid.begin(), mid.end());
+        std::vector<unsigned char> m8(n);
+        for_chunks(n, nth, [&](int, size_t lo, size_t hi) {
+          for (size_t i = lo; i < hi; i++) m8[i] = (unsigned char)mid[i];
+        });
         HIPCHK(dalloc(&ctx->d_mid8, n));
         HIPCHK(hipMemcpy(ctx->d_mid8, m8.data(), n, hipMemcpyHostToDevice));
         // the same ids in 8 x 16 bricks (one 128-byte line each) for the band kernel's subgrid-1 view
         const int bp = (nnx + 15) / 16, bz = (nnz + 7) / 8;
         std::vector<unsigned char> mb((size_t)128 * bp * bz, 0);
-        for (int z = 0; z < nnz; z++)
-          for (int x = 0; x < nnx; x++)
-            mb[(((size_t)(z >> 3) * bp + (x >> 4)) << 7) | ((z & 7) << 4) | (x & 15)] = m8[(size_t)z * nnx + x];
+        for_chunks((size_t)bz, std::min(nth, bz), [&](int, size_t b0, size_t b1) {  // brick rows
+          for (int z = (int)b0 * 8; z < std::min(nnz, (int)b1 * 8); z++)
+            for (int x = 0; x < nnx; x++)
+              mb[(((size_t)(z >> 3) * bp + (x >> 4)) << 7) | ((z & 7) << 4) | (x & 15)] = m8[(size_t)z * nnx + x];
+        });
         HIPCHK(dalloc(&ctx->d_mid8b, mb.size()));
         HIPCHK(hipMemcpy(ctx->d_mid8b, mb.data(), mb.size(), hipMemcpyHostToDevice));
         ctx->mid8b_pitch = bp;

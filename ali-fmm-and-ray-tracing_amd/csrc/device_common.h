@@ -351,11 +351,13 @@ struct TbpWalk {
     if (x_pos < 0) x_pos += M.nx0;
     if (y_pos < 0) y_pos += M.nz0;
   }
-  // the piece's time at slowness slown (time_between_points' summand)
-  AF_DEV double piece_time(double nxv, double nyv, double dnx, double slown) const {
+  // the piece's length [m] and its time at slowness slown (time_between_points' summand)
+  AF_DEV double piece_dist(double nxv, double nyv, double dnx) const {
     double ddx = prev_x - nxv, ddy = prev_y - nyv;
-    double distance = dnx * sqrt(ddx * ddx + ddy * ddy);
-    return distance * slown;
+    return dnx * sqrt(ddx * ddx + ddy * ddy);
+  }
+  AF_DEV double piece_time(double nxv, double nyv, double dnx, double slown) const {
+    return piece_dist(nxv, nyv, dnx) * slown;
   }
 };
 

@@ -53,10 +53,16 @@ AF_DEV bool key_less(const Key& a, const Key& b) { return a.v < b.v || (a.v == b
 #define AF_RAY_PF 8
 #endif
 constexpr int kRuns = 4;  // runs per segment handled this way (more: the one-lane loop)
-struct RayScratch {       // per wavefront
+// piece lengths kept from the first walk for the summing one (segments of more pieces walk again)
+#ifndef AF_RAY_PC
+#define AF_RAY_PC 12
+#endif
+constexpr int kPc = AF_RAY_PC;
+struct RayScratch {  // per wavefront
   double slo[64 * kRuns];
   double ang[64];
   int item[64 * kRuns];
+  double dist[64 * (kPc > 0 ? kPc : 1)];  // piece k of lane l: dist[64 k + l]
 };
 
 // the group-velocity evaluation, one copy in the kernel: inlined at every call site it put the
@@ -88,7 +94,7 @@ AF_DEV double tbp_wave(const DevModel& M, const MatLds& ms, RayScratch& S, bool 
   TbpWalk w;
   double angle = 0.0;
   unsigned ids = 0, starts = 0;  // run r: material id in byte r, first piece in byte r
-  int nr = 0;
+  int nr = 0, npc = 0;            // runs, pieces
   if (valid) {
     w.setup(x1, x2, y1, y2, sg, angle);
     w.begin();
@@ -120,6 +126,7 @@ AF_DEV double tbp_wave(const DevModel& M, const MatLds& ms, RayScratch& S, bool 
           int yp, xp;
           w.cell(M, nxv, nyv, yp, xp);
           idv[q] = ms.id(yp, xp);
+          if (q < kPc) S.dist[64 * q + wl] = w.piece_dist(nxv, nyv, dnx);
           w.prev_x = nxv;
           w.prev_y = nyv;
           npf = q + 1;
@@ -136,18 +143,18 @@ AF_DEV double tbp_wave(const DevModel& M, const MatLds& ms, RayScratch& S, bool 
       int yp, xp;
       w.cell(M, nxv, nyv, yp, xp);
       run(k, ms.id(yp, xp));
+      if (k < kPc) S.dist[64 * k + wl] = w.piece_dist(nxv, nyv, dnx);
       w.prev_x = nxv;
       w.prev_y = nyv;
     }
+    npc = k;
   }
   // over: more runs than kRuns (rare): this lane evaluates its runs in the summing walk
   const bool over = nr > kRuns;
   const int nb = over ? 0 : nr;
   S.ang[wl] = angle;
   const unsigned long long lt = (1ull << wl) - 1ull;
-  // two item lists: table materials (cheap) from the front, Christoffel ones (the closed form's
-  // trigonometry) from the back, so that a round of Christoffel evaluations is not shared with
-  // table ones (both sides of the branch would issue) and the costly rounds are as few as they can be
+  // the runs as items (lane, run, material id), compacted over the wavefront
   int ntot = 0;
 #pragma unroll
   for (int r = 0; r < kRuns; r++) {
@@ -178,10 +185,21 @@ AF_DEV double tbp_wave(const DevModel& M, const MatLds& ms, RayScratch& S, bool 
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   if (!valid) return 0.0;
   double section_time = 0.0;
-  w.begin();
   int r = 0, last = -1;
   double slown = over ? 0.0 : S.slo[wl * kRuns];
   int next_start = !over && nr > 1 ? (int)((starts >> 8) & 255u) : -1;
+  if (!over && npc <= kPc) {  // the kept piece lengths, summed in order
+    for (int k = 0; k < npc; k++) {
+      if (k == next_start) {
+        r++;
+        slown = S.slo[wl * kRuns + r];
+        next_start = r + 1 < nr ? (int)((starts >> (8 * (r + 1))) & 255u) : -1;
+      }
+      section_time += S.dist[64 * k + wl] * slown;
+    }
+    return section_time;
+  }
+  w.begin();
   for (int k = 0; !w.done(); k++) {
     double nxv, nyv;
     w.piece(nxv, nyv);

@@ -29,5 +29,5 @@ names = ["heap_wait_relax", "heap_down", "heap_addupd", "heap_classify", "relax_
 out = {"sources": ns, "init_ms": ti, "pops": pops, "walk_us_per_pop": ti * 1e3 / pops,
        "cycles_per_pop": {n: round(m[8 + k] / pops, 1) for k, n in enumerate(names) if n != "-"}}
 # diagnostic builds put counts in the stage-tick slots: re-checks, clean entries, re-checks on one lane
-out["per_pop"] = {n: round(m[k] / pops, 3) for k, n in enumerate(("rechecks", "clean_entries", "fast_same_stage"))}
+out["per_pop"] = {n: round(m[k] / pops, 3) for k, n in enumerate(("rechecks", "clean_entries", "serial_rechecks"))}
 print(json.dumps(out))
