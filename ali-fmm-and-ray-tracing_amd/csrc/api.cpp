@@ -316,6 +316,8 @@ int alifmm_get_option(alifmm_ctx* ctx, const char* name, double* value) {
   else if (!strcmp(name, "last_k")) *value = ctx->last_k;
   else if (!strcmp(name, "n_cu")) *value = ctx->n_cu;
   else if (!strcmp(name, "vmax")) *value = ctx->vmax;  // model's fastest speed (set_model; the exact-walk stop)
+  else if (!strcmp(name, "nmat")) *value = ctx->nmat;  // distinct material records (0: past the id table)
+  else if (!strcmp(name, "ray_lanes")) *value = ctx->last_ray_lanes;  // lanes per ray, last find_rays
   // timings of the last alifmm_find_rays / alifmm_take_rays call (ms): ray kernel and point-packing
   // kernel (HIP events, summed over the launches), the whole call, and the kept points' copy-out
   else if (!strcmp(name, "ray_kernel_ms")) *value = ctx->t_ray_kernel;
@@ -1430,6 +1432,7 @@ int alifmm_find_rays(alifmm_ctx* ctx, int npairs, const int32_t* field_slot, con
       P.times = d_t;
       P.flags = d_flags;
       P.glanes = af_ray_group_lanes(sg, ray_packed);
+      ctx->last_ray_lanes = P.glanes;
       RCHK(hipEventRecord(ctx->ev[0], ctx->stream));
       RCHK(af_launch_rays(&P, ctx->stream));
       RCHK(hipEventRecord(ctx->ev[1], ctx->stream));

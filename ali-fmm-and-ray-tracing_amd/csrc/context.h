@@ -104,6 +104,7 @@ struct alifmm_ctx {
   Arena arena;
   double t_init = 0, t_band = 0, t_total = 0;
   double t_ray_kernel = 0, t_ray_pack = 0, t_find_rays = 0, t_take_rays = 0;  // last find_rays / take_rays (ms)
+  int last_ray_lanes = 0;  // lanes per ray of the last find_rays launch (rays.hip af_ray_group_lanes)
   // packed points of the last alifmm_find_rays(ray_xy = NULL, ray_xy_cap = ALIFMM_KEEP_RAYS) call,
   // per ray in the caller's order, until alifmm_take_rays() copies them out
   std::vector<std::vector<double>> kept_rays;  // host-staged (several subgrids in one call)

@@ -65,7 +65,9 @@ int alifmm_set_option(alifmm_ctx* ctx, const char* name, double value);
  * covers T <= exact_r * dnx / vmax), "stream_tail_ms" and "stream_fallback" (last travel with a host
  * destination: ms from the band kernel's end to the last streamed tile copied; fields copied after
  * the launch instead of streamed), "exact_redo" (last travel, subgrid > 1: sources the LDS exact
- * walk handed to the HBM walk). */
+ * walk handed to the HBM walk), "nmat" (distinct material records of the model; 0 when there are
+ * more than the id table holds), "ray_lanes" (lanes per ray of the last find_rays launch: 9, 16, 32
+ * or 64). */
 int alifmm_get_option(alifmm_ctx* ctx, const char* name, double* value);
 
 /* Shape of a travel-time field for subgrid size sg: (sg*(nnz-1)+1, sg*(nnx-1)+1). */

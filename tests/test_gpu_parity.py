@@ -647,6 +647,46 @@ def test_many_materials_paths(ctx, envelope, n):
     assert int(lens[0]) == len(ox) and abs(t[0] - ot) <= EXACT * ot, (n, t[0], ot, int(lens[0]), len(ox))
 
 
+def test_rays_material_runs(ctx, envelope):
+    """The ray kernel's material runs (rays.hip tbp_wave) on a model with many material changes per
+    segment: per-cell orientations drawn from 100 values and a table / Christoffel mix (200
+    materials: the LDS path with byte ids), so candidate segments cross up to five or more
+    materials (runs past kRuns take the one-lane loop).  Rays through the GPU field: a request big
+    enough for 9-lane groups (7 rays per wavefront) equals a small one (16-lane groups) bit for bit,
+    and sampled rays equal the oracle's on the same field (<= 1e-12; bit-exact in practice)."""
+    n = 61
+    rng = np.random.default_rng(11)
+    dnx = 1e-3
+    veln = rng.integers(0, 100, (n, n)).astype(np.float64) * 1.7
+    velpn = (rng.random((n, n)) < 0.3).astype(np.int64)  # 30 % table materials, the rest Christoffel
+    vm = np.where(velpn == 1, 5790.0, 1.0)
+    sd = W.stif_field(n, n)
+    vt = W.default_table()
+    sx, sz = 30, 2
+    ctx.set_model(veln, velpn, vm, sd, vt, vt, dnx)
+    assert 100 < ctx.get_option("nmat") <= 256
+    ctx.travel([dnx * sx], [dnx * sz], copy_out=False)
+    T = ctx.get_field(0, 1)
+    srcs = np.array([[x, n - 1 - (x % 7)] for x in range(3, n - 3, 4)], dtype=np.float64)
+    m = len(srcs)
+    rec = np.tile([[sx, sz]], (m, 1)).astype(np.float64)
+    t1, l1, f1, _ = ctx.find_rays(np.zeros(m, dtype=np.int32), srcs, rec, with_points=False)
+    assert ctx.get_option("ray_lanes") == 16
+    big = 256 * 4 * 2 * 7 + 5  # the device fills with 9-lane groups from n_cu x 4 x 2 x 7 rays
+    reps = -(-big // m)
+    tb, lb, fb, _ = ctx.find_rays(np.zeros(m * reps, dtype=np.int32), np.tile(srcs, (reps, 1)),
+                                  np.tile(rec, (reps, 1)), with_points=False)
+    assert ctx.get_option("ray_lanes") == 9
+    assert np.array_equal(tb.reshape(reps, m), np.tile(t1, (reps, 1)))
+    assert np.array_equal(lb.reshape(reps, m), np.tile(l1, (reps, 1)))
+    worst = 0.0
+    for k in range(0, m, 3):
+        ox, oy, ot = O.find_ray(dnx, vt, list(srcs[k]), [sx, sz], T, veln, velpn, vm, sd, 1)
+        worst = max(worst, float(abs(t1[k] - ot) / ot))
+        assert int(l1[k]) == len(ox) and abs(t1[k] - ot) <= EXACT * ot, (k, t1[k], ot, int(l1[k]), len(ox))
+    envelope["ray_material_runs"] = worst
+
+
 def test_empty_and_degenerate_requests(A, ctx, envelope):
     """Edge cases of the drop-in surface: no selected sources, no ray pairs, a 1-column grid, a
     source outside the grid (reference: IndexError-like failure -> the C-ABI's argument error)."""
