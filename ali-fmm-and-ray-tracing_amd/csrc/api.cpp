@@ -83,6 +83,8 @@ static const int kMaxRayCand = 256;
 // ray point buffers larger than this are freed at the end of each alifmm_find_rays call
 static const size_t kRayBufKeepBytes = (size_t)1 << 30;
 
+// host copies up to this size go straight to pageable memory while the pinned ring is unallocated
+static const size_t kSmallD2H = (size_t)64 << 20;
 // contexts alive in this process (copy teams share the process's CPU share between them)
 static std::atomic<int> g_live_ctx{0};
 
@@ -1177,6 +1179,15 @@ struct D2HSeg {
 static int d2h_pageable(alifmm_ctx* ctx, const std::vector<D2HSeg>& segs) {
   const int nb = alifmm_ctx::kPinBufs;
   const size_t pb = alifmm_ctx::kPinBytes;
+  size_t total = 0;
+  for (const auto& g : segs) total += g.bytes;
+  if (total <= kSmallD2H && !ctx->pin[0]) {
+    // a small copy before the ring exists (e.g. the weld example's 8 MB of ray points): plain copies,
+    // not 4 x 32 MB of fresh pinned memory (~30 ms to allocate) and a copy team
+    for (const auto& g : segs) HIPCHK(hipMemcpyAsync(g.dst, g.src, g.bytes, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return ALIFMM_OK;
+  }
   for (int b = 0; b < nb; b++) {
     if (!ctx->pin[b]) HIPCHK(hipHostMalloc(&ctx->pin[b], pb, hipHostMallocDefault));
     if (!ctx->pin_ev[b]) HIPCHK(hipEventCreateWithFlags(&ctx->pin_ev[b], hipEventDisableTiming));

@@ -40,7 +40,9 @@ def main():
     g = np.load(os.path.join(REPO, "tests", "golden", "weld_sg9.npz"))
     rel = {i: abs(trav_times[i, 46] - float(g["time_%d" % i])) / float(g["time_%d" % i]) for i in (0, 15, 30)}
     print(json.dumps({"wall_s": dt, "rays": int(np.sum(trans_pairs)), "receiver_fields": n_trans,
-                      "subgrid": 9, "max_ray_len": max_len, "ray_time_rel_err_vs_reference": rel}))
+                      "subgrid": 9, "max_ray_len": max_len, "ray_time_rel_err_vs_reference": rel,
+                      "split": model.last_timing,
+                      "travel_init_band_total_ms": model._ctx(0).last_timing()}))
 
 
 if __name__ == "__main__":
