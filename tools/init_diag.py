@@ -15,9 +15,15 @@ import workloads as W  # noqa: E402
 
 ctx = _alifmm.Context(0)
 vt = W.default_table()
-ctx.set_model(*W.weldlike_model(), vt, vt, W.weldlike_dnx())
-sx, sz = W.c4_sources(128)
-ns = int(sys.argv[1]) if len(sys.argv) > 1 else 128
+if len(sys.argv) > 1 and sys.argv[1] == "c3":  # BASELINE C3: one interior source on the grain model
+    ctx.set_model(*W.c3_model(), vt, vt, 1e-3)
+    cx, cz = W.c3_source()
+    sx, sz = np.array([cx]), np.array([cz])
+    ns = 1
+else:
+    ctx.set_model(*W.weldlike_model(), vt, vt, W.weldlike_dnx())
+    sx, sz = W.c4_sources(128)
+    ns = int(sys.argv[1]) if len(sys.argv) > 1 else 128
 ctx.travel(sx[:ns], sz[:ns], copy_out=False)
 ctx.travel(sx[:ns], sz[:ns], copy_out=False)
 ti, tb, _ = ctx.last_timing()
