@@ -38,6 +38,11 @@ constexpr int kInitStab = 64;         // stiffness rows staged in LDS
 #ifndef AF_INIT_PARCLS
 #define AF_INIT_PARCLS 1
 #endif
+// the next pop classified and handed to the relax role before the last sift-up of the current
+// one when that sift-up cannot reach the root (stage walks)
+#ifndef AF_INIT_EARLY
+#define AF_INIT_EARLY 1
+#endif
 #if AF_INIT_DIAG
 #define AF_DG_T0(v) const long long v = clock64();
 #define AF_DG_ADD(L, k, v) (L)->dg[k] += clock64() - (v);
@@ -122,7 +127,9 @@ struct Heap {
   // addtree :94-138
   // fresh: the node is known to be far (a relaxation job; its status already reads 1, set by
   // the relax role), else its status tells whether it already has an entry
-  AF_DEV void add(int iz, int ix, bool fresh = false) {
+  AF_DEV void add(int iz, int ix, bool fresh = false) { add_key(iz, ix, L->T[iz * nx + ix], fresh); }
+  // the same with the node's ttn given (read when its relaxation was posted)
+  AF_DEV void add_key(int iz, int ix, double key, bool fresh) {
     ntr += 1;
     if (ntr >= kInitHeap) { err = 1; ntr = kInitHeap - 1; return; }
     if (!fresh && L->S[iz * nx + ix] > 0) {  // already in the heap: a second entry
@@ -131,13 +138,14 @@ struct Heap {
     }
     L->S[iz * nx + ix] = (short)ntr;
     L->hcell[ntr] = (unsigned short)((iz << 8) | ix);
-    L->hkey[ntr] = L->T[iz * nx + ix];
+    L->hkey[ntr] = key;
     sift(iz, ix, ntr);
   }
   // updtree :141-175
-  AF_DEV void upd(int iz, int ix) {
+  AF_DEV void upd(int iz, int ix) { upd_key(iz, ix, L->T[iz * nx + ix]); }
+  AF_DEV void upd_key(int iz, int ix, double key) {
     const int tpc = L->S[iz * nx + ix];
-    L->hkey[tpc] = L->T[iz * nx + ix];
+    L->hkey[tpc] = key;
     sift(iz, ix, tpc);
   }
   // a node's ttn changed: every heap entry of a node with two entries takes the new value
@@ -313,15 +321,22 @@ AF_DEV int await_change(int* w, int last) {  // the next value != last, or -2 on
 // neighbour's addtree / updtree as soon as its relaxation is done (L->done counts relaxations), so
 // the sift-ups run beside the later neighbours' relaxations (they only move heap indices: the
 // validity the relaxations read stays).  false: the relax role timed out
-AF_DEV bool pop_two_role(Heap& h, int& seq, int& jobs, int n) {
+// posted: the pop's jobs were already handed over (classified early, below).  early(key, cell):
+// called before the last job's addtree / updtree with that node's new key and cell; it may
+// classify the next pop and hand its jobs over first (they overwrite L->job: the job is read
+// before), so that the relax role starts on them while this sift-up runs
+template <class Early>
+AF_DEV bool pop_two_role(Heap& h, int& seq, int& jobs, int n, bool posted, Early early) {
   InitLds* L = h.L;
   h.pops++;
   if (n == 0) {  // nothing to relax
     h.pop_down();
     return true;
   }
-  L->njob = n;
-  post(&L->cmd, ++seq);
+  if (!posted) {
+    L->njob = n;
+    post(&L->cmd, ++seq);
+  }
   AF_DG_T0(td)
   h.pop_down();
   AF_DG_ADD(L, 1, td)
@@ -331,13 +346,19 @@ AF_DEV bool pop_two_role(Heap& h, int& seq, int& jobs, int n) {
     AF_DG_ADD(L, 0, tw)
     AF_DG_T0(ta)
     const int jk = L->job[k];
-    if (job_kind(jk) & kJobAdd) h.add(job_z(jk), job_x(jk), true);
-    else h.upd(job_z(jk), job_x(jk));
-    if (h.ndup) h.sync(job_z(jk), job_x(jk));
+    const int jz = job_z(jk), jx = job_x(jk);
+    const double key = L->T[jz * h.nx + jx];
+    if (k == n - 1) early(key, (jz << 8) | jx);
+    if (job_kind(jk) & kJobAdd) h.add_key(jz, jx, key, true);
+    else h.upd_key(jz, jx, key);
+    if (h.ndup) h.sync(jz, jx);
     AF_DG_ADD(L, 2, ta)
   }
   jobs += n;
   return true;
+}
+AF_DEV bool pop_two_role(Heap& h, int& seq, int& jobs, int n) {
+  return pop_two_role(h, seq, jobs, n, false, [](double, int) {});
 }
 
 struct RelaxWin {
@@ -514,11 +535,13 @@ AF_DEV void stage_loop(Heap& h, const DevModel& M, const StageCfg& c, int tid) {
   if (tid < 64) {  // heap role: wavefront 0 (uniform; single stores by lane 0)
     int seq = 0, jobs = 0;
     bool finished = false;
-    while (h.ntr > 0 && !finished && !h.err) {
-      AF_DG_T0(tc)
+    // the root pop's classification: marks it known, writes its jobs, returns their number;
+    // fin: a neighbour lies past the stage's max distance
+    auto classify = [&](bool& fin) -> int {
       const int ix = h.bx(1), iz = h.bz(1);
       if (tid == 0) L->S[iz * nx + ix] = 0;
       int n = 0;
+      bool finished = false;
       if (AF_INIT_PARCLS) {
         // lane d < 4: neighbour d in the reference's order (x - 1, x + 1, z - 1, z + 1)
         const int d = tid & 3;
@@ -526,9 +549,9 @@ AF_DEV void stage_loop(Heap& h, const DevModel& M, const StageCfg& c, int tid) {
         const bool inb = tid < 4 && (d < 2 ? (0 <= xx && xx <= nx - 1) : (0 <= zz && zz <= nz - 1));
         const int st = inb ? (int)L->S[zz * nx + xx] : 0;
         const bool job = inb && (st == -1 || st > 0);
-        const bool fin = tid < 4 && !inb && (d < 2 ? abs(c.isx - xx) : abs(c.isz - zz)) == c.max_dist + 1;
+        const bool out = tid < 4 && !inb && (d < 2 ? abs(c.isx - xx) : abs(c.isz - zz)) == c.max_dist + 1;
         const unsigned long long jm = __ballot(job);
-        if (__ballot(fin)) finished = true;
+        if (__ballot(out)) finished = true;
         if (job)
           L->job[__popcll(jm & ((1ull << tid) - 1ull))] =
               job_pack(zz, xx, st == -1 ? kJobAdd : (kJobUpd | (d < 2 && c.quirk ? kJobQuirk : 0)));
@@ -559,8 +582,43 @@ AF_DEV void stage_loop(Heap& h, const DevModel& M, const StageCfg& c, int tid) {
           }
         }
       }
+      fin = finished;
+      return n;
+    };
+    // a pop classified (and its jobs handed over) while the previous pop's last sift-up was due
+    int pre_n = -1;
+    bool pre_fin = false;
+    while (h.ntr > 0 && !finished && !h.err) {
+      AF_DG_T0(tc)
+      int n;
+      const bool posted = pre_n >= 0;
+      if (posted) {
+        n = pre_n;
+        finished = pre_fin;
+        pre_n = -1;
+      } else {
+        n = classify(finished);
+      }
       AF_DG_ADD(L, 3, tc)
-      if (!pop_two_role(h, seq, jobs, n)) h.err = 1;
+      // the next pop is known before the last job's sift-up when that job can neither reach the
+      // root (its key is not below the root's: sift-ups move on strict '<') nor be the root, and no
+      // node has two heap entries (their keys follow ttn); it is then classified and handed over
+      // first.  The heap operations keep the reference's order (this sift-up, then the next pop's
+      // downtree); the next pop's relaxations read ttn and validity only, which sift-ups never touch
+      auto early = [&](double key, int cell) {
+        if (!AF_INIT_EARLY || finished || h.err || h.ndup || h.ntr < 1 || key < L->hkey[1] ||
+            (int)L->hcell[1] == cell)
+          return;
+        bool f2 = false;
+        const int n2 = classify(f2);
+        pre_n = n2;
+        pre_fin = f2;
+        if (n2 > 0) {
+          L->njob = n2;
+          post(&L->cmd, ++seq);
+        }
+      };
+      if (!pop_two_role(h, seq, jobs, n, posted, early)) h.err = 1;
     }
     post(&L->cmd, -1);
   } else if (tid >= 64) {
