@@ -1,0 +1,9 @@
+#!/bin/bash
+# init walk (with the early hand-over): stage shortcut for changed entries (fs1) vs re-running the stage (fs0)
+O=gpurun_out/r5ah
+mkdir -p $O
+for v in fs0 fs1 fs0 fs1; do
+  ALIFMM_LIB=$PWD/variants/$v/libalifmm.so timeout -k 10 300 python -u tools/kbench.py $v 128 16 >> $O/kbench.jsonl 2>$O/$v.err || exit 1
+  ALIFMM_LIB=$PWD/variants/$v/libalifmm.so timeout -k 10 200 python -u tools/c3_bench.py | sed "s/^{/{\"variant\": \"$v\", /" >> $O/c3.jsonl 2>>$O/$v.err || exit 1
+done
+timeout -k 10 420 python -u -m pytest tests -m gpu -x -q --timeout 180 --timeout-method thread > $O/pytest.log 2>&1
