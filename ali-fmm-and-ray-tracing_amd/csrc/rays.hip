@@ -2,15 +2,16 @@
 //
 // One group of G lanes per ray (G = 16, 32 or 64: the smallest power of two >= the 6*sg+3
 // candidates of an axis plane, so subgrid 1 packs 4 rays into a wavefront; G = 64 loops over the
-// candidates when there are more).  Each step is uniform within the group except the candidate
+// candidates when there are more; G = 9 at subgrid 1 when the request fills the device with 7 rays
+// per wavefront, af_ray_group_lanes).  Each step is uniform within the group except the candidate
 // evaluation: lane i evaluates candidate i of the plane (6*sg+3 candidates on axis planes,
 // <= 5*sg+3 on diagonal planes), i.e. rec_TTF at the candidate plus the straight-segment time
 // time_between_points (:2835-2989, a DDA over coarse cells).  The parabolic local-minimum search
 // (:3192-3218) is a lexicographic (value, order) reduction over the group's lanes, which selects
 // exactly the candidate the reference's sequential strict-'<' scan selects.  ray_time (:2992-3022) is
-// accumulated segment by segment as the ray grows, i.e. in the reference's summation order, so
-// times match the CPU to the last bit
-// (the trigonometry is correctly rounded, cr_math.h).  All arithmetic is double precision.
+// summed after the walk, the group's lanes evaluating consecutive segments and lane order giving
+// the reference's left-to-right sum, so times match the CPU to the last bit (the trigonometry is
+// correctly rounded, cr_math.h).  All arithmetic is double precision.
 // Every candidate's time_between_points() is a chain of dependent reads (material id, material
 // record, stiffness row or group table, the trig tables): with LDSMAT the records, stiffness rows,
 // group table and the CR trig tables are staged in LDS once per workgroup, so only the material-id
@@ -34,17 +35,19 @@ struct Key {
 };
 AF_DEV bool key_less(const Key& a, const Key& b) { return a.v < b.v || (a.v == b.v && a.order < b.order); }
 
-// wavefronts per SIMD the kernel is compiled for (232 VGPRs at 2; 3 or 4 force fewer registers)
+// wavefronts per SIMD the kernel is compiled for (174 VGPRs at 2; 3 or 4 force fewer registers and
+// measured no faster, profiles/r5q; the LDS of a 4-wavefront block also allows two blocks per CU)
 #ifndef AF_RAY_WPE
 #define AF_RAY_WPE 2
 #endif
 // Material runs: time_between_points() evaluates the group velocity once per run of pieces in one
 // material; the lanes of a wavefront reach their runs' evaluations at different pieces, so the
 // one-lane loop re-issues the evaluation for every piece index at which any lane changes material.
-// tbp_wave walks every active lane's segment first (runs: material id and first piece), spreads
-// the runs' evaluations over the active lanes (rounds of one evaluation per lane), then walks the
-// pieces again and sums them in the reference's order.  The same values: a run's slowness depends
-// on its material record and the segment's angle only.
+// tbp_wave walks every active lane's segment first (runs: material id and first piece; the piece
+// lengths are kept in LDS), spreads the runs' evaluations over the active lanes (rounds of one
+// evaluation per lane), then sums the pieces in the reference's order (segments longer than the
+// kept pieces walk again).  The same values: a run's slowness depends on its material record and
+// the segment's angle only.
 #ifndef AF_RAY_BATCH
 #define AF_RAY_BATCH 1
 #endif
@@ -65,8 +68,9 @@ struct RayScratch {  // per wavefront
   double dist[64 * (kPc > 0 ? kPc : 1)];  // piece k of lane l: dist[64 k + l]
 };
 
-// the group-velocity evaluation, one copy in the kernel: inlined at every call site it put the
-// kernel's code past the instruction cache (AF_RAY_SLO_NOINLINE 0: inlined)
+// the group-velocity evaluation, one copy in the kernel: inlined at every call site the kernel's
+// code was 131 KB, out of line 18 + 27 KB at the same speed (profiles/r5q; AF_RAY_SLO_NOINLINE 0:
+// inlined)
 #ifndef AF_RAY_SLO_NOINLINE
 #define AF_RAY_SLO_NOINLINE 1
 #endif
