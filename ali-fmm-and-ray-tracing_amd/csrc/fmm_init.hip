@@ -5,9 +5,11 @@
 // are solved with the reference's own heap-ordered FMM: the heap (with its round-half-even parent,
 // SURVEY B-D3), the stage-1 nnz=nnx1 quirk (:1645, padded reads) and the hand-over order are
 // reproduced exactly, so the init region is the reference's up to device transcendental ulps.
-// The heap walk is inherently serial: one lane of wavefront 0 runs the heap, one lane of
-// wavefront 1 relaxes each pop's neighbours while the heap runs downtree (stage_loop); all lanes
-// clear LDS, fill the straight-ray footprint and decimate between stages.  Output: the decimated
+// The heap walk is inherently serial: wavefront 0 runs the heap (its sifts on one lane, a pop's
+// neighbour classification on four), wavefront 1 relaxes each pop's neighbours while the heap
+// runs downtree, and the next pop is handed over before the current pop's last sift-up when that
+// sift-up cannot reach the root (stage_loop); all lanes clear LDS, fill the straight-ray footprint
+// and decimate between stages.  Output: the decimated
 // stage-3 nodes that the band kernel hands over to the main grid (:2006-2040), as (cell, ttn,
 // class) triples.
 #define CR_LDS_TABLES  // cr_math.h tables in LDS (crm::lds_init at kernel start)
