@@ -96,11 +96,14 @@ static int host_threads() {
     const int v = atoi(e);
     if (v >= 1) n = v;
   }
-  return std::min(n, 32);
+  // contexts that upload models at the same time (update_parallel: one per GPU) share the share
+  return std::max(1, std::min(n, 32) / std::max(1, g_live_ctx.load()));
 }
 // fn(chunk, lo, hi) over nch contiguous chunks of [0, n), one thread each
-static void for_chunks(size_t n, int nch, const std::function<void(int, size_t, size_t)>& fn) {
-  if (nch <= 1 || n < 65536) {
+// (serially below min_n items: the default suits per-cell passes; row passes give a smaller one)
+static void for_chunks(size_t n, int nch, const std::function<void(int, size_t, size_t)>& fn,
+                       size_t min_n = 65536) {
+  if (nch <= 1 || n < min_n) {
     fn(0, 0, n);
     return;
   }
@@ -279,7 +282,10 @@ const char* alifmm_last_error(alifmm_ctx* ctx) { return ctx ? ctx->err.c_str() :
 
 int alifmm_set_option(alifmm_ctx* ctx, const char* name, double value) {
   if (!ctx || !name) return ALIFMM_E_ARG;
-  if (!strcmp(name, "cdelta") && value > 0) ctx->cdelta = value;
+  if (!strcmp(name, "cdelta") && value > 0) {
+    ctx->cdelta = value;
+    ctx->cdelta_set = true;
+  }
   else if (!strcmp(name, "r0") && value >= 0) ctx->r0 = value;
   else if (!strcmp(name, "cdelta_far") && value >= 0) ctx->cdelta_far = value;
   else if (!strcmp(name, "r_far") && value >= 0) ctx->r_far = value;
@@ -299,9 +305,10 @@ int alifmm_set_option(alifmm_ctx* ctx, const char* name, double value) {
 
 int alifmm_get_option(alifmm_ctx* ctx, const char* name, double* value) {
   if (!ctx || !name || !value) return ALIFMM_E_ARG;
-  if (!strcmp(name, "cdelta")) *value = ctx->cdelta;
+  if (!strcmp(name, "cdelta")) *value = band_cdelta(ctx);  // in force for the resident model
   else if (!strcmp(name, "r0")) *value = ctx->r0;
-  else if (!strcmp(name, "cdelta_far")) *value = ctx->cdelta_far;
+  else if (!strcmp(name, "cdelta_far")) *value = band_cdelta_far(ctx);
+  else if (!strcmp(name, "mat_jump")) *value = ctx->mat_jump;
   else if (!strcmp(name, "r_far")) *value = ctx->r_far;
   else if (!strcmp(name, "far_sg")) *value = ctx->far_sg;
   else if (!strcmp(name, "batch")) *value = ctx->batch;
@@ -320,6 +327,7 @@ int alifmm_get_option(alifmm_ctx* ctx, const char* name, double* value) {
   else if (!strcmp(name, "vmax")) *value = ctx->vmax;  // model's fastest speed (set_model; the exact-walk stop)
   else if (!strcmp(name, "nmat")) *value = ctx->nmat;  // distinct material records (0: past the id table)
   else if (!strcmp(name, "ray_lanes")) *value = ctx->last_ray_lanes;  // lanes per ray, last find_rays
+  else if (!strcmp(name, "ray_waves_per_simd")) *value = af_ray_waves_per_simd();  // ray kernel occupancy target
   // timings of the last alifmm_find_rays / alifmm_take_rays call (ms): ray kernel and point-packing
   // kernel (HIP events, summed over the launches), the whole call, and the kept points' copy-out
   else if (!strcmp(name, "ray_kernel_ms")) *value = ctx->t_ray_kernel;
@@ -394,6 +402,29 @@ int alifmm_set_model(alifmm_ctx* ctx, int nnz, int nnx, const double* veln, cons
     }
   }
   if (!(vmax > 0)) return fail(ctx, ALIFMM_E_ARG, "model has no positive velocity");
+  // material-interface density (band_cdelta): 4-neighbour pairs whose (veln, vel_map, velpn,
+  // stiffness row) differ, over all pairs; rows spread over the host threads
+  double jump = 0.0;
+  {
+    std::vector<long> cnt(std::max(1, nth), 0);
+    auto same = [&](size_t a, size_t b) {
+      return !memcmp(&veln[a], &veln[b], 8) && !memcmp(&vel_map[a], &vel_map[b], 8) && vp[a] == vp[b] &&
+             (!stif_den || sidx[a] == sidx[b]);
+    };
+    for_chunks((size_t)nnz, n < 65536 ? 1 : std::min(nth, nnz), [&](int c, size_t z0, size_t z1) {
+      long k = 0;
+      for (size_t z = z0; z < z1; z++)
+        for (int x = 0; x < nnx; x++) {
+          const size_t i = z * nnx + x;
+          if (x + 1 < nnx && !same(i, i + 1)) k++;
+          if (z + 1 < (size_t)nnz && !same(i, i + nnx)) k++;
+        }
+      cnt[c] = k;
+    }, 1);
+    long k = 0;
+    for (long v : cnt) k += v;
+    jump = (double)k / (double)((long)(nnz - 1) * nnx + (long)nnz * (nnx - 1));
+  }
   free_model(ctx);
   HIPCHK(dalloc(&ctx->d_veln, n));
   HIPCHK(dalloc(&ctx->d_vm, n));
@@ -453,7 +484,7 @@ int alifmm_set_model(alifmm_ctx* ctx, int nnz, int nnx, const double* veln, cons
           for (int z = (int)b0 * 8; z < std::min(nnz, (int)b1 * 8); z++)
             for (int x = 0; x < nnx; x++)
               mb[(((size_t)(z >> 3) * bp + (x >> 4)) << 7) | ((z & 7) << 4) | (x & 15)] = m8[(size_t)z * nnx + x];
-        });
+        }, n < 65536 ? SIZE_MAX : 1);
         HIPCHK(dalloc(&ctx->d_mid8b, mb.size()));
         HIPCHK(hipMemcpy(ctx->d_mid8b, mb.data(), mb.size(), hipMemcpyHostToDevice));
         ctx->mid8b_pitch = bp;
@@ -471,6 +502,7 @@ int alifmm_set_model(alifmm_ctx* ctx, int nnz, int nnx, const double* veln, cons
   ctx->gox = gox;
   ctx->goz = goz;
   ctx->vmax = vmax;
+  ctx->mat_jump = jump;
   if (ctx->nmat > 0) {  // fouds18_A() slownesses per material (band kernels' fallback)
     HIPCHK(dalloc(&ctx->d_mslo, 8 * (size_t)ctx->nmat));
     const af::DevModel M = dev_model(ctx);
@@ -726,10 +758,10 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
   P.nx = fx;
   P.dnx = ctx->dnx;
   P.dnz = ctx->dnz;
-  P.cdelta = ctx->cdelta;
+  P.cdelta = band_cdelta(ctx, sg);
   P.vmax = ctx->vmax;
   P.r0 = ctx->r0;
-  P.cdelta_far = sg <= ctx->far_sg ? ctx->cdelta_far : 0.0;
+  P.cdelta_far = sg <= ctx->far_sg ? band_cdelta_far(ctx, sg) : 0.0;
   P.r_far = ctx->r_far;
   P.capL = (int)capL;
   P.capC = (int)capC;

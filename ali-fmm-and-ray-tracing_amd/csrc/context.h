@@ -77,10 +77,16 @@ struct alifmm_ctx {
   double* d_gtab = nullptr;
   double* d_ptab = nullptr;
   // options
+  // band width (units of dnx / vmax): the caller's "cdelta" when set, else chosen from the model
+  // (band_cdelta: 0.5, narrowed to 0.2 on models whose material changes from cell to cell)
   double cdelta = 0.5, r0 = 40.0;
-  // band width 0.6 beyond r_far = 256 nodes (ramped in over 256 .. 512; profiles/r5i: 16 sources
-  // 169 -> 148 ms, 128 sources unchanged, parity envelope within 15 % of the uniform 0.5 band)
-  double cdelta_far = 0.6, r_far = 256.0;
+  bool cdelta_set = false;
+  double mat_jump = 0.0;  // set_model: fraction of 4-neighbour cell pairs whose materials differ
+  // band width beyond r_far = 256 nodes (ramped in over 256 .. 512; profiles/r5i: 16 sources
+  // 169 -> 148 ms, 128 sources unchanged, parity envelope within 15 % of the uniform 0.5 band):
+  // < 0 = 1.2 x the band width in force (0.6 at 0.5); 0 = off; > 0 = the caller's, never narrower
+  // than the band width in force (band_cdelta_far)
+  double cdelta_far = -1.0, r_far = 256.0;
   int far_sg = 1;  // largest subgrid the far band applies to (subgrid 9 weld rays: profiles/r5j)
   int exact_r = 20;
   void* team = nullptr;  // api.cpp CopyTeam: host copy threads of the pinned staging ring
@@ -143,6 +149,25 @@ struct alifmm_ctx {
   long stream_fallback = 0;  // last travel_into: fields copied after the kernel (not streamed)
   long exact_redo = 0;       // last travel (subgrid > 1): sources the LDS exact walk handed to the HBM walk
 };
+
+// the band width in force for the resident model on the subgrid-sg grid, and the far band's (0: off)
+static inline double band_cdelta(const alifmm_ctx* c, int sg = 1) {
+  if (c->cdelta_set) return c->cdelta;
+  // CPU band model vs the heap oracle (tools/cdelta_auto_sweep.py, profiles/r6_cdelta_auto_sweep.jsonl):
+  // at 0.5 every swept model stays below 6.1e-3 except per-cell random orientation + vel_map
+  // (jump fraction ~1: 1.16e-2 on the 61^2 test model); at 0.2 every swept model is <= 4e-5.
+  // The fraction is per pair of the band's grid (the model's / sg on the subgrid-sg grid); every
+  // BASELINE config keeps 0.5 (C2 weld 0.178, C3 0.0066, C4 0.020)
+  const double j = c->mat_jump / sg, j0 = 0.3, j1 = 0.6, lo = 0.2;
+  if (j <= j0) return c->cdelta;
+  if (j >= j1) return lo;
+  return c->cdelta + (lo - c->cdelta) * (j - j0) / (j1 - j0);
+}
+static inline double band_cdelta_far(const alifmm_ctx* c, int sg = 1) {
+  if (c->cdelta_far == 0.0) return 0.0;
+  const double cd = band_cdelta(c, sg);
+  return c->cdelta_far < 0 ? 1.2 * cd : std::max(c->cdelta_far, cd);
+}
 
 static inline int fail(alifmm_ctx* c, int code, const char* fmt, ...) {
   char buf[512];

@@ -121,6 +121,9 @@ constexpr int kHash = 1 << kHashLog;
 #ifndef AF_PROF_SPILL
 #define AF_PROF_SPILL 0
 #endif
+#ifndef AF_PROF_CLAIM  // diagnostic: sub[2] = the accepted list's tile sort, sub[3] = the claim's closing drain
+#define AF_PROF_CLAIM 0
+#endif
 #ifndef AF_PROF_FBWAIT
 #define AF_PROF_FBWAIT 0
 #endif
@@ -284,6 +287,16 @@ struct SbLayout {
 #endif
   }
 };
+
+// known: 0 (hand-over) or the acceptance stamp -(2 + step) (AF_CLAIM_OWN); far -1; close 1 + slot
+AF_DEV bool sb_known(int s) { return s == 0 || s < -1; }
+#ifndef AF_CLAIM_OWN
+#define AF_CLAIM_OWN 1
+#endif
+#ifndef AF_CLAIM_OWN_U
+#define AF_CLAIM_OWN_U 2
+#endif
+constexpr int kCU = AF_CLAIM_OWN_U;  // claim items per lane and pass (AF_CLAIM_OWN)
 
 // 12-point neighbourhood of an interior cell (no other member's columns in reach) from Tb; same
 // values and validity as NbFieldT::load (rows past the grid invalid; other out-of-grid positions
@@ -784,6 +797,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
     asm volatile("" : "+v"(tid));
     const int lane = tid & 63, wv = tid >> 6;
     const int par = (int)(steps & 1), prv = par ^ 1;
+    const int stampA = -2 - (int)steps;  // status of the cells accepted in this step (AF_CLAIM_OWN)
     double* const Epar = E0 + par * ecells;
     const double* const Eprv = E0 + prv * ecells;
     const int eprv = tbc + prv * ecells;  // Eprv as an index from Tb
@@ -814,7 +828,8 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
         }
       }
     }
-    for (int k = tid * 4; k < kHash; k += kThreads * 4) *(int4*)&sh->H[k] = make_int4(0, 0, 0, 0);
+    if (!AF_CLAIM_OWN)
+      for (int k = tid * 4; k < kHash; k += kThreads * 4) *(int4*)&sh->H[k] = make_int4(0, 0, 0, 0);
 #if AF_SORT_ACC
     for (int k = tid; k < kSortB; k += kThreads) sh->Sb[k] = 0;
 #endif
@@ -834,7 +849,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
     const long long tdr = prof ? wall_clock64() : 0;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores have completed
     __syncthreads();
-#if !AF_PROF_FBWAIT && !AF_PROF_SPILL
+#if !AF_PROF_FBWAIT && !AF_PROF_SPILL && !AF_PROF_CLAIM
     AF_SUBT(3, tdr)
 #endif
     if (hstream && !sh->hsoff) {
@@ -961,7 +976,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
               sh->err = 2;
             } else {
               AL.put(sa, c[u]);
-              gst(Sb + SL.at(pkz(c[u]), pkx(c[u])), (int)kKnown);
+              gst(Sb + SL.at(pkz(c[u]), pkx(c[u])), AF_CLAIM_OWN ? stampA : (int)kKnown);
               if (hstream) tile_known(sh, ts, pkz(c[u]), pkx(c[u]), par);
               if (LO) {
                 Lt.put_lds(e, INFINITY);
@@ -1011,6 +1026,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
     AF_TICK(1)
     const int nA = min(sh->nA, capL), nRx = min(sh->nRx, capC);
     int* alist = sh->Al;
+    const long long tso = prof ? wall_clock64() : 0;
 #if AF_SORT_ACC
     if (nA > AF_SORT_ACC && nA <= kAcap) {  // (uniform) counting sort of the accepted list by tile
       for (int a = tid; a < nA; a += kThreads) atomicAdd(&sh->Sb[tile_bucket(sh->Al[a])], 1);
@@ -1034,12 +1050,100 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
       alist = sh->As;
     }
 #endif
+#if AF_PROF_CLAIM
+    AF_SUBT(2, tso)
+#endif
     // ---- P3b: claim ----
     const int nItems = 4 * nA + nRx;
-    const bool use_hash = nItems <= kHashItems;
+    const bool use_hash = !AF_CLAIM_OWN && nItems <= kHashItems;
     const bool lds_items = nA <= kAcap && nRx <= kRcap;
     const int stamp = (int)steps;
-    for (int q0 = AF_CLAIM_SPREAD ? 0 : wv * 64 * kClaimU; q0 < nItems; q0 += kThreads * kClaimU) {
+    // one claimed cell per lane (r >= 0, status s): far or close non-known cells join the interior
+    // or the boundary list (one LDS atomic per wave for both)
+    auto emit = [&](int rr, int ss) {
+      const bool take = rr >= 0 && !sb_known(ss);
+      const bool bnd = take && g.edge(pkx(rr));
+      const unsigned long long mi = __ballot(take && !bnd), mb = __ballot(bnd);
+      if ((mi | mb) == 0) return;
+      unsigned long long base2 = 0;
+      if (lane == 0)
+        base2 = atomicAdd(&sh->nE2, (unsigned long long)__popcll(mi) | ((unsigned long long)__popcll(mb) << 32));
+      base2 = __shfl(base2, 0);
+      const unsigned long long lt = (1ull << lane) - 1ull;
+      const int slot = ss > 0 ? ss - 1 : -1;
+      if ((mi >> lane) & 1ull) {
+        const int pos = (int)(unsigned)base2 + __popcll(mi & lt);
+        if (pos < capC) {
+          EL.put(pos, rr);
+          EP.put(pos, slot);
+        } else {
+          sh->err = 2;
+        }
+      }
+      if ((mb >> lane) & 1ull) {
+        const int pos = (int)(unsigned)(base2 >> 32) + __popcll(mb & lt);
+        if (pos < capC) {
+          BL.put(pos, rr);
+          BP.put(pos, slot);
+        } else {
+          sh->err = 2;
+        }
+      }
+    };
+    // Claim by ownership (AF_CLAIM_OWN): no deduplication structure.  A cell c next to accepted
+    // cells is claimed by exactly one item: the own accepted neighbour a = c - dir[d] with the
+    // lowest direction d, else (no own accepted neighbour) the neighbour member's rim cell (RX
+    // item; a cell has at most one neighbour across a stripe boundary).  "Accepted this step" is
+    // the status stamp the accept scan wrote (-(2 + step)), so an item loads c's status and those
+    // of c's own neighbours in the directions before its own — all loads of a lane's kCU items
+    // issued together: one memory round trip per pass of kThreads * kCU items (the hash claim
+    // below waits for LDS atomics and a status load in every pass of kThreads items).
+    if (AF_CLAIM_OWN) {
+      for (int q0 = 0; q0 < nItems; q0 += kThreads * kCU) {
+        int r[kCU], s[kCU], pn[kCU][4];
+        unsigned pm[kCU];
+#pragma unroll
+        for (int u = 0; u < kCU; u++) {
+          const int q = q0 + u * kThreads + tid;
+          int c = -1, dd = 4;
+          if (q < nItems) {
+            if (q < 4 * nA) {
+              dd = q & 3;
+              c = nb_cell(lds_items ? alist[q >> 2] : AL.get(q >> 2), dd, nz, nx);
+              if (c >= 0 && g.owner(pkx(c)) != me) c = -1;  // claimed by its owner (from my rim list)
+            } else {
+              c = lds_items ? RX.lds(q - 4 * nA) : RX.get(q - 4 * nA);
+            }
+          }
+          r[u] = c;
+          unsigned m = 0;
+          if (c >= 0) {
+            const int z = pkz(c), x = pkx(c);
+            // a' = c - dir[d']: (z, x + 1), (z, x - 1), (z + 1, x), (z - 1, x)
+            if (dd > 0 && x + 1 < nx && g.owner(x + 1) == me) m |= 1u;
+            if (dd > 1 && x > 0 && g.owner(x - 1) == me) m |= 2u;
+            if (dd > 2 && z + 1 < nz) m |= 4u;
+            if (dd > 3 && z > 0) m |= 8u;
+          }
+          pm[u] = m;
+        }
+#pragma unroll
+        for (int u = 0; u < kCU; u++) {
+          const int z = pkz(max(r[u], 0)), x = pkx(max(r[u], 0));
+          s[u] = r[u] >= 0 ? gld(Sb + SL.at(z, x)) : (int)kKnown;
+          pn[u][0] = (pm[u] & 1u) ? gld(Sb + SL.at(z, x + 1)) : 0;
+          pn[u][1] = (pm[u] & 2u) ? gld(Sb + SL.at(z, x - 1)) : 0;
+          pn[u][2] = (pm[u] & 4u) ? gld(Sb + SL.at(z + 1, x)) : 0;
+          pn[u][3] = (pm[u] & 8u) ? gld(Sb + SL.at(z - 1, x)) : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < kCU; u++) {
+          const bool mine = pn[u][0] != stampA && pn[u][1] != stampA && pn[u][2] != stampA && pn[u][3] != stampA;
+          emit(mine && !sb_known(s[u]) ? r[u] : -1, s[u]);
+        }
+      }
+    }
+    for (int q0 = AF_CLAIM_SPREAD ? 0 : wv * 64 * kClaimU; q0 < (AF_CLAIM_OWN ? 0 : nItems); q0 += kThreads * kClaimU) {
       int r[kClaimU], s[kClaimU], o[kClaimU];
       const long long tdd = prof ? wall_clock64() : 0;
       unsigned hh[kClaimU];
@@ -1111,7 +1215,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
       int ci = 0, cb = 0;
 #pragma unroll
       for (int u = 0; u < kClaimU; u++) {
-        const bool take = r[u] >= 0 && s[u] != kKnown && o[u] < stamp;
+        const bool take = r[u] >= 0 && !sb_known(s[u]) && o[u] < stamp;
         const bool bnd = take && g.edge(pkx(r[u]));
         bi[u] = __ballot(take && !bnd);
         bb[u] = __ballot(bnd);
@@ -1152,8 +1256,17 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
     }
     // this step's edge-buffer stores (accept scan, P0) precede this step's commits to the same
     // addresses (a wave that issued no load since has not waited for them yet)
-    if (K > 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const long long tcw = prof ? wall_clock64() : 0;
+#ifndef AF_DRAIN_LATE
+#define AF_DRAIN_LATE 0
+#endif
+    // (AF_DRAIN_LATE: the same wait placed before the commit's barrier instead, where the stores
+    // have long completed)
+    if (K > 1 && !AF_DRAIN_LATE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+#if AF_PROF_CLAIM
+    AF_SUBT(3, tcw)
+#endif
     const int nEi = min((int)(unsigned)sh->nE2, capC);
     const int nEb = min((int)(unsigned)(sh->nE2 >> 32), capC - nEi);
     if (nEb > 0) {  // boundary cells after the interior ones
@@ -1237,7 +1350,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
             const long f = (long)zz * nx + xx;
             if (g.owner(xx) == me) {
               t = far0(gld(Tb + TL.at(zz, xx)));
-              kn = gld(Sb + SL.at(zz, xx)) == kKnown;
+              kn = sb_known(gld(Sb + SL.at(zz, xx)));
             } else {  // known at the end of the last step (sign), or accepted now (close, T <= thr)
               const double ev = gld_sc1(Eprv + g.eidx(zz, xx));
               t = far0(fabs(ev));
@@ -1289,6 +1402,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
         __syncthreads();
       }
     }
+    if (K > 1 && AF_DRAIN_LATE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     AF_TICK(4)
     // ---- P5: commit own cells; edge cells also into this step's edge buffer (slot marked DIRTY:

@@ -63,6 +63,7 @@ def parse():
     ap.add_argument("--gather", action="store_true", help="N > 1: also time an RCCL gather of all fields to rank 0")
     ap.add_argument("--members", type=int, default=None, help="band-kernel workgroups per source (0: auto)")
     ap.add_argument("--cdelta", type=float, default=None)
+    ap.add_argument("--no-c5", action="store_true", help="skip the BASELINE config 5 leg (receiver fields + rays)")
     return ap.parse_args()
 
 
@@ -274,6 +275,70 @@ def c3_line(ctx, W):
     return out
 
 
+C5_PER_SIDE = 256
+
+
+def c5_receivers(rank, world):
+    """BASELINE config 5's receivers of this rank: the 256 bottom transducers (x = 8 + 16 k,
+    z = 4095) dealt block-cyclically (sharding.deal), as find_all_TTF_rays_parallel hands each
+    worker whole receivers and traces a receiver's rays in the process that built its field
+    (parallel_TTF_rays, Anis_TTF_rays.py:3715-3733, :4550-4685)."""
+    import sharding
+
+    return np.array(sharding.deal(range(C5_PER_SIDE), world)[rank], dtype=np.int64)
+
+
+def c5_leg(ctx, rank, world, dist, n, dnx, barrier):
+    """BASELINE config 5 after the C4 steps: 256 top transducers (z = 0) firing into 256 bottom
+    receivers (trans_pairs[i, 256 + j] = 1, the pattern of Weld_rays.py:52-55): each rank builds its
+    receivers' fields (resident) and traces their 256 rays each (times only), then the (256, 256)
+    times matrix is gathered to rank 0 (gloo: 512 KB).  Timed: fields + rays, max over ranks."""
+    ctx.release_fields()
+    xs = (8 + 16 * np.arange(C5_PER_SIDE)).astype(np.float64)
+    mine = c5_receivers(rank, world)
+    rx = xs[mine]
+    src = np.stack([xs, np.zeros(C5_PER_SIDE)], 1)
+    # warm-up: the travel arena and the ray buffers at the timed call's size (kept by the context)
+    ctx.travel(dnx * rx[:2], np.full(min(2, len(rx)), dnx * (n - 1)), first_slot=0, copy_out=False)
+    nr = len(rx) * C5_PER_SIDE
+    ctx.find_rays(np.zeros(nr, dtype=np.int32), np.tile(src, (len(rx), 1)),
+                  np.tile([rx[0], float(n - 1)], (nr, 1)), with_points=False)
+    barrier()
+    t0 = time.perf_counter()
+    ctx.travel(dnx * rx, np.full(len(rx), dnx * (n - 1)), first_slot=0, copy_out=False)
+    t1 = time.perf_counter()
+    slots = np.repeat(np.arange(len(rx)), C5_PER_SIDE)
+    s_xy = np.tile(src, (len(rx), 1))
+    r_xy = np.repeat(np.stack([rx, np.full(len(rx), float(n - 1))], 1), C5_PER_SIDE, axis=0)
+    times, lens, flags, _ = ctx.find_rays(slots, s_xy, r_xy, with_points=False)
+    t2 = time.perf_counter()
+    barrier()
+    total = max_over_ranks(t2 - t0, dist)
+    fields_s = max_over_ranks(t1 - t0, dist)
+    rays_s = max_over_ranks(t2 - t1, dist)
+    part = (mine.tolist(), times.reshape(len(rx), C5_PER_SIDE).tolist(), int(lens.sum()))
+    parts = [part]
+    if dist is not None:
+        parts = [None] * world
+        dist.all_gather_object(parts, part)
+    ctx.release_fields()
+    if rank != 0:
+        return None
+    tm = np.full((C5_PER_SIDE, C5_PER_SIDE), np.nan)  # [source i, receiver j]
+    for js, tj, _ in parts:
+        for j, row in zip(js, tj):
+            tm[:, j] = row
+    rays = C5_PER_SIDE * C5_PER_SIDE
+    return {"workload": "C5: 4096x4096 weld-like grid, 256 top Tx (z=0) -> 256 bottom Rx (z=4095), x = 8 + 16 k: "
+                        "256 receiver fields (subgrid 1) dealt over the GPUs + 65 536 rays on the receiver's GPU",
+            "total_s": total, "fields_s": fields_s, "rays_s": rays_s, "rays": rays, "rays_per_s": rays / total,
+            "fields_per_s": C5_PER_SIDE / total, "receivers_per_gpu": [len(p[0]) for p in parts],
+            "points": int(sum(p[2] for p in parts)),
+            "times_complete": bool(np.all(np.isfinite(tm)) and np.all(tm > 0)),
+            "times_checksum": float(np.sum(tm)),
+            "times": "gathered to rank 0 as the (256, 256) matrix (gloo)"}
+
+
 def cpu_baseline(args, scx, scz, model, vt, dnx, cells):
     """the C restatement of the reference's solver, one source per thread on the
     CPUs this job is granted (affinity and cgroup quota), plus one source on one core; the
@@ -336,8 +401,14 @@ def main():
             dist.all_gather_object(got, [int(i) for i in ids])
         else:
             got = [[int(i) for i in ids]]
+        rec = [None] * world
+        if dist is not None:
+            dist.all_gather_object(rec, c5_receivers(rank, world).tolist())
+        else:
+            rec = [c5_receivers(0, 1).tolist()]
         if rank == 0:
-            print(json.dumps({"stub": True, "n_gpus": ran, "sources_per_rank": got}), flush=True)
+            print(json.dumps({"stub": True, "n_gpus": ran, "sources_per_rank": got, "c5_receivers_per_rank": rec}),
+                  flush=True)
         if dist is not None:
             dist.destroy_process_group()
         return
@@ -468,6 +539,9 @@ def main():
         del F
         for c in M._ctxs.values():
             c.close()
+    c5 = None
+    if not args.no_c5:
+        c5 = c5_leg(ctx, rank, world, dist, n, dnx, barrier)
     c3 = None
     if world == 1 and not args.no_c3:
         c3 = c3_line(ctx, W)
@@ -512,6 +586,7 @@ def main():
             "result_return": ret,
             "update_end_to_end": e2e,
             "c3": c3,
+            "c5": c5,
             "cpu_baseline": cpu,
         }
         if cpu:

@@ -41,7 +41,8 @@ const char* alifmm_last_error(alifmm_ctx* ctx);
  *   vel_map  (nnz, nnx) float64  velocity scale
  *   stif_den (nnz, nnx, 5) int64 c22, c23, c33, c44 [MPa], density [kg/m^3]; NULL = None
  *   group_tab, phase_tab (361, ncol) float64  velocity tables (ALI_FMM.velocity_dat / phase_vel)
- *   dnx, dnz grid spacing [m]; gox, goz origin [m]                                            */
+ *   dnx, dnz grid spacing [m]; gox, goz origin [m]
+ * ncol must be below 32768 (the init kernels pack velpn and ncol into one int): ALIFMM_E_ARG.    */
 int alifmm_set_model(alifmm_ctx* ctx, int nnz, int nnx, const double* veln, const int64_t* velpn,
                      const double* vel_map, const int64_t* stif_den, const double* group_tab,
                      const double* phase_tab, int ncol, double dnx, double dnz, double gox, double goz);
@@ -49,19 +50,25 @@ int alifmm_set_model(alifmm_ctx* ctx, int nnz, int nnx, const double* veln, cons
 /* Tuning: "members" (workgroups per source of the band kernel: 0 = as many as the device holds
  * for the batch, else 1 .. 16; results are bit-identical for every value), "stripe_log"
  * (column-stripe width log2 of the band kernel's ownership, 0 = automatic), "prof" (1: record the
- * band profile, alifmm_band_profile), "cdelta" (band width in units of dnx/vmax, default 0.5),
+ * band profile, alifmm_band_profile), "cdelta" (band width in units of dnx/vmax; unset, the
+ * library chooses it per model: 0.5, narrowed down to 0.2 where the materials change from cell to
+ * cell — fraction of neighbour pairs with different materials ("mat_jump", / subgrid) from 0.3 to
+ * 0.6; get_option reads the subgrid-1 value),
  * "r0" (near-source band schedule radius in cells, default 40), "exact_r" (radius in cells of the
  * exact heap-ordered main-loop prefix, 0..48, default 20), "batch" (sources per launch, default
  * 256), "exact_lds" (subgrid > 1: 1 = the exact walk with its state in LDS, fmm_exact_lds.hip,
  * where the stage grids fit — subgrid <= 9; 0 = the HBM walk, fmm_exact.hip; bit-identical),
  * "coop" (band launch: 1 = cooperative, 0 = plain after a residency check), "cdelta_far" /
  * "r_far" (band width beyond Tmin = r_far * dnx / vmax, ramped in over r_far .. 2 r_far; default
- * 0.6 from 256 cells; cdelta_far 0 = one width everywhere), "far_sg" (the largest subgrid the
+ * 1.2 x the band width in force from 256 cells (0.6 at 0.5); a value set is never narrower than
+ * the band width in force; cdelta_far 0 = one width everywhere), "far_sg" (the largest subgrid the
  * far band applies to, default 1), "stream_out" (subgrid-1 travels
  * with a host destination stream the fields out of the band kernel, alifmm_travel_into; default 1). */
 int alifmm_set_option(alifmm_ctx* ctx, const char* name, double value);
 /* Read an option, or "last_k" (workgroups per source of the last band launch), "n_cu"
- * (compute units of the device), "vmax" (the model's fastest speed [m/s]: the exact prefix
+ * (compute units of the device), "cdelta" / "cdelta_far" (the widths in force for the resident
+ * model), "mat_jump" (the model's fraction of 4-neighbour cell pairs whose materials differ),
+ * "vmax" (the model's fastest speed [m/s]: the exact prefix
  * covers T <= exact_r * dnx / vmax), "stream_tail_ms" and "stream_fallback" (last travel with a host
  * destination: ms from the band kernel's end to the last streamed tile copied; fields copied after
  * the launch instead of streamed), "exact_redo" (last travel, subgrid > 1: sources the LDS exact

@@ -343,6 +343,10 @@ def test_bench_launches_its_own_ranks(world):
     per = line["sources_per_rank"]
     assert len(per) == world and sorted(sum(per, [])) == list(range(128))
     assert max(map(len, per)) - min(map(len, per)) <= 1
+    # the C5 leg's deal: every one of the 256 bottom receivers on exactly one rank (its rays with it)
+    rec = line["c5_receivers_per_rank"]
+    assert len(rec) == world and sorted(sum(rec, [])) == list(range(256))
+    assert max(map(len, rec)) - min(map(len, rec)) <= 1
 
 
 def test_bench_refuses_more_gpus_than_visible():
