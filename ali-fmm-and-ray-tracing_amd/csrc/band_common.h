@@ -22,6 +22,7 @@ struct HList {
 
 AF_DEV int lane_id() { return threadIdx.x & 63; }
 
+
 // Uniform double kept in (and re-read from) scalar registers: the compiler cannot hoist
 // expressions derived from it above this point.  The persistent band kernels launder their
 // step-invariant doubles per phase so that derived constants are not kept live (and spilled to
@@ -41,7 +42,7 @@ AF_DEV int wave_push(int* counter, bool pred, int cap, int* err) {
   int leader = __ffsll((long long)m) - 1;
   int base = 0;
   if (lane == leader) base = atomicAdd(counter, __popcll(m));
-  base = __shfl(base, leader);
+  base = bcast(base, leader);
   int off = __popcll(m & ((1ull << lane) - 1ull));
   if (!pred) return -1;
   int slot = base + off;
@@ -64,8 +65,8 @@ AF_DEV void wave_push2(int* c1, int* c2, bool pred, int cap, int* err, int& s1, 
     b1 = atomicAdd(c1, __popcll(m));
     b2 = atomicAdd(c2, __popcll(m));
   }
-  b1 = __shfl(b1, leader);
-  b2 = __shfl(b2, leader);
+  b1 = bcast(b1, leader);
+  b2 = bcast(b2, leader);
   if (!pred) return;
   int off = __popcll(m & ((1ull << lane) - 1ull));
   s1 = b1 + off;
@@ -79,6 +80,49 @@ AF_DEV void wave_push2(int* c1, int* c2, bool pred, int cap, int* err, int& s1, 
 AF_DEV double wave_min(double v) {
   for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
   return v;
+}
+
+// Wave reductions by DPP moves inside each row of 16 lanes (quad xor 1, quad xor 2, half-row
+// mirror, row mirror) and v_readlane of the four rows: no LDS round trips (a __shfl_xor ladder is
+// six ds_bpermute round trips, twelve for a double).  EVERY lane of the wave must be active.
+template <int CTRL>
+AF_DEV int dppm_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false);
+}
+template <int CTRL>
+AF_DEV double dppm_d(double v) {
+  const long long b = __double_as_longlong(v);
+  const unsigned lo = (unsigned)dppm_i<CTRL>((int)b), hi = (unsigned)dppm_i<CTRL>((int)(b >> 32));
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+AF_DEV double rdlane_d(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)b, l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+AF_DEV double wave_min_full(double v) {
+  v = fmin(v, dppm_d<0xB1>(v));
+  v = fmin(v, dppm_d<0x4E>(v));
+  v = fmin(v, dppm_d<0x141>(v));
+  v = fmin(v, dppm_d<0x140>(v));
+  return fmin(fmin(rdlane_d(v, 0), rdlane_d(v, 16)), fmin(rdlane_d(v, 32), rdlane_d(v, 48)));
+}
+AF_DEV int wave_sum_full(int v) {
+  v += dppm_i<0xB1>(v);
+  v += dppm_i<0x4E>(v);
+  v += dppm_i<0x141>(v);
+  v += dppm_i<0x140>(v);
+  return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) + __builtin_amdgcn_readlane(v, 32) +
+         __builtin_amdgcn_readlane(v, 48);
+}
+AF_DEV int wave_or_full(int v) {
+  v |= dppm_i<0xB1>(v);
+  v |= dppm_i<0x4E>(v);
+  v |= dppm_i<0x141>(v);
+  v |= dppm_i<0x140>(v);
+  return __builtin_amdgcn_readlane(v, 0) | __builtin_amdgcn_readlane(v, 16) | __builtin_amdgcn_readlane(v, 32) |
+         __builtin_amdgcn_readlane(v, 48);
 }
 
 // Lists hold cells as packed (z << 16 | x) keys (grids are < 32768 per side): no integer
@@ -95,16 +139,18 @@ AF_DEV int nb_cell(int c, int d, int nz, int nx) {
   return (z < 0 || z >= nz || x < 0 || x >= nx) ? -1 : pk(z, x);
 }
 
-// exclusive prefix sum over the wave's lanes, and the wave total
+// exclusive prefix sum over the wave's lanes, and the wave total: DPP row shifts (1, 2, 4, 8)
+// then row broadcasts 15 / 31 (a disabled source lane contributes the 0 "old" value); EVERY
+// lane of the wave must be active
 AF_DEV int wave_excl_scan(int v, int& total) {
-  const int lane = threadIdx.x & 63;
   int inc = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int t = __shfl_up(inc, o);
-    if (lane >= o) inc += t;
-  }
-  total = __shfl(inc, 63);
+  inc += __builtin_amdgcn_update_dpp(0, inc, 0x111, 0xf, 0xf, false);  // row_shr:1
+  inc += __builtin_amdgcn_update_dpp(0, inc, 0x112, 0xf, 0xf, false);  // row_shr:2
+  inc += __builtin_amdgcn_update_dpp(0, inc, 0x114, 0xf, 0xf, false);  // row_shr:4
+  inc += __builtin_amdgcn_update_dpp(0, inc, 0x118, 0xf, 0xf, false);  // row_shr:8
+  inc += __builtin_amdgcn_update_dpp(0, inc, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  inc += __builtin_amdgcn_update_dpp(0, inc, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+  total = bcast(inc, 63);
   return inc - v;
 }
 

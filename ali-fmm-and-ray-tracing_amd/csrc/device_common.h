@@ -71,6 +71,15 @@ constexpr double kRad2Deg = 180.0 / M_PI;
 // Fast paths for |a| < 2b (every call site: angles mod 180/90/pi) give the same bits as the
 // generic fmod route: fmod(a, b) is exact, and a -/+ b is exact there by Sterbenz's lemma; the
 // only rounding is the final '+ b' of negative remainders, which the reference performs too.
+// value of lane l (wave-uniform l) for every lane: v_readlane into a scalar register, no LDS round
+// trip (a __shfl from one lane is a ds_bpermute: an LDS round trip in the wave's dependent chain)
+AF_DEV int bcast(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+AF_DEV unsigned long long bcast64(unsigned long long v, int l) {
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), l);
+  return ((unsigned long long)hi << 32) | lo;
+}
+
 AF_DEV double pymod(double a, double b) {
   if (b > 0) {
     if (a >= 0 && a < b) return a == 0 ? 0.0 : a;  // -0.0 -> +0.0 as copysign(0, b)

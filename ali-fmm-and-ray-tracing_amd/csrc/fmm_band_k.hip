@@ -115,6 +115,16 @@ constexpr int kHash = 1 << kHashLog;
 #ifndef AF_CLAIM_SPREAD
 #define AF_CLAIM_SPREAD 1
 #endif
+#ifndef AF_CLAIM_OWN
+#define AF_CLAIM_OWN 1
+#endif
+#ifndef AF_CLAIM_OWN_U
+#define AF_CLAIM_OWN_U 2
+#endif
+constexpr int kCU = AF_CLAIM_OWN_U;  // claim items per lane and pass (AF_CLAIM_OWN)
+#ifndef AF_FB_ROUND
+#define AF_FB_ROUND (128 >> (13 - AF_HASHLOG_D))
+#endif
 #ifndef AF_DIAG_DBL
 #define AF_DIAG_DBL 0
 #endif
@@ -178,6 +188,9 @@ constexpr int kTileMax = ts::kOwnTileMax;
 #define AF_HS_U 4  // items per thread and batch of stage_tiles
 #endif
 
+// LDS of the claim hash: the hash claim's 8192 slots, else just the fallback's staging windows
+constexpr int kHashArr = AF_CLAIM_OWN ? (AF_FB_ROUND * 25 * 2) : kHash;
+
 struct Lds {
   double red[kWaves];
   double Lt[kLcap];  // close set: T of the slot (+inf: free)
@@ -195,7 +208,7 @@ struct Lds {
   int Dc[kDcap];  // edge cells accepted this step (copied forward next step) ...
   double Dv[kDcap];  // ... and their T
   int Rx[kRcap];  // claim items from the neighbour members' accepted rim cells; fallback list
-  alignas(16) int H[kHash];
+  alignas(16) int H[kHashArr];  // claim hash (the hash claim); fallback staging windows
 #if AF_SORT_ACC
   int As[kAcap];     // the accepted list in tile order
   int Sb[kSortB];    // bucket counts -> offsets
@@ -290,13 +303,6 @@ struct SbLayout {
 
 // known: 0 (hand-over) or the acceptance stamp -(2 + step) (AF_CLAIM_OWN); far -1; close 1 + slot
 AF_DEV bool sb_known(int s) { return s == 0 || s < -1; }
-#ifndef AF_CLAIM_OWN
-#define AF_CLAIM_OWN 1
-#endif
-#ifndef AF_CLAIM_OWN_U
-#define AF_CLAIM_OWN_U 2
-#endif
-constexpr int kCU = AF_CLAIM_OWN_U;  // claim items per lane and pass (AF_CLAIM_OWN)
 
 // 12-point neighbourhood of an interior cell (no other member's columns in reach) from Tb; same
 // values and validity as NbFieldT::load (rows past the grid invalid; other out-of-grid positions
@@ -374,11 +380,8 @@ AF_DEV void load_nb(NbFieldT& nb, const double* T, const TbLayout& L, int eprv, 
 // LDS — T at the end of the previous step (NaN -> 0 as GField) and known-ness (own cell: status 0;
 // another member's: known in the previous edge buffer, or close with T <= thr) — then one lane per
 // cell runs fouds18_A() on the staged window (few registers: the accessor is two LDS reads).
-#ifndef AF_FB_ROUND
-#define AF_FB_ROUND (128 >> (13 - AF_HASHLOG_D))
-#endif
 constexpr int kFbRound = AF_FB_ROUND;  // cells per staging round (25 doubles each in the claim-hash space)
-static_assert(kFbRound * 25 * sizeof(double) <= kHash * sizeof(int), "staging windows fit the claim hash");
+static_assert(kFbRound * 25 * sizeof(double) <= kHashArr * sizeof(int), "staging windows fit the claim hash");
 struct Win5 {
   const double* t;  // 25 values, row-major (dz + 2) * 5 + (dx + 2)
   unsigned known;   // bit (dz + 2) * 5 + (dx + 2)
@@ -552,7 +555,9 @@ AF_DEV bool x1_poll(KX* X, int K, int par, unsigned tag, Lds* sh, int mprev, int
     if (++spins > (1L << 25)) return false;
   }
   const unsigned w = (unsigned)v;
-  const unsigned w1 = __shfl_down(w, 1), w2 = __shfl_down(w, 2), w3 = __shfl_down(w, 3);
+  // words 1..3 of each member into its lane 4q (DPP quad permutes [1,2,3,3], [2,3,3,3], [3,3,3,3])
+  const unsigned w1 = (unsigned)dppm_i<0xF9>((int)w), w2 = (unsigned)dppm_i<0xFE>((int)w),
+                 w3 = (unsigned)dppm_i<0xFF>((int)w);
   double tmin = INFINITY;
   int live = 0, err = 0;
   if ((lane & 3) == 0 && lane < nw) {
@@ -563,11 +568,9 @@ AF_DEV bool x1_poll(KX* X, int K, int par, unsigned tag, Lds* sh, int mprev, int
     if (q == mprev) sh->nrim[0] = (int)(w3 & 0xffffffu);
     if (K > 2 && q == mnext) sh->nrim[1] = (int)(w3 & 0xffffffu);
   }
-  tmin = wave_min(tmin);
-  for (int o = 32; o > 0; o >>= 1) {
-    live += __shfl_xor(live, o);
-    err |= __shfl_xor(err, o);
-  }
+  tmin = wave_min_full(tmin);
+  live = wave_sum_full(live);
+  err = wave_or_full(err);
   if (lane == 0) {
     sh->tmin_g = tmin;
     sh->live_g = live;
@@ -833,7 +836,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
 #if AF_SORT_ACC
     for (int k = tid; k < kSortB; k += kThreads) sh->Sb[k] = 0;
 #endif
-    tmin = wave_min(tmin);
+    tmin = wave_min_full(tmin);
     if (lane == 0) sh->red[wv] = tmin;
     if (tid == 0) {
       sh->nA = 0;
@@ -963,8 +966,8 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
           ba = atomicAdd(&sh->nA, tot);
           bf = atomicAdd(&sh->nF, tot);
         }
-        ba = __shfl(ba, 0);
-        bf = __shfl(bf, 0);
+        ba = bcast(ba, 0);
+        bf = bcast(bf, 0);
         const unsigned long long lt = (1ull << lane) - 1ull;
 #pragma unroll
         for (int u = 0; u < kAccU; u++) {
@@ -1068,7 +1071,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
       unsigned long long base2 = 0;
       if (lane == 0)
         base2 = atomicAdd(&sh->nE2, (unsigned long long)__popcll(mi) | ((unsigned long long)__popcll(mb) << 32));
-      base2 = __shfl(base2, 0);
+      base2 = bcast64(base2, 0);
       const unsigned long long lt = (1ull << lane) - 1ull;
       const int slot = ss > 0 ? ss - 1 : -1;
       if ((mi >> lane) & 1ull) {
@@ -1099,8 +1102,12 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
     // issued together: one memory round trip per pass of kThreads * kCU items (the hash claim
     // below waits for LDS atomics and a status load in every pass of kThreads items).
     if (AF_CLAIM_OWN) {
+      // stripe crossings instead of owner(): with K > 1 a column next to one's own belongs to
+      // another member exactly when it lies across a stripe boundary
+      const int W1 = (1 << g.wlog) - 1;
+      const bool one = K == 1;
       for (int q0 = 0; q0 < nItems; q0 += kThreads * kCU) {
-        int r[kCU], s[kCU], pn[kCU][4];
+        int r[kCU], s[kCU], pn[kCU][4], si[kCU];
         unsigned pm[kCU];
 #pragma unroll
         for (int u = 0; u < kCU; u++) {
@@ -1109,32 +1116,52 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
           if (q < nItems) {
             if (q < 4 * nA) {
               dd = q & 3;
-              c = nb_cell(lds_items ? alist[q >> 2] : AL.get(q >> 2), dd, nz, nx);
-              if (c >= 0 && g.owner(pkx(c)) != me) c = -1;  // claimed by its owner (from my rim list)
+              const int ac = lds_items ? alist[q >> 2] : AL.get(q >> 2);
+              const int z = pkz(ac) + (dd == 2 ? -1 : dd == 3 ? 1 : 0);
+              const int x = pkx(ac) + (dd == 0 ? -1 : dd == 1 ? 1 : 0);
+              const int xa = pkx(ac) & W1;
+              // in the grid, and own (claimed by its owner from my rim list otherwise)
+              const bool ok = z >= 0 && z < nz && x >= 0 && x < nx &&
+                              (one || !((dd == 0 && xa == 0) || (dd == 1 && xa == W1)));
+              c = ok ? pk(z, x) : -1;
             } else {
               c = lds_items ? RX.lds(q - 4 * nA) : RX.get(q - 4 * nA);
             }
           }
           r[u] = c;
           unsigned m = 0;
+          int idx = 0;
           if (c >= 0) {
-            const int z = pkz(c), x = pkx(c);
-            // a' = c - dir[d']: (z, x + 1), (z, x - 1), (z + 1, x), (z - 1, x)
-            if (dd > 0 && x + 1 < nx && g.owner(x + 1) == me) m |= 1u;
-            if (dd > 1 && x > 0 && g.owner(x - 1) == me) m |= 2u;
+            const int z = pkz(c), x = pkx(c), xr = x & W1;
+            // a' = c - dir[d']: (z, x + 1), (z, x - 1), (z + 1, x), (z - 1, x); own iff not across
+            if (dd > 0 && x + 1 < nx && (one || xr != W1)) m |= 1u;
+            if (dd > 1 && x > 0 && (one || xr != 0)) m |= 2u;
             if (dd > 2 && z + 1 < nz) m |= 4u;
             if (dd > 3 && z > 0) m |= 8u;
+            idx = SL.at(z, x);
           }
           pm[u] = m;
+          si[u] = idx;
         }
+        // the neighbours' status indices from c's: within the 4 x 8 brick +-1 / +-8, else the
+        // neighbour brick (x: +-25, z: +-(32 pitch - 24))
+        const int zstep = 32 * SL.pitch - 24;
 #pragma unroll
         for (int u = 0; u < kCU; u++) {
-          const int z = pkz(max(r[u], 0)), x = pkx(max(r[u], 0));
-          s[u] = r[u] >= 0 ? gld(Sb + SL.at(z, x)) : (int)kKnown;
+          const int c = max(r[u], 0), xi = pkx(c) & 7, zi = pkz(c) & 3, i0 = si[u];
+          s[u] = r[u] >= 0 ? gld(Sb + i0) : (int)kKnown;
+#if AF_BRICK
+          pn[u][0] = (pm[u] & 1u) ? gld(Sb + i0 + (xi != 7 ? 1 : 25)) : 0;
+          pn[u][1] = (pm[u] & 2u) ? gld(Sb + i0 - (xi != 0 ? 1 : 25)) : 0;
+          pn[u][2] = (pm[u] & 4u) ? gld(Sb + i0 + (zi != 3 ? 8 : zstep)) : 0;
+          pn[u][3] = (pm[u] & 8u) ? gld(Sb + i0 - (zi != 0 ? 8 : zstep)) : 0;
+#else
+          const int z = pkz(c), x = pkx(c);
           pn[u][0] = (pm[u] & 1u) ? gld(Sb + SL.at(z, x + 1)) : 0;
           pn[u][1] = (pm[u] & 2u) ? gld(Sb + SL.at(z, x - 1)) : 0;
           pn[u][2] = (pm[u] & 4u) ? gld(Sb + SL.at(z + 1, x)) : 0;
           pn[u][3] = (pm[u] & 8u) ? gld(Sb + SL.at(z - 1, x)) : 0;
+#endif
         }
 #pragma unroll
         for (int u = 0; u < kCU; u++) {
@@ -1226,7 +1253,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
       unsigned long long base2 = 0;
       if (lane == 0 && (ci | cb))
         base2 = atomicAdd(&sh->nE2, (unsigned long long)ci | ((unsigned long long)cb << 32));
-      base2 = __shfl(base2, 0);
+      base2 = bcast64(base2, 0);
       int basei = (int)(unsigned)base2, baseb = (int)(unsigned)(base2 >> 32);
       const unsigned long long lt = (1ull << lane) - 1ull;
 #pragma unroll
@@ -1291,7 +1318,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
         const int fl = __ffsll((long long)fm) - 1;
         int fb = 0;
         if (lane == fl) fb = atomicAdd(&sh->nFb, __popcll(fm));
-        fb = __shfl(fb, fl) + __popcll(fm & ((1ull << lane) - 1ull));
+        fb = bcast(fb, fl) + __popcll(fm & ((1ull << lane) - 1ull));
         if (v == -1.0 && fb < kRcap) sh->Rx[fb] = e;
       }
     };

@@ -8,7 +8,12 @@
 #   kab:SIZES[:REP]   tools/kbench.py for every variants/*/libalifmm.so, REP rounds interleaved
 #   prof:PASSES       tools/profile.sh TAG "PASSES" (stats fetch write sq ...; ',' = space)
 #   shares            FETCH / WRITE passes at the 2 / 4 / 8-GPU shares (64 / 32 / 16 sources)
-#   py:SCRIPT[:ARGS]  python tools/SCRIPT ARGS                -> gpurun_out/TAG/SCRIPT.log
+#   py:SCRIPT[:ARGS]  python tools/SCRIPT ARGS (':' = space)  -> gpurun_out/TAG/SCRIPT.log
+#   vab:SCRIPT[:ARGS] the same for every variants/*/libalifmm.so (ALIFMM_LIB), last output line
+#                     of each prefixed with the variant name   -> gpurun_out/TAG/vab.log
+#   smoke             __graft_entry__.smoke()                  -> gpurun_out/TAG_smoke.log
+# Variant builds: tools/kvariants.sh "NAME -DFLAG=..." ...; profiles of another program:
+#   PROG="python3 tools/weld_split.py" tools/gpu.sh TAG prof:stats,sq
 # SIZES are comma-separated source counts, e.g. kab:16,128:2
 set -o pipefail
 TAG=$1; shift
@@ -43,7 +48,19 @@ for STEP in "$@"; do
       done ;;
     py)
       S=${ARG%%:*}; A=${ARG#*:}; [ "$A" = "$ARG" ] && A=""
-      timeout -k 10 600 python -u tools/$S ${A//,/ } > $O/${S%.py}.log 2>&1 ;;
+      timeout -k 10 600 python -u tools/$S ${A//:/ } > $O/${S%.py}.log 2>&1 ;;
+    vab)
+      S=${ARG%%:*}; A=${ARG#*:}; [ "$A" = "$ARG" ] && A=""
+      rc=0
+      for d in variants/*/; do
+        n=$(basename $d)
+        out=$(ALIFMM_LIB=$PWD/$d/libalifmm.so timeout -k 10 300 python -u tools/$S ${A//:/ } 2> $O/vab_$n.err) \
+          || { echo "variant $n failed"; tail -5 $O/vab_$n.err; rc=1; break; }
+        echo "$n $(echo "$out" | tail -1)" >> $O/vab.log
+      done
+      [ $rc -eq 0 ] ;;
+    smoke)
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 ;;
     *)
       echo "unknown step $STEP"; exit 2 ;;
   esac
