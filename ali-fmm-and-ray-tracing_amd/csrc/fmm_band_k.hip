@@ -1131,13 +1131,12 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
           r[u] = c;
           unsigned m = 0;
           int idx = 0;
-          if (c >= 0) {
-            const int z = pkz(c), x = pkx(c), xr = x & W1;
+          {
+            const int cc = max(c, 0), z = pkz(cc), x = pkx(cc), xr = x & W1;
             // a' = c - dir[d']: (z, x + 1), (z, x - 1), (z + 1, x), (z - 1, x); own iff not across
-            if (dd > 0 && x + 1 < nx && (one || xr != W1)) m |= 1u;
-            if (dd > 1 && x > 0 && (one || xr != 0)) m |= 2u;
-            if (dd > 2 && z + 1 < nz) m |= 4u;
-            if (dd > 3 && z > 0) m |= 8u;
+            m = (dd > 0 && x + 1 < nx && (one || xr != W1) ? 1u : 0u) | (dd > 1 && x > 0 && (one || xr != 0) ? 2u : 0u) |
+                (dd > 2 && z + 1 < nz ? 4u : 0u) | (dd > 3 && z > 0 ? 8u : 0u);
+            m = c >= 0 ? m : 0u;
             idx = SL.at(z, x);
           }
           pm[u] = m;
@@ -1149,13 +1148,14 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
 #pragma unroll
         for (int u = 0; u < kCU; u++) {
           const int c = max(r[u], 0), xi = pkx(c) & 7, zi = pkz(c) & 3, i0 = si[u];
-          s[u] = r[u] >= 0 ? gld(Sb + i0) : (int)kKnown;
 #if AF_BRICK
+          s[u] = r[u] >= 0 ? gld(Sb + i0) : (int)kKnown;
           pn[u][0] = (pm[u] & 1u) ? gld(Sb + i0 + (xi != 7 ? 1 : 25)) : 0;
           pn[u][1] = (pm[u] & 2u) ? gld(Sb + i0 - (xi != 0 ? 1 : 25)) : 0;
           pn[u][2] = (pm[u] & 4u) ? gld(Sb + i0 + (zi != 3 ? 8 : zstep)) : 0;
           pn[u][3] = (pm[u] & 8u) ? gld(Sb + i0 - (zi != 0 ? 8 : zstep)) : 0;
 #else
+          s[u] = r[u] >= 0 ? gld(Sb + i0) : (int)kKnown;
           const int z = pkz(c), x = pkx(c);
           pn[u][0] = (pm[u] & 1u) ? gld(Sb + SL.at(z, x + 1)) : 0;
           pn[u][1] = (pm[u] & 2u) ? gld(Sb + SL.at(z, x - 1)) : 0;

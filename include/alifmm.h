@@ -60,7 +60,7 @@ int alifmm_set_model(alifmm_ctx* ctx, int nnz, int nnx, const double* veln, cons
  * where the stage grids fit — subgrid <= 9; 0 = the HBM walk, fmm_exact.hip; bit-identical),
  * "coop" (band launch: 1 = cooperative, 0 = plain after a residency check), "cdelta_far" /
  * "r_far" (band width beyond Tmin = r_far * dnx / vmax, ramped in over r_far .. 2 r_far; default
- * 1.2 x the band width in force from 256 cells (0.6 at 0.5); a value set is never narrower than
+ * 1.4 x the band width in force from 768 cells (0.7 at 0.5); a value set is never narrower than
  * the band width in force; cdelta_far 0 = one width everywhere), "far_sg" (the largest subgrid the
  * far band applies to, default 1), "stream_out" (subgrid-1 travels
  * with a host destination stream the fields out of the band kernel, alifmm_travel_into; default 1). */

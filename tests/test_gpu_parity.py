@@ -574,12 +574,12 @@ def test_sharded_contexts_bit_identical_c4(A, monkeypatch):
 
 
 def test_far_band_vs_band_model(ctx, envelope):
-    """The default far band (band width 0.6 beyond Tmin = 256 dnx / vmax, ramped in up to 512;
-    subgrid 1) on a 401^2 anisotropic grain model whose front runs ~540 nodes from a corner
-    source: the field equals the CPU band model's (oracle/band_model.c with the same schedule) to
-    <= 1e-9 — the device applies the schedule the model states —, differs from the one-width band
-    (the far band did engage), and stays within the small-grid bar vs the heap oracle (6e-3 / 2e-4;
-    the CPU band model measures 7.8e-4 / 3.9e-5 here, the one-width band 7.2e-4 / 3.8e-5)."""
+    """The far band (default: band width 1.4 x cdelta = 0.7 beyond Tmin = 768 dnx / vmax, ramped in
+    up to 1536; subgrid 1), moved in to r_far = 256 so that it engages on a 401^2 anisotropic grain
+    model whose front runs ~540 nodes from a corner source: the field equals the CPU band model's
+    (oracle/band_model.c with the same schedule) to <= 1e-9 — the device applies the schedule the
+    model states —, differs from the one-width band (the far band did engage), and stays within the
+    small-grid bar vs the heap oracle (6e-3 / 2e-4)."""
     import _alifmm
 
     n, dnx = 401, 1e-3
@@ -589,24 +589,27 @@ def test_far_band_vs_band_model(ctx, envelope):
     sd = W.stif_field(n, n)
     vt = W.default_table()
     sx, sz = 20, 20
-    ctx.set_model(veln, velpn, vm, sd, vt, vt, dnx)
-    assert ctx.get_option("cdelta") == 0.5 and ctx.get_option("mat_jump") < 0.3  # grains: the default band
-    assert ctx.get_option("cdelta_far") == 0.6 and ctx.get_option("r_far") == 256
-    ctx.travel([dnx * sx], [dnx * sz], copy_out=False)
-    T = ctx.get_field(0, 1)
-    B, _ = O.band_travel(dnx * sx, dnx * sz, veln, velpn, vm, sd, vt, vt, ctx.get_option("vmax"),
-                         cdelta=ctx.get_option("cdelta"), exact_init=True, r0=ctx.get_option("r0"),
-                         exact_r=ctx.get_option("exact_r"), dnx=dnx, cdelta_far=0.6, r_far=256.0)
-    dm = float(np.max(np.abs(T - B) / np.maximum(B, 1e-300)))
-    envelope["far_band_vs_band_model_401"] = dm
-    assert dm <= 1e-9, dm
+    c1 = _alifmm.Context(0)
     c2 = _alifmm.Context(0)
     try:
+        c1.set_model(veln, velpn, vm, sd, vt, vt, dnx)
+        assert c1.get_option("cdelta") == 0.5 and c1.get_option("mat_jump") < 0.3  # grains: the default band
+        assert c1.get_option("cdelta_far") == 0.7 and c1.get_option("r_far") == 768
+        c1.set_option("r_far", 256)
+        c1.travel([dnx * sx], [dnx * sz], copy_out=False)
+        T = c1.get_field(0, 1)
+        B, _ = O.band_travel(dnx * sx, dnx * sz, veln, velpn, vm, sd, vt, vt, c1.get_option("vmax"),
+                             cdelta=c1.get_option("cdelta"), exact_init=True, r0=c1.get_option("r0"),
+                             exact_r=c1.get_option("exact_r"), dnx=dnx, cdelta_far=0.7, r_far=256.0)
+        dm = float(np.max(np.abs(T - B) / np.maximum(B, 1e-300)))
+        envelope["far_band_vs_band_model_401"] = dm
+        assert dm <= 1e-9, dm
         c2.set_option("cdelta_far", 0.0)
         c2.set_model(veln, velpn, vm, sd, vt, vt, dnx)
         c2.travel([dnx * sx], [dnx * sz], copy_out=False)
         assert not np.array_equal(c2.get_field(0, 1), T)
     finally:
+        c1.close()
         c2.close()
     R = O.travel(dnx * sx, dnx * sz, veln, velpn, vm, sd, vt, vt, dnx=dnx)
     _check_field(envelope, "far_band_401", T, R, (sx, sz), tol=(6e-3, 2e-4))
@@ -633,7 +636,7 @@ def test_many_materials_paths(ctx, envelope, n):
     sx, sz = 17, 23
     ctx.set_model(veln, velpn, vm, sd, vt, vt, dnx)
     assert ctx.get_option("mat_jump") > 0.95
-    assert ctx.get_option("cdelta") == 0.2 and abs(ctx.get_option("cdelta_far") - 0.24) < 1e-15
+    assert ctx.get_option("cdelta") == 0.2 and abs(ctx.get_option("cdelta_far") - 0.28) < 1e-15
     ctx.travel([dnx * sx], [dnx * sz], copy_out=False)
     T = ctx.get_field(0, 1)
     B, _ = O.band_travel(dnx * sx, dnx * sz, veln, velpn, vm, sd, vt, vt, ctx.get_option("vmax"),
@@ -653,9 +656,10 @@ def test_many_materials_paths(ctx, envelope, n):
 
 def test_explicit_cdelta_far_band(envelope):
     """A caller's band width carries the far band with it: cdelta 0.3 alone gives a far
-    band 1.2 x 0.3; an explicit cdelta_far narrower than the band width in force is raised to it;
-    cdelta_far 0 turns it off.  The 401^2 grain field at cdelta 0.3 (far band engaged) equals the
-    CPU band model's with the same widths (<= 1e-9) and stays within the small-grid bar."""
+    band 1.4 x 0.3; an explicit cdelta_far narrower than the band width in force is raised to it;
+    cdelta_far 0 turns it off.  The 401^2 grain field at cdelta 0.3 (far band engaged from r_far
+    256) equals the CPU band model's with the same widths (<= 1e-9) and stays within the small-grid
+    bar."""
     import _alifmm
 
     n, dnx = 401, 1e-3
@@ -668,13 +672,15 @@ def test_explicit_cdelta_far_band(envelope):
     c = _alifmm.Context(0)
     try:
         c.set_option("cdelta", 0.3)
+        c.set_option("r_far", 256)
         c.set_model(veln, velpn, vm, sd, vt, vt, dnx)
-        assert c.get_option("cdelta") == 0.3 and abs(c.get_option("cdelta_far") - 0.36) < 1e-15
+        cf = c.get_option("cdelta_far")
+        assert c.get_option("cdelta") == 0.3 and abs(cf - 0.42) < 1e-15
         c.travel([dnx * sx], [dnx * sz], copy_out=False)
         T = c.get_field(0, 1)
         B, _ = O.band_travel(dnx * sx, dnx * sz, veln, velpn, vm, sd, vt, vt, c.get_option("vmax"),
                              cdelta=0.3, exact_init=True, r0=c.get_option("r0"), exact_r=c.get_option("exact_r"),
-                             dnx=dnx, cdelta_far=0.36, r_far=256.0)
+                             dnx=dnx, cdelta_far=cf, r_far=256.0)
         dm = float(np.max(np.abs(T - B) / np.maximum(B, 1e-300)))
         envelope["explicit_cdelta03_vs_band_model_401"] = dm
         assert dm <= 1e-9, dm

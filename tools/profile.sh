@@ -15,7 +15,7 @@ cd /tmp
 if [ -n "$PROG" ]; then
   B=$(echo "$PROG" | sed "s|tools/|$ROOT/tools/|")
 else
-  B="python3 $ROOT/bench.py --no-cpu --no-return --no-e2e --no-c3"
+  B="python3 $ROOT/bench.py --no-cpu --no-return --no-e2e --no-c3 --no-c5"
 fi
 for PASS in $PASSES; do
   case $PASS in
