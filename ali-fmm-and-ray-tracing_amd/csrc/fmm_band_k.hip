@@ -225,7 +225,8 @@ struct Lds {
   int hsoff;     // streaming given up (ring_space timed out): no more staging or publishing
   double tmin_g, thr;
   unsigned long long nE2;  // claimed-list lengths: interior (low half), boundary (high half)
-  int nA, nF, hi, taken, nD, nR, nRx, live_g, err_g, err, nFb;
+  int nA, nF, hi, nD, nRx, live_g, err_g, err, nFb;
+  int takenb[2], nRb[2];  // [step parity]: fresh close-set slots taken by the commit; rim-list length
   int nrim[2];  // rim-list lengths of the neighbour members (left, right) this step
 };
 
@@ -675,7 +676,8 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
     sh->hi = 0;
     sh->nF = 0;
     sh->nD = 0;
-    sh->nR = 0;
+    sh->nRb[0] = sh->nRb[1] = 0;
+    sh->takenb[0] = sh->takenb[1] = 0;
     sh->err = 0;
     sh->nrim[0] = sh->nrim[1] = 0;
     // a list may be staged and not yet published when the next asks for slots: fewer slots than
@@ -766,6 +768,9 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
     }
   }
   __syncthreads();
+  // the close set's high-water mark, carried in a (uniform) register from step to step: the step's
+  // end needs no barrier for it (every thread computes the next value from the commit's count)
+  int hi_r = __builtin_amdgcn_readfirstlane(sh->hi);
   RunCfg R;
   R.nz = nz;
   R.nx = nx;
@@ -804,7 +809,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
     double* const Epar = E0 + par * ecells;
     const double* const Eprv = E0 + prv * ecells;
     const int eprv = tbc + prv * ecells;  // Eprv as an index from Tb
-    const int hi = sh->hi;
+    const int hi = hi_r;
     // ---- P0h: ring space for the tiles completed last step (staged after the X1 drain) ----
     if (hstream && tid == 0) {
       sh->spos += sh->nst;
@@ -824,7 +829,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
         tmin = fmin(tmin, t);
         const int c = (K > 1 && t < INFINITY) ? ((lo ? L.lds(e) : L.get(e)) & kCell) : 0;
         const bool pub = K > 1 && t < INFINITY && g.rim(pkx(c));
-        const int s = wave_push(&sh->nR, pub, P.capR, &sh->err);
+        const int s = wave_push(&sh->nRb[par], pub, P.capR, &sh->err);
         if (s >= 0) {
           gst_sc1(rimc + ((long)me * 2 + par) * P.capR + s, c);
           gst_sc1(rimt + ((long)me * 2 + par) * P.capR + s, t);
@@ -842,7 +847,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
       sh->nA = 0;
       sh->nE2 = 0;
       sh->nFb = 0;
-      sh->taken = 0;
+      sh->takenb[par] = 0;
       sh->nRx = 0;
     }
     __syncthreads();
@@ -871,7 +876,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
         gst_sc1(&X->x1[me][par][0], gtag | (tb & 0xffffffffull));
         gst_sc1(&X->x1[me][par][1], gtag | (tb >> 32));
         gst_sc1(&X->x1[me][par][2], gtag | (unsigned)(hi - sh->nF));
-        gst_sc1(&X->x1[me][par][3], gtag | ((unsigned)min(sh->err, 255) << 24) | (unsigned)min(sh->nR, 0xffffff));
+        gst_sc1(&X->x1[me][par][3], gtag | ((unsigned)min(sh->err, 255) << 24) | (unsigned)min(sh->nRb[par], 0xffffff));
       }
       if (wv == 0 && !x1_poll(X, K, par, (unsigned)(steps + 1), sh, mprev, mnext)) {
         if (lane == 0) sh->err = 7;
@@ -1429,8 +1434,12 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
         __syncthreads();
       }
     }
-    if (K > 1 && AF_DRAIN_LATE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    // (no barrier here: the one before the fallback rounds, or the last round's, already separates
+    // every evaluation and fallback write from the commit)
+    if (K > 1 && AF_DRAIN_LATE) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
     AF_TICK(4)
     // ---- P5: commit own cells; edge cells also into this step's edge buffer (slot marked DIRTY:
     // the next step's accept scan copies them forward) ----
@@ -1461,7 +1470,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
             fresh = true;
           }
         }
-        const int k = wave_push(&sh->taken, fresh, 1 << 30, &sh->err);
+        const int k = wave_push(&sh->takenb[par], fresh, 1 << 30, &sh->err);
         if (k >= 0) {
           const int slot = k < nF ? (LO ? FS.lds(nF - 1 - k) : FS.get(nF - 1 - k)) : hi + (k - nF);
           if (slot >= capL) {
@@ -1482,11 +1491,15 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
     if (nE <= kEcap && hi + nE <= kLcap) commit(std::true_type{});
     else commit(std::false_type{});
     __syncthreads();
+    // No barrier at the step's end: the next step's first reads of what this end writes are behind
+    // its P1 barrier (nF: X1 by thread 0 itself, the accept after it), the step's hi is in a
+    // register, and the per-step counters are double-buffered by step parity (a slow wave may still
+    // read takenb[par] here while a fast one resets takenb[par ^ 1] in the next P1)
+    const int tk_ = sh->takenb[par];
+    hi_r = __builtin_amdgcn_readfirstlane(hi + max(0, tk_ - nF));
     if (tid == 0) {
-      const int tk_ = sh->taken;
       sh->nF = max(0, nF - tk_);
-      sh->hi = hi + max(0, tk_ - nF);
-      sh->nR = 0;  // the next step's rim list
+      sh->nRb[par] = 0;  // the rim list of step + 2
     }
     if (prof) {
       ls[0] += hi - sh->nF;
@@ -1499,7 +1512,6 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
 #endif
     }
     steps++;
-    __syncthreads();
     AF_TICK(5)
   }
 #undef AF_TICK
