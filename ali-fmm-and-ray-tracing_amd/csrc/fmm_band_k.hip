@@ -226,6 +226,7 @@ struct Lds {
   double tmin_g, thr;
   unsigned long long nE2;  // claimed-list lengths: interior (low half), boundary (high half)
   int nA, nF, hi, nD, nRx, live_g, err_g, err, nFb;
+  int xl;  // AF_XCD_LOCAL: every member of the source on this member's XCD (set by the exchange)
   int takenb[2], nRb[2];  // [step parity]: fresh close-set slots taken by the commit; rim-list length
   int nrim[2];  // rim-list lengths of the neighbour members (left, right) this step
 };
@@ -540,6 +541,26 @@ AF_DEV void publish_tiles(Lds* sh, const TileStream& ts, int b, int lane) {
 // word per lane) until every member's words carry this step's tag, then the wave reduces them:
 // global Tmin, live close cells (sum), error (or), and the neighbour members' rim-list lengths.
 // false on timeout (a member is not resident)
+// XCD-local cross-member data (AF_XCD_LOCAL): once every member of a source has reported the same
+// XCD (HW_REG_XCC_ID, carried in its exchange word 2), the members' edge buffers, rim lists
+// and exchange words are stored plainly instead of write-through (sc1): the stores complete in the
+// XCD's L2, which the readers' sc1 (L1-bypassing) loads are served from, instead of travelling to
+// memory and dropping the line from L2.  Placement is read, not assumed: members on different XCDs
+// keep the sc1 stores (MI355X_MICROARCH.md "inter-workgroup visibility").
+#ifndef AF_XCD_LOCAL
+#define AF_XCD_LOCAL 1
+#endif
+AF_DEV int xcc_id() {
+  int v;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(v));
+  return v;
+}
+template <class T>
+AF_DEV void xst(T* p, T v, bool loc) {
+  if (AF_XCD_LOCAL && loc) gst(p, v);
+  else gst_sc1(p, v);
+}
+
 AF_DEV bool x1_poll(KX* X, int K, int par, unsigned tag, Lds* sh, int mprev, int mnext) {
   const int lane = threadIdx.x & 63;
   const int nw = 4 * K;
@@ -564,11 +585,14 @@ AF_DEV bool x1_poll(KX* X, int K, int par, unsigned tag, Lds* sh, int mprev, int
   if ((lane & 3) == 0 && lane < nw) {
     const int q = lane >> 2;
     tmin = __longlong_as_double((long long)(((unsigned long long)w1 << 32) | w));
-    live = (int)w2;
+    live = (int)(w2 & 0x0fffffffu);
     err = (int)(w3 >> 24);
     if (q == mprev) sh->nrim[0] = (int)(w3 & 0xffffffu);
     if (K > 2 && q == mnext) sh->nrim[1] = (int)(w3 & 0xffffffu);
   }
+  // every member's XCD (bits 28..31 of its word 2) equal to this one's
+  const bool other_xcd = (lane & 3) == 0 && lane < nw && (int)(w2 >> 28) != xcc_id();
+  const bool same = __ballot(other_xcd) == 0;
   tmin = wave_min_full(tmin);
   live = wave_sum_full(live);
   err = wave_or_full(err);
@@ -576,6 +600,7 @@ AF_DEV bool x1_poll(KX* X, int K, int par, unsigned tag, Lds* sh, int mprev, int
     sh->tmin_g = tmin;
     sh->live_g = live;
     sh->err_g = err;
+    sh->xl = same ? 1 : 0;
   }
   return true;
 }
@@ -678,6 +703,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
     sh->nD = 0;
     sh->nRb[0] = sh->nRb[1] = 0;
     sh->takenb[0] = sh->takenb[1] = 0;
+    sh->xl = 0;
     sh->err = 0;
     sh->nrim[0] = sh->nrim[1] = 0;
     // a list may be staged and not yet published when the next asks for slots: fewer slots than
@@ -831,8 +857,8 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
         const bool pub = K > 1 && t < INFINITY && g.rim(pkx(c));
         const int s = wave_push(&sh->nRb[par], pub, P.capR, &sh->err);
         if (s >= 0) {
-          gst_sc1(rimc + ((long)me * 2 + par) * P.capR + s, c);
-          gst_sc1(rimt + ((long)me * 2 + par) * P.capR + s, t);
+          xst(rimc + ((long)me * 2 + par) * P.capR + s, c, (bool)sh->xl);
+          xst(rimt + ((long)me * 2 + par) * P.capR + s, t, (bool)sh->xl);
         }
       }
     }
@@ -873,10 +899,12 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
         // X1: flagged words (step + 1 in the high half), one store each; the payload arrives with the flag
         const unsigned long long gtag = (unsigned long long)(unsigned)(steps + 1) << 32;
         const unsigned long long tb = (unsigned long long)__double_as_longlong(tmin);
-        gst_sc1(&X->x1[me][par][0], gtag | (tb & 0xffffffffull));
-        gst_sc1(&X->x1[me][par][1], gtag | (tb >> 32));
-        gst_sc1(&X->x1[me][par][2], gtag | (unsigned)(hi - sh->nF));
-        gst_sc1(&X->x1[me][par][3], gtag | ((unsigned)min(sh->err, 255) << 24) | (unsigned)min(sh->nRb[par], 0xffffff));
+        const bool loc = sh->xl;
+        xst(&X->x1[me][par][0], gtag | (tb & 0xffffffffull), loc);
+        xst(&X->x1[me][par][1], gtag | (tb >> 32), loc);
+        // word 2: this member's XCD (bits 28..31) and live close cells (a front, far below 2^28)
+        xst(&X->x1[me][par][2], gtag | ((unsigned)xcc_id() << 28) | ((unsigned)(hi - sh->nF) & 0x0fffffffu), loc);
+        xst(&X->x1[me][par][3], gtag | ((unsigned)min(sh->err, 255) << 24) | (unsigned)min(sh->nRb[par], 0xffffff), loc);
       }
       if (wv == 0 && !x1_poll(X, K, par, (unsigned)(steps + 1), sh, mprev, mnext)) {
         if (lane == 0) sh->err = 7;
@@ -897,7 +925,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
     if (K > 1) {
       const int nD = min(sh->nD, capC);
       for (int d = tid; d < nD; d += kThreads) {
-        gst_sc1(Epar + g.eidx(pkz(DC.get(d)), pkx(DC.get(d))), -DV.get(d));
+        xst(Epar + g.eidx(pkz(DC.get(d)), pkx(DC.get(d))), -DV.get(d), (bool)sh->xl);
       }
       __syncthreads();  // the list is refilled by this step's acceptance
     }
@@ -950,7 +978,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
           if (K > 1 && live) {
             const bool ed = g.edge(pkx(c[u]));
             if (raw < 0 || (acc[u] && ed)) {  // dirty (committed last step) or accepted edge cell
-              gst_sc1(Epar + g.eidx(pkz(c[u]), pkx(c[u])), acc[u] ? -t[u] : t[u]);
+              xst(Epar + g.eidx(pkz(c[u]), pkx(c[u])), acc[u] ? -t[u] : t[u], (bool)sh->xl);
               if (raw < 0 && !acc[u]) {
                 if (LO) L.put_lds(e, c[u]);
                 else L.put(e, c[u]);
@@ -1457,7 +1485,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
           const int p = LO ? EP.lds(e) : EP.get(e);
           gst(Tb + TL.at(pkz(r), pkx(r)), v);
           ed = g.edge(pkx(r));
-          if (ed) gst_sc1(Epar + g.eidx(pkz(r), pkx(r)), v);
+          if (ed) xst(Epar + g.eidx(pkz(r), pkx(r)), v, (bool)sh->xl);
           if (p >= 0) {
             if (LO) {
               Lt.put_lds(p, v);
