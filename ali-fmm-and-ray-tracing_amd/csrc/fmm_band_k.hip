@@ -36,7 +36,9 @@
 //
 // Cross-CU data (flags, rim lists, edge buffers) is stored with sc1 stores, drained (vmcnt 0) by
 // every wave before the flag, and read with sc1 loads after the flag (MI355X_MICROARCH.md
-// "inter-workgroup visibility", Valid forms).  Flags and rim lists are double-buffered by parity.
+// "inter-workgroup visibility", Valid forms); once every member has reported the same XCD
+// (HW_REG_XCC_ID in its exchange word) the stores are plain and complete in that XCD's L2, where
+// the sc1 loads are served (AF_XCD_LOCAL).  Flags and rim lists are double-buffered by parity.
 #define CR_LDS_TABLES  // cr_math.h tables in LDS (crm::lds_init at kernel start)
 #include <algorithm>
 #include <type_traits>
