@@ -45,7 +45,7 @@ static void release_kept_rays(alifmm_ctx* c) {
   c->kept_pts = 0;
 }
 static void free_arena(Arena& a) {
-  dfree(a.S); dfree(a.own); dfree(a.lists); dfree(a.dlists); dfree(a.Ts); dfree(a.Ss); dfree(a.srcs); dfree(a.ho); dfree(a.jobs);
+  dfree(a.S); dfree(a.lists); dfree(a.dlists); dfree(a.Ts); dfree(a.Ss); dfree(a.srcs); dfree(a.ho); dfree(a.jobs);
   dfree(a.rimc); dfree(a.rimt); dfree(a.kx); dfree(a.Tb); dfree(a.Sb);
   dfree(a.dscx); dfree(a.dscz);
   a = Arena();
@@ -571,7 +571,6 @@ static int ensure_arena(alifmm_ctx* ctx, int nsrc, long cells, long scells, long
   HIPCHK(dalloc(&a.Tb, (size_t)nsrc * tbc));
   HIPCHK(dalloc(&a.Sb, (size_t)nsrc * sbc));
   if (scells > 0) HIPCHK(dalloc(&a.S, (size_t)nsrc * scells));
-  HIPCHK(dalloc(&a.own, (size_t)nsrc * cells));
   HIPCHK(dalloc(&a.lists, (size_t)nsrc * (4 * capL + 6 * capC)));
   HIPCHK(dalloc(&a.dlists, (size_t)nsrc * (capL + 2 * capC)));
   if (K > 1) {
@@ -708,7 +707,6 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
     memset(&b, 0, sizeof b);
     b.T = ctx->fields[slot].d;
     b.S = sg > 1 ? a.S + (size_t)i * a.scells : nullptr;
-    b.own = a.own + (size_t)i * a.cells;
     int* base = a.lists + (size_t)i * (4 * a.capL + 6 * a.capC);
     b.Lin = base;
     b.FS = base + a.capL;
@@ -744,7 +742,6 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
     // start far (NaN, fields.h); subgrid 1: the band kernel's copy-out writes every cell
     if (sg > 1) HIPCHK(hipMemsetAsync(b.T, 0xFF, (size_t)cells * 8, fs));
     if (sg > 1) HIPCHK(hipMemsetAsync(b.S, 0xFF, (size_t)cells * 4, fs));  // the exact kernel's status: kFar
-    HIPCHK(hipMemsetAsync(b.own, 0xFF, (size_t)cells * 4, fs));  // claim stamps -1
   }
   if (fs != ctx->stream) HIPCHK(hipEventRecord(ctx->ev_fill, fs));
   HIPCHK(hipMemcpyAsync(a.srcs, hs.data(), sizeof(af::BandSrc) * n, hipMemcpyHostToDevice, ctx->stream));

@@ -28,7 +28,6 @@ struct Arena {  // per-chunk scratch, reused across calls
   int nsrc = 0;
   long cells = 0, scells = 0, capL = 0, capC = 0, capS = 0;
   int* S = nullptr;  // row-major status, scells per source (subgrid > 1 only)
-  int* own = nullptr;
   int* lists = nullptr;    // Lin | FS | A | L | C | Cp | D | Rx | Bl | Bp per source
   double* dlists = nullptr;  // Lt | V | Dv per source
   int K = 0;                 // K-member kernel: members the rim lists are sized for

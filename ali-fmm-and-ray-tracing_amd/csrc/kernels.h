@@ -23,7 +23,6 @@ struct BandSrc {
   int* S;         // status, row-major: fmm_exact_kernel's (mode 1), read by the band's hand-over
   int* Sb;        // the band kernel's status (layout fmm_band_k.hip SbLayout): far -1, known 0,
                   // close 1 + close-set slot
-  int* own;       // claim stamps (steps with more claim items than the LDS hash holds)
   int* Lin;       // mode 1: close cells handed over by fmm_exact_kernel (nl0 of them)
   int* L;         // close set: cells
   double* Lt;     // close set: T
