@@ -104,7 +104,7 @@ constexpr int kWaves = kThreads / 64;
 #define AF_ACAP AF_ACAP_D
 #endif
 constexpr int kLcap = AF_LCAP, kAcap = AF_ACAP, kEcap = AF_ECAP;
-constexpr int kBcap = 512 / AF_WG_PER_CU, kDcap = 512 / AF_WG_PER_CU, kRcap = 1024 / AF_WG_PER_CU;
+constexpr int kBcap = 512 / AF_WG_PER_CU, kDcap = 256 / AF_WG_PER_CU, kRcap = 1024 / AF_WG_PER_CU;
 #ifndef AF_X1_SLEEP
 #define AF_X1_SLEEP 1
 #endif
@@ -191,8 +191,8 @@ struct Lds {
   int Ep[kEcap];  // slot of a claimed close cell, -1 for a far cell
   int Bl[kBcap];  // claimed cells whose stencil reaches another member's columns
   int Bp[kBcap];
-  int Dc[kDcap];  // edge cells accepted this step (copied forward next step) ...
-  double Dv[kDcap];  // ... and their T
+  int Dc[2][kDcap];  // [step parity]: edge cells accepted in a step (copied forward by the next) ...
+  double Dv[2][kDcap];  // ... and their T
   int Rx[kRcap];  // claim items from the neighbour members' accepted rim cells; fallback list
   alignas(16) int H[kHashArr];  // fallback staging windows
 #if AF_SORT_ACC
@@ -209,9 +209,10 @@ struct Lds {
   int spos, nst; // tiles staged before this step; tiles staged this step
   int cons;      // tiles the host has taken out of the ring (last read)
   int hsoff;     // streaming given up (ring_space timed out): no more staging or publishing
-  double tmin_g, thr;
+  double tmin_g;
   unsigned long long nE2;  // claimed-list lengths: interior (low half), boundary (high half)
-  int nA, nF, hi, nD, nRx, live_g, err_g, err, nFb;
+  int nA, nF, hi, nRx, live_g, err_g, err, nFb;
+  int nDb[2];  // [step parity]: lengths of Dc / Dv
   int xl;  // AF_XCD_LOCAL: every member of the source on this member's XCD (set by the exchange)
   int takenb[2], nRb[2];  // [step parity]: fresh close-set slots taken by the commit; rim-list length
   int nrim[2];  // rim-list lengths of the neighbour members (left, right) this step
@@ -646,8 +647,9 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
   const HList<double, kEcap> VL{sh->Vl, B->V + me * hC};
   const HList<int, kBcap> BL{sh->Bl, B->Bl + me * hC};
   const HList<int, kBcap> BP{sh->Bp, B->Bp + me * hC};
-  const HList<int, kDcap> DC{sh->Dc, B->D + me * hC};
-  const HList<double, kDcap> DV{sh->Dv, B->Dv + me * hC};
+  // the accepted-edge-cell lists of the two step parities (global spill: half of the slice each)
+  const long hD = hC / 2;
+  const int capD = (int)hD;
   const HList<int, kRcap> RX{sh->Rx, B->Rx + me * hC};
   const int capL = (int)hL, capC = (int)hC;
   // rim lists [member][parity][capR]; edge buffers [parity][cells] (selected by arithmetic on the
@@ -683,7 +685,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
     sh->qpos = sh->spos = sh->nst = sh->cons = sh->hsoff = 0;
     sh->hi = 0;
     sh->nF = 0;
-    sh->nD = 0;
+    sh->nDb[0] = sh->nDb[1] = 0;
     sh->nRb[0] = sh->nRb[1] = 0;
     sh->takenb[0] = sh->takenb[1] = 0;
     sh->xl = 0;
@@ -856,17 +858,19 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
       sh->nFb = 0;
       sh->takenb[par] = 0;
       sh->nRx = 0;
+      sh->nDb[par] = 0;  // (the last step's P0 read nDb[prv])
     }
-    __syncthreads();
-    tmin = sh->red[0];
-    for (int w = 1; w < kWaves; w++) tmin = fmin(tmin, sh->red[w]);
-    const double delta = launder_u(R.delta), t0 = launder_u(R.t0);
+    // every wave's cross-member stores (this scan's rim list, the last step's edge-buffer and
+    // tile-ring stores) complete before the one barrier, after which thread 0 raises the flags
     const long long tdr = prof ? wall_clock64() : 0;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores have completed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 #if !AF_PROF_FBWAIT && !AF_PROF_SPILL && !AF_PROF_CLAIM
     AF_SUBT(3, tdr)
 #endif
+    tmin = sh->red[0];
+    for (int w = 1; w < kWaves; w++) tmin = fmin(tmin, sh->red[w]);
+    const double delta = launder_u(R.delta), t0 = launder_u(R.t0);
     if (hstream && !sh->hsoff) {
       // publish the tiles staged last step (their stores have drained: the wait above), then stage
       // the ones completed last step (slots reserved in P0h)
@@ -902,13 +906,18 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
     AF_TICK(0)
     if (sh->live_g <= 0 || sh->err_g || sh->err) break;
     // ---- P0: last step's accepted edge cells into this step's edge buffer.  Only now: every member
-    // has passed this step's X1, i.e. finished the previous step, which read this buffer ----
+    // has passed this step's X1, i.e. finished the previous step, which read this buffer.  The
+    // list is the last step's parity (this step's acceptance fills the other one: no barrier) ----
+    const HList<int, kDcap> DC{sh->Dc[par], B->D + me * hC + par * hD};
+    const HList<double, kDcap> DV{sh->Dv[par], B->Dv + me * hC + par * hD};
     if (K > 1) {
-      const int nD = min(sh->nD, capC);
+      const HList<int, kDcap> DCp{sh->Dc[prv], B->D + me * hC + prv * hD};
+      const HList<double, kDcap> DVp{sh->Dv[prv], B->Dv + me * hC + prv * hD};
+      const int nD = min(sh->nDb[prv], capD);
       for (int d = tid; d < nD; d += kThreads) {
-        xst(Epar + g.eidx(pkz(DC.get(d)), pkx(DC.get(d))), -DV.get(d), (bool)sh->xl);
+        const int c = DCp.get(d);
+        xst(Epar + g.eidx(pkz(c), pkx(c)), -DVp.get(d), (bool)sh->xl);
       }
-      __syncthreads();  // the list is refilled by this step's acceptance
     }
     tmin = sh->tmin_g;
     double dl = delta;
@@ -920,12 +929,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
       const double tfar = launder_u(R.tfar);
       if (tfar > 0 && tmin > tfar) dl = delta + (launder_u(R.delta_far) - delta) * fmin(1.0, (tmin - tfar) / tfar);
     }
-    const double thr = tmin + dl;
-    if (tid == 0) {
-      sh->thr = thr;
-      sh->nD = 0;
-    }
-    __syncthreads();
+    const double thr = tmin + dl;  // (every thread: no barrier for it)
     // the neighbour members' rim lists: loads issued now, consumed after the accept scan (P3a)
     int rpc = -1;
     double rpt = INFINITY;
@@ -965,7 +969,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
                 else L.put(e, c[u]);
               }
             }
-            const int d = wave_push(&sh->nD, acc[u] && ed, capC, &sh->err);
+            const int d = wave_push(&sh->nDb[par], acc[u] && ed, capD, &sh->err);
             if (d >= 0) {
               DC.put(d, c[u]);
               DV.put(d, t[u]);
@@ -1256,7 +1260,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
 #endif
     {
       const int nFb = sh->nFb;
-      const double thr_f = sh->thr;
+      const double thr_f = thr;
       double* const win = reinterpret_cast<double*>(sh->H);  // kFbRound x 25 doubles
       unsigned* const wmask = reinterpret_cast<unsigned*>(sh->Al);
       const int nlist = min(nFb, kRcap);
