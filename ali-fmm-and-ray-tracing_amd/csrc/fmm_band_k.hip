@@ -128,6 +128,11 @@ constexpr int kCU = AF_CLAIM_OWN_U;
 #ifndef AF_PROF_FBWAIT
 #define AF_PROF_FBWAIT 0
 #endif
+// diagnostic: sub[2] / sub[3] = evaluation time (from the phase start) of the slowest wave with
+// interior cells only / with a boundary cell (sub[1]: boundary cells, sub[0]: XCD-local steps, x 100)
+#ifndef AF_PROF_EVW
+#define AF_PROF_EVW 0
+#endif
 // fallback fouds18_A(): four lanes per cell (1) or one (0)
 #ifndef AF_F18_SPLIT
 #define AF_F18_SPLIT 1
@@ -142,8 +147,15 @@ constexpr int kCU = AF_CLAIM_OWN_U;
 #ifndef AF_SORT_ACC
 #define AF_SORT_ACC 256
 #endif
+// ... and only with at most AF_SORT_KMAX members per source (narrow stripes gain nothing from it)
+#ifndef AF_SORT_KMAX
+#define AF_SORT_KMAX 8
+#endif
 #ifndef AF_SORTB
 #define AF_SORTB AF_SORTB_D
+#endif
+#ifndef AF_NB_MIX
+#define AF_NB_MIX 2
 #endif
 constexpr int kSortB = AF_SORTB;
 AF_DEV int tile_bucket(int c) { return ((pkz(c) >> 3) & (kSortB / 32 - 1)) << 5 | ((pkx(c) >> 3) & 31); }
@@ -216,6 +228,10 @@ struct Lds {
   int xl;  // AF_XCD_LOCAL: every member of the source on this member's XCD (set by the exchange)
   int takenb[2], nRb[2];  // [step parity]: fresh close-set slots taken by the commit; rim-list length
   int nrim[2];  // rim-list lengths of the neighbour members (left, right) this step
+#if AF_PROF_EVW
+  long long evt[kWaves];  // diagnostic: each wave's evaluation end
+  int evb[kWaves];        // ... and whether it had cells (1) with a boundary one (2)
+#endif
 };
 
 
@@ -348,7 +364,14 @@ AF_DEV void load_nb(NbFieldT& nb, const double* T, const TbLayout& L, int eprv, 
   }
   if (off32) {
 #pragma unroll
-    for (int k = 0; k < 12; k++) t[k] = fabs(gld_sc1((const double*)((const char*)T + ((unsigned)idx[k] << 3))));
+    for (int k = 0; k < 12; k++) {
+      const double* a = (const double*)((const char*)T + ((unsigned)idx[k] << 3));
+      // AF_NB_MIX: own-column points (this member's field: plain loads see its own stores) 1: the
+      // cell's own column plain, 2: every own point plain
+      if (AF_NB_MIX >= 1 && dx[k] == 0) t[k] = fabs(gld(a));
+      else if (AF_NB_MIX == 2) t[k] = fabs(ot[dx[k] + 2] ? gld_sc1(a) : gld(a));
+      else t[k] = fabs(gld_sc1(a));
+    }
   } else {
 #pragma unroll
     for (int k = 0; k < 12; k++) t[k] = fabs(gld_sc1(T + idx[k]));
@@ -695,6 +718,9 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
     // two lists could wait for the host forever (tile_stream.h kRingSlots)
     if (hstream && P.rslots < 2 * kTdCap) sh->err = 11;
   }
+#if AF_SORT_ACC
+  for (int k = tid; k < kSortB; k += kThreads) sh->Sb[k] = 0;  // (re-zeroed after each sort)
+#endif
   __syncthreads();
   // ---------------- hand-over: own cells only ----------------
   if (MODE == 0) {
@@ -847,9 +873,6 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
         }
       }
     }
-#if AF_SORT_ACC
-    for (int k = tid; k < kSortB; k += kThreads) sh->Sb[k] = 0;
-#endif
     tmin = wave_min_full(tmin);
     if (lane == 0) sh->red[wv] = tmin;
     if (tid == 0) {
@@ -902,7 +925,9 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
     if (tid == 0 && steps >= P.max_steps) sh->err = 8;  // a band that never finishes (cannot happen
                                                        // with valid inputs): stop instead of hanging
     __syncthreads();
+#if !AF_PROF_EVW
     AF_SUBT(0, tx1)
+#endif
     AF_TICK(0)
     if (sh->live_g <= 0 || sh->err_g || sh->err) break;
     // ---- P0: last step's accepted edge cells into this step's edge buffer.  Only now: every member
@@ -1043,13 +1068,15 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
       }
     }
     __syncthreads();
+#if !AF_PROF_EVW
     AF_SUBT(1, trr)
+#endif
     AF_TICK(1)
     const int nA = min(sh->nA, capL), nRx = min(sh->nRx, capC);
     int* alist = sh->Al;
     const long long tso = prof ? wall_clock64() : 0;
 #if AF_SORT_ACC
-    if (nA > AF_SORT_ACC && nA <= kAcap) {  // (uniform) counting sort of the accepted list by tile
+    if (nA > AF_SORT_ACC && nA <= kAcap && K <= AF_SORT_KMAX) {  // (uniform) counting sort of the accepted list by tile
       for (int a = tid; a < nA; a += kThreads) atomicAdd(&sh->Sb[tile_bucket(sh->Al[a])], 1);
       __syncthreads();
       static_assert(kSortB % 64 == 0 && kSortB / 64 <= kWaves, "one bucket per thread of the first waves");
@@ -1068,6 +1095,8 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
         sh->As[atomicAdd(&sh->Sb[tile_bucket(c)], 1)] = c;
       }
       __syncthreads();
+      // the buckets zeroed for the next sort (many barriers away)
+      for (int k = tid; k < kSortB; k += kThreads) sh->Sb[k] = 0;
       alist = sh->As;
     }
 #endif
@@ -1209,6 +1238,9 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
       __syncthreads();
     }
     AF_TICK(2)
+#if AF_PROF_EVW
+    const long long tev0 = PROF ? wall_clock64() : 0;
+#endif
     const int nE = nEi + nEb;
     // ---- P4: evaluate ----
     const bool lds_e = nE <= kEcap;
@@ -1252,9 +1284,28 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
 #endif
     }
     AF_TICK(3)
+#if AF_PROF_EVW
+    if (PROF && me == 0 && lane == 0) {
+      sh->evt[wv] = wall_clock64();
+      sh->evb[wv] = wv * 64 >= nE ? 0 : (wv * 64 + 63 >= nEi ? 2 : 1);
+    }
+#endif
     // ---- P4b: fouds18_A() over the compacted fallback list, in staged rounds ----
     const long long tfw = prof ? wall_clock64() : 0;
     __syncthreads();
+#if AF_PROF_EVW
+    if (prof) {
+      long long ti = 0, tb = 0;
+      for (int w = 0; w < kWaves; w++) {
+        if (sh->evb[w] == 1) ti = max(ti, sh->evt[w] - tev0);
+        if (sh->evb[w] == 2) tb = max(tb, sh->evt[w] - tev0);
+      }
+      sub[2] += ti;
+      sub[3] += tb;
+      sub[1] += 100 * nEb;           // (kbench: mean boundary cells per step)
+      sub[0] += sh->xl ? 100 : 0;    // (kbench: fraction of steps with XCD-local exchange)
+    }
+#endif
 #if AF_PROF_FBWAIT  // diagnostic: sub[3] = the wait for the other waves' evaluation
     AF_SUBT(3, tfw)
 #endif
