@@ -129,9 +129,15 @@ constexpr int kCU = AF_CLAIM_OWN_U;
 #define AF_PROF_FBWAIT 0
 #endif
 // diagnostic: sub[2] / sub[3] = evaluation time (from the phase start) of the slowest wave with
-// interior cells only / with a boundary cell (sub[1]: boundary cells, sub[0]: XCD-local steps, x 100)
+// interior cells only / with a boundary cell, summed over the steps with both (sub[1]: their count,
+// sub[0]: XCD-local steps, x 100)
 #ifndef AF_PROF_EVW
 #define AF_PROF_EVW 0
+#endif
+// diagnostic: sub[2] / sub[3] = (1) the close-set scan / the scan + the drain before the X1
+// barrier, from the step's start; (2) P0 / P0 + the accept scan, from the X1 barrier
+#ifndef AF_PROF_SEG
+#define AF_PROF_SEG 0
 #endif
 // fallback fouds18_A(): four lanes per cell (1) or one (0)
 #ifndef AF_F18_SPLIT
@@ -873,6 +879,9 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
         }
       }
     }
+#if AF_PROF_SEG == 1
+    if (prof) sub[2] += wall_clock64() - tk;
+#endif
     tmin = wave_min_full(tmin);
     if (lane == 0) sh->red[wv] = tmin;
     if (tid == 0) {
@@ -888,8 +897,11 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
     const long long tdr = prof ? wall_clock64() : 0;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-#if !AF_PROF_FBWAIT && !AF_PROF_SPILL && !AF_PROF_CLAIM
+#if !AF_PROF_FBWAIT && !AF_PROF_SPILL && !AF_PROF_CLAIM && !AF_PROF_SEG
     AF_SUBT(3, tdr)
+#endif
+#if AF_PROF_SEG == 1
+    if (prof) sub[3] += wall_clock64() - tk;
 #endif
     tmin = sh->red[0];
     for (int w = 1; w < kWaves; w++) tmin = fmin(tmin, sh->red[w]);
@@ -944,6 +956,9 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
         xst(Epar + g.eidx(pkz(c), pkx(c)), -DVp.get(d), (bool)sh->xl);
       }
     }
+#if AF_PROF_SEG == 2
+    if (prof) sub[2] += wall_clock64() - tk;
+#endif
     tmin = sh->tmin_g;
     double dl = delta;
     if (t0 > 0 && tmin < t0) dl = delta * (tmin / t0);
@@ -1040,6 +1055,9 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
     };
     if (hi <= kLcap) accept(std::true_type{});
     else accept(std::false_type{});
+#if AF_PROF_SEG == 2
+    if (prof) sub[3] += wall_clock64() - tk;
+#endif
     // ---- P3a: the neighbour members' accepted rim cells -> claim items (their cross neighbour) ----
     const long long trr = prof ? wall_clock64() : 0;
     if (K > 1) {
@@ -1300,9 +1318,11 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
         if (sh->evb[w] == 1) ti = max(ti, sh->evt[w] - tev0);
         if (sh->evb[w] == 2) tb = max(tb, sh->evt[w] - tev0);
       }
-      sub[2] += ti;
-      sub[3] += tb;
-      sub[1] += 100 * nEb;           // (kbench: mean boundary cells per step)
+      if (ti > 0 && tb > 0) {  // steps with both kinds of wave
+        sub[2] += ti;
+        sub[3] += tb;
+        sub[1] += 100;
+      }
       sub[0] += sh->xl ? 100 : 0;    // (kbench: fraction of steps with XCD-local exchange)
     }
 #endif

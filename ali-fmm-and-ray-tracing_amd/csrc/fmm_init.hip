@@ -42,6 +42,9 @@ constexpr int kInitStab = 64;         // stiffness rows staged in LDS
 #endif
 // the next pop classified and handed to the relax role before the last sift-up of the current
 // one when that sift-up cannot reach the root (stage walks)
+#ifndef AF_INIT_IPARENT
+#define AF_INIT_IPARENT 1
+#endif
 #ifndef AF_INIT_EARLY
 #define AF_INIT_EARLY 1
 #endif
@@ -104,7 +107,12 @@ struct Heap {
   AF_DEV int bz(int k) const { return L->hcell[k] >> 8; }
   AF_DEV int bx(int k) const { return L->hcell[k] & 255; }
   AF_DEV double tb(int k) const { return L->hkey[k]; }
-  AF_DEV static int parent(int t) { return (int)rint((double)t / 2.0); }  // half-even (:123)
+  // round(t / 2), half-even (:123), in integer arithmetic (AF_INIT_IPARENT; 0: through a double)
+  AF_DEV static int parent(int t) {
+    if (!AF_INIT_IPARENT) return (int)rint((double)t / 2.0);
+    const int m = t >> 1;
+    return (t & 1) ? m + (m & 1) : m;
+  }
   AF_DEV void sift(int iz, int ix, int tpc) { sift_up(iz, ix, tpc); }
   // The moving entry stays in registers while it sifts: one round of LDS reads per level (the
   // other entry's key and node), the status writes in the reference's order.

@@ -26,6 +26,9 @@ for PASS in $PASSES; do
     sq2) timeout -s KILL 300 rocprofv3 --pmc SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_INSTS_LDS SQ_INSTS_VMEM SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES SQ_WAIT_INST_LDS --output-format csv -d $OUT/pmc_sq2 -o run -- $B "$@" > $OUT/pmc_sq2.log 2>&1 ;;
     sq3) timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_SALU SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU_CVT --output-format csv -d $OUT/pmc_sq3 -o run -- $B "$@" > $OUT/pmc_sq3.log 2>&1 ;;
     ta) timeout -s KILL 300 rocprofv3 --pmc TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum TCP_PENDING_STALL_CYCLES_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_LATENCY_sum GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d $OUT/pmc_ta -o run -- $B "$@" > $OUT/pmc_ta.log 2>&1 ;;
+    list) timeout -s KILL 120 rocprofv3 -L > $OUT/list.txt 2>&1 ;;
+    ic) timeout -s KILL 120 rocprofv3 --pmc SQC_ICACHE_MISSES SQC_ICACHE_HITS --output-format csv -d $OUT/pmc_ic -o run -- $B "$@" > $OUT/pmc_ic.log 2>&1 ;;
+    ic2) timeout -s KILL 120 rocprofv3 --pmc SQ_IFETCH SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM SQ_INSTS_LDS SQ_INSTS_BRANCH --output-format csv -d $OUT/pmc_ic2 -o run -- $B "$@" > $OUT/pmc_ic2.log 2>&1 ;;
     calib) timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_calib -o run -- $ROOT/tools/micro/fetch_calib > $OUT/pmc_calib.log 2>&1 ;;
     wcalib) timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_wcalib -o run -- $ROOT/tools/micro/write_calib > $OUT/pmc_wcalib.log 2>&1 ;;
     *) echo "unknown pass $PASS"; exit 2 ;;
