@@ -677,7 +677,8 @@ static int travel_chunk(alifmm_ctx* ctx, int sg, int n, const double* scx, const
   }
   // band kernel: members per source and the stripe geometry (KGeom)
   const int K = choose_members(ctx, n, fx);
-  const int wlog = ctx->stripe_log ? ctx->stripe_log : (K >= 8 ? 4 : 6), W = 1 << wlog;
+  // stripe width: 16 columns at 16 members, 32 at 8, 64 below (C4 sweeps, profiles/r6z*)
+  const int wlog = ctx->stripe_log ? ctx->stripe_log : (K >= 16 ? 4 : K >= 8 ? 5 : 6), W = 1 << wlog;
   const long nstripes = (fx + W - 1) / W;
   const long capR = K > 1 ? 2L * fz * ((nstripes + K - 1) / K) + 64 : 0;
   const long ecells = K > 1 ? nstripes * 4L * fz : 0;  // per edge buffer (4 columns per stripe)
