@@ -258,7 +258,31 @@ struct TbLayout {
     return z * pitch + x;
 #endif
   }
+  // at(z, x) == zpart(z) + xpart(x): the bit fields do not overlap, so a stencil's 12 indices
+  // are sums of 5 row parts and 5 column parts
+  AF_DEV int zpart(int z) const {
+#if AF_BRICK
+    return (z >> 2) * (pitch << 4) + ((z & 3) << 2);
+#else
+    return z * pitch;
+#endif
+  }
+  AF_DEV int xpart(int x) const {
+#if AF_BRICK
+    return ((x >> 2) << 4) + (x & 3);
+#else
+    return x;
+#endif
+  }
 };
+// stencil indices from the separable row / column parts (1) or per point (0): boundary cells
+// (load_nb) and interior cells (load_tb)
+#ifndef AF_NB_SEP
+#define AF_NB_SEP 1
+#endif
+#ifndef AF_TB_SEP
+#define AF_TB_SEP 0
+#endif
 
 // Working field -> row-major result for the stripes member `me` owns (s = me, me + K, ...; stripe
 // widths are multiples of 4, so bricks never straddle two owners).  Item = one 4 x 4 brick: one
@@ -322,10 +346,20 @@ AF_DEV void load_tb(NbFieldT& nb, const double* Tb, const TbLayout& L, int nz, i
   nb.iz = z;
   nb.ix = x;
   double t[12];
+  if (AF_TB_SEP) {
+    int zp[5], xp[5];
 #pragma unroll
-  for (int k = 0; k < 12; k++) {
-    const int zz = min(max(z + dz[k], 0), nz - 1), xx = min(max(x + dx[k], 0), nx - 1);
-    t[k] = gld(Tb + L.at(zz, xx));
+    for (int r = 0; r < 5; r++) zp[r] = L.zpart(min(max(z + r - 2, 0), nz - 1));
+#pragma unroll
+    for (int c = 0; c < 5; c++) xp[c] = L.xpart(min(max(x + c - 2, 0), nx - 1));
+#pragma unroll
+    for (int k = 0; k < 12; k++) t[k] = gld(Tb + (zp[dz[k] + 2] + xp[dx[k] + 2]));
+  } else {
+#pragma unroll
+    for (int k = 0; k < 12; k++) {
+      const int zz = min(max(z + dz[k], 0), nz - 1), xx = min(max(x + dx[k], 0), nx - 1);
+      t[k] = gld(Tb + L.at(zz, xx));
+    }
   }
   unsigned m = 0;
 #pragma unroll
@@ -352,22 +386,43 @@ AF_DEV void load_nb(NbFieldT& nb, const double* T, const TbLayout& L, int eprv, 
   bool ot[5];
 #pragma unroll
   for (int r = 0; r < 5; r++) zc[r] = min(max(z + r - 2, 0), g.nz - 1);  // rows z-2 .. z+2 (clamped)
+  int idx[12];
+  if (AF_NB_SEP) {
+    // own points: row part + column part; a column across the stripe boundary (at most the two
+    // on one side: stripes are >= 8 wide) is edge-buffer column ecol(x + dx) = e0 + dx, with e0
+    // from this cell's stripe s and offset r: s * 4 + r on the left edge, s * 4 + r + 4 - W on the right
+    const int W = 1 << g.wlog, r0 = x & (W - 1);
+    const int e0 = ((x >> g.wlog) << 2) + r0 + (r0 < 2 ? 0 : 4 - W);
+    int zp[5];
 #pragma unroll
-  for (int c = 0; c < 5; c++) {  // columns x-2 .. x+2: own (working field) or edge buffer (column-major)
-    ot[c] = g.other(x, c - 2);
-    cb[c] = ot[c] ? eprv + g.ecol(x + c - 2) * g.nz : min(max(x + c - 2, 0), g.nx - 1);
+    for (int r = 0; r < 5; r++) zp[r] = L.zpart(zc[r]);
+#pragma unroll
+    for (int c = 0; c < 5; c++) {
+      ot[c] = g.other(x, c - 2);
+      cb[c] = ot[c] ? eprv + (e0 + c - 2) * g.nz : L.xpart(min(max(x + c - 2, 0), g.nx - 1));
+    }
+#pragma unroll
+    for (int k = 0; k < 12; k++) {
+      const int r = dz[k] + 2, c = dx[k] + 2;
+      idx[k] = ot[c] ? cb[c] + zc[r] : zp[r] + cb[c];  // (in range: no clamp)
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < 5; c++) {  // columns x-2 .. x+2: own (working field) or edge buffer (column-major)
+      ot[c] = g.other(x, c - 2);
+      cb[c] = ot[c] ? eprv + g.ecol(x + c - 2) * g.nz : min(max(x + c - 2, 0), g.nx - 1);
+    }
+#pragma unroll
+    for (int k = 0; k < 12; k++) {
+      const int r = dz[k] + 2, c = dx[k] + 2;
+      const int i = ot[c] ? cb[c] + zc[r] : L.at(zc[r], cb[c]);
+      idx[k] = i < 0 ? 0 : i >= total ? total - 1 : i;
+    }
   }
   double t[12];
   // 32-bit byte offsets (scalar base + vector offset form) while field + edge buffers stay below
   // 4 GB (2^29 doubles, every C1..C5 grid); larger allocations address with 64-bit pointers
   const bool off32 = total < (1 << 29);  // (uniform)
-  int idx[12];
-#pragma unroll
-  for (int k = 0; k < 12; k++) {
-    const int r = dz[k] + 2, c = dx[k] + 2;
-    const int i = ot[c] ? cb[c] + zc[r] : L.at(zc[r], cb[c]);
-    idx[k] = i < 0 ? 0 : i >= total ? total - 1 : i;
-  }
   if (off32) {
 #pragma unroll
     for (int k = 0; k < 12; k++) {
