@@ -113,6 +113,9 @@ constexpr int kBcap = 512 / AF_WG_PER_CU, kDcap = 256 / AF_WG_PER_CU, kRcap = 10
 #define AF_CLAIM_OWN_U 2
 #endif
 constexpr int kCU = AF_CLAIM_OWN_U;
+#ifndef AF_CLAIM_ADAPT
+#define AF_CLAIM_ADAPT 1
+#endif
 #ifndef AF_FB_ROUND
 #define AF_FB_ROUND (128 >> (13 - AF_HASHLOG_D))
 #endif
@@ -1224,69 +1227,77 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
       // another member exactly when it lies across a stripe boundary
       const int W1 = (1 << g.wlog) - 1;
       const bool one = K == 1;
-      for (int q0 = 0; q0 < nItems; q0 += kThreads * kCU) {
-        int r[kCU], s[kCU], pn[kCU][4], si[kCU];
-        unsigned pm[kCU];
+      // kCU items per lane and pass; one (AF_CLAIM_ADAPT) when one pass of one item per thread
+      // holds them all: a second item's instructions would issue for nothing (16 sources: 117.9 ->
+      // 115.6 ms; a one-item last pass after full ones measured slower, profiles/r6x/kab_claim_adapt*)
+      auto claim_pass = [&](auto ucount, int qa, int qb) {
+        constexpr int kU = decltype(ucount)::value;
+        for (int q0 = qa; q0 < qb; q0 += kThreads * kU) {
+          int r[kU], s[kU], pn[kU][4], si[kU];
+          unsigned pm[kU];
 #pragma unroll
-        for (int u = 0; u < kCU; u++) {
-          const int q = q0 + u * kThreads + tid;
-          int c = -1, dd = 4;
-          if (q < nItems) {
-            if (q < 4 * nA) {
-              dd = q & 3;
-              const int ac = lds_items ? alist[q >> 2] : AL.get(q >> 2);
-              const int z = pkz(ac) + (dd == 2 ? -1 : dd == 3 ? 1 : 0);
-              const int x = pkx(ac) + (dd == 0 ? -1 : dd == 1 ? 1 : 0);
-              const int xa = pkx(ac) & W1;
-              // in the grid, and own (claimed by its owner from my rim list otherwise)
-              const bool ok = z >= 0 && z < nz && x >= 0 && x < nx &&
-                              (one || !((dd == 0 && xa == 0) || (dd == 1 && xa == W1)));
-              c = ok ? pk(z, x) : -1;
-            } else {
-              c = lds_items ? RX.lds(q - 4 * nA) : RX.get(q - 4 * nA);
+          for (int u = 0; u < kU; u++) {
+            const int q = q0 + u * kThreads + tid;
+            int c = -1, dd = 4;
+            if (q < nItems) {
+              if (q < 4 * nA) {
+                dd = q & 3;
+                const int ac = lds_items ? alist[q >> 2] : AL.get(q >> 2);
+                const int z = pkz(ac) + (dd == 2 ? -1 : dd == 3 ? 1 : 0);
+                const int x = pkx(ac) + (dd == 0 ? -1 : dd == 1 ? 1 : 0);
+                const int xa = pkx(ac) & W1;
+                // in the grid, and own (claimed by its owner from my rim list otherwise)
+                const bool ok = z >= 0 && z < nz && x >= 0 && x < nx &&
+                                (one || !((dd == 0 && xa == 0) || (dd == 1 && xa == W1)));
+                c = ok ? pk(z, x) : -1;
+              } else {
+                c = lds_items ? RX.lds(q - 4 * nA) : RX.get(q - 4 * nA);
+              }
             }
+            r[u] = c;
+            unsigned m = 0;
+            int idx = 0;
+            {
+              const int cc = max(c, 0), z = pkz(cc), x = pkx(cc), xr = x & W1;
+              // a' = c - dir[d']: (z, x + 1), (z, x - 1), (z + 1, x), (z - 1, x); own iff not across
+              m = (dd > 0 && x + 1 < nx && (one || xr != W1) ? 1u : 0u) | (dd > 1 && x > 0 && (one || xr != 0) ? 2u : 0u) |
+                  (dd > 2 && z + 1 < nz ? 4u : 0u) | (dd > 3 && z > 0 ? 8u : 0u);
+              m = c >= 0 ? m : 0u;
+              idx = SL.at(z, x);
+            }
+            pm[u] = m;
+            si[u] = idx;
           }
-          r[u] = c;
-          unsigned m = 0;
-          int idx = 0;
-          {
-            const int cc = max(c, 0), z = pkz(cc), x = pkx(cc), xr = x & W1;
-            // a' = c - dir[d']: (z, x + 1), (z, x - 1), (z + 1, x), (z - 1, x); own iff not across
-            m = (dd > 0 && x + 1 < nx && (one || xr != W1) ? 1u : 0u) | (dd > 1 && x > 0 && (one || xr != 0) ? 2u : 0u) |
-                (dd > 2 && z + 1 < nz ? 4u : 0u) | (dd > 3 && z > 0 ? 8u : 0u);
-            m = c >= 0 ? m : 0u;
-            idx = SL.at(z, x);
+          // the neighbours' status indices from c's: within the 4 x 8 brick +-1 / +-8, else the
+          // neighbour brick (x: +-25, z: +-(32 pitch - 24))
+          const int zstep = 32 * SL.pitch - 24;
+#pragma unroll
+          for (int u = 0; u < kU; u++) {
+            const int c = max(r[u], 0), xi = pkx(c) & 7, zi = pkz(c) & 3, i0 = si[u];
+  #if AF_BRICK
+            s[u] = r[u] >= 0 ? gld(Sb + i0) : (int)kKnown;
+            pn[u][0] = (pm[u] & 1u) ? gld(Sb + i0 + (xi != 7 ? 1 : 25)) : 0;
+            pn[u][1] = (pm[u] & 2u) ? gld(Sb + i0 - (xi != 0 ? 1 : 25)) : 0;
+            pn[u][2] = (pm[u] & 4u) ? gld(Sb + i0 + (zi != 3 ? 8 : zstep)) : 0;
+            pn[u][3] = (pm[u] & 8u) ? gld(Sb + i0 - (zi != 0 ? 8 : zstep)) : 0;
+  #else
+            s[u] = r[u] >= 0 ? gld(Sb + i0) : (int)kKnown;
+            const int z = pkz(c), x = pkx(c);
+            pn[u][0] = (pm[u] & 1u) ? gld(Sb + SL.at(z, x + 1)) : 0;
+            pn[u][1] = (pm[u] & 2u) ? gld(Sb + SL.at(z, x - 1)) : 0;
+            pn[u][2] = (pm[u] & 4u) ? gld(Sb + SL.at(z + 1, x)) : 0;
+            pn[u][3] = (pm[u] & 8u) ? gld(Sb + SL.at(z - 1, x)) : 0;
+  #endif
           }
-          pm[u] = m;
-          si[u] = idx;
-        }
-        // the neighbours' status indices from c's: within the 4 x 8 brick +-1 / +-8, else the
-        // neighbour brick (x: +-25, z: +-(32 pitch - 24))
-        const int zstep = 32 * SL.pitch - 24;
 #pragma unroll
-        for (int u = 0; u < kCU; u++) {
-          const int c = max(r[u], 0), xi = pkx(c) & 7, zi = pkz(c) & 3, i0 = si[u];
-#if AF_BRICK
-          s[u] = r[u] >= 0 ? gld(Sb + i0) : (int)kKnown;
-          pn[u][0] = (pm[u] & 1u) ? gld(Sb + i0 + (xi != 7 ? 1 : 25)) : 0;
-          pn[u][1] = (pm[u] & 2u) ? gld(Sb + i0 - (xi != 0 ? 1 : 25)) : 0;
-          pn[u][2] = (pm[u] & 4u) ? gld(Sb + i0 + (zi != 3 ? 8 : zstep)) : 0;
-          pn[u][3] = (pm[u] & 8u) ? gld(Sb + i0 - (zi != 0 ? 8 : zstep)) : 0;
-#else
-          s[u] = r[u] >= 0 ? gld(Sb + i0) : (int)kKnown;
-          const int z = pkz(c), x = pkx(c);
-          pn[u][0] = (pm[u] & 1u) ? gld(Sb + SL.at(z, x + 1)) : 0;
-          pn[u][1] = (pm[u] & 2u) ? gld(Sb + SL.at(z, x - 1)) : 0;
-          pn[u][2] = (pm[u] & 4u) ? gld(Sb + SL.at(z + 1, x)) : 0;
-          pn[u][3] = (pm[u] & 8u) ? gld(Sb + SL.at(z - 1, x)) : 0;
-#endif
+          for (int u = 0; u < kU; u++) {
+            const bool mine = pn[u][0] != stampA && pn[u][1] != stampA && pn[u][2] != stampA && pn[u][3] != stampA;
+            emit(mine && !sb_known(s[u]) ? r[u] : -1, s[u]);
+          }
         }
-#pragma unroll
-        for (int u = 0; u < kCU; u++) {
-          const bool mine = pn[u][0] != stampA && pn[u][1] != stampA && pn[u][2] != stampA && pn[u][3] != stampA;
-          emit(mine && !sb_known(s[u]) ? r[u] : -1, s[u]);
-        }
-      }
+      };
+      if (AF_CLAIM_ADAPT && nItems <= kThreads) claim_pass(std::integral_constant<int, 1>{}, 0, nItems);
+      else claim_pass(std::integral_constant<int, kCU>{}, 0, nItems);
     }
     // this step's edge-buffer stores (accept scan, P0) precede this step's commits to the same
     // addresses (a wave that issued no load since has not waited for them yet)
