@@ -113,6 +113,10 @@ constexpr int kBcap = 512 / AF_WG_PER_CU, kDcap = 256 / AF_WG_PER_CU, kRcap = 10
 #define AF_CLAIM_OWN_U 2
 #endif
 constexpr int kCU = AF_CLAIM_OWN_U;
+// the boundary list read in place after the interior one (1) or copied behind it (0)
+#ifndef AF_BL_INPLACE
+#define AF_BL_INPLACE 1
+#endif
 #ifndef AF_CLAIM_ADAPT
 #define AF_CLAIM_ADAPT 1
 #endif
@@ -1314,7 +1318,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
 #endif
     const int nEi = min((int)(unsigned)sh->nE2, capC);
     const int nEb = min((int)(unsigned)(sh->nE2 >> 32), capC - nEi);
-    if (nEb > 0) {  // boundary cells after the interior ones
+    if (!AF_BL_INPLACE && nEb > 0) {  // boundary cells after the interior ones
       for (int j2 = tid; j2 < nEb; j2 += kThreads) {
         EL.put(nEi + j2, BL.get(j2));
         EP.put(nEi + j2, BP.get(j2));
@@ -1326,8 +1330,20 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
     const long long tev0 = PROF ? wall_clock64() : 0;
 #endif
     const int nE = nEi + nEb;
+    // the claimed cells as one list: interior (EL / EP), then boundary (BL / BP), read in place
+    // (AF_BL_INPLACE) or from EL / EP after the copy above; VL and the fallback list index it
+    auto cellE = [&](int e, auto lds_only) {
+      constexpr bool LO = decltype(lds_only)::value;
+      if (AF_BL_INPLACE && e >= nEi) return LO ? BL.lds(e - nEi) : BL.get(e - nEi);
+      return LO ? EL.lds(e) : EL.get(e);
+    };
+    auto slotE = [&](int e, auto lds_only) {
+      constexpr bool LO = decltype(lds_only)::value;
+      if (AF_BL_INPLACE && e >= nEi) return LO ? BP.lds(e - nEi) : BP.get(e - nEi);
+      return LO ? EP.lds(e) : EP.get(e);
+    };
     // ---- P4: evaluate ----
-    const bool lds_e = nE <= kEcap;
+    const bool lds_e = nE <= kEcap && (!AF_BL_INPLACE || nEb <= kBcap);  // (uniform) every list in LDS
     const double dnx_e = launder_u(R.dnx);
     auto eval_done = [&](int e, double v) {
       if (lds_e) VL.put_lds(e, v);
@@ -1350,7 +1366,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
     for (int j = tid; j < nE; j += kThreads) {
       const int e = AF_EVAL_BFIRST ? (j < nEb ? nEi + j : j - nEb) : j;
       const bool interior = AF_EVAL_BFIRST ? j - lane >= nEb : e - lane + 64 <= nEi;  // (wave-uniform)
-      const int r = lds_e ? EL.lds(e) : EL.get(e);
+      const int r = lds_e ? cellE(e, std::true_type{}) : cellE(e, std::false_type{});
       const int z = pkz(r), x = pkx(r);
       NbFieldT nb;
       if (interior) load_tb(nb, Tb, TL, nz, nx, z, x);
@@ -1411,7 +1427,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
           const int q = r0 + i / 25, o = i % 25;
           const int e = q < nlist ? sh->Rx[q] : q - nlist;
           if (q >= nlist && VL.get(e) != -1.0) continue;  // scan part: fallback cells only
-          const int c = EL.get(e);
+          const int c = cellE(e, std::false_type{});
           const int zz = pkz(c) + o / 5 - 2, xx = pkx(c) + o % 5 - 2;
           double t = 0.0;
           bool kn = false;
@@ -1438,7 +1454,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
             const int q = r0 + ci;
             const int e = q < nlist ? sh->Rx[q] : q - nlist;
             if (q < nlist || VL.get(e) == -1.0) {  // (the same for the cell's four lanes)
-              const int c = EL.get(e);
+              const int c = cellE(e, std::false_type{});
               const int z = pkz(c), x = pkx(c);
               const Win5 F{win + 25 * ci, wmask[ci], z, x};
               const CellMat cm = band_mat<LDSMAT, MODE == 0>(M, sh->mat, sh->stab, R.mv, z, x);
@@ -1458,7 +1474,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
           const int q = r0 + tid;
           const int e = q < nlist ? sh->Rx[q] : q - nlist;
           if (q < nlist || VL.get(e) == -1.0) {
-            const int c = EL.get(e);
+            const int c = cellE(e, std::false_type{});
             const int z = pkz(c), x = pkx(c);
             const Win5 F{win + 25 * tid, wmask[tid], z, x};
             const CellMat cm = band_mat<LDSMAT, MODE == 0>(M, sh->mat, sh->stab, R.mv, z, x);
@@ -1489,9 +1505,9 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
         int r = 0;
         double v = 0.0;
         if (e < nE) {
-          r = LO ? EL.lds(e) : EL.get(e);
+          r = cellE(e, lds_only);
           v = LO ? VL.lds(e) : VL.get(e);
-          const int p = LO ? EP.lds(e) : EP.get(e);
+          const int p = slotE(e, lds_only);
           gst(Tb + TL.at(pkz(r), pkx(r)), v);
           ed = g.edge(pkx(r));
           if (ed) xst(Epar + g.eidx(pkz(r), pkx(r)), v, (bool)sh->xl);
@@ -1525,7 +1541,7 @@ __global__ __launch_bounds__(kThreads) AF_WPE_ATTR void fmm_band_k_kernel(BandPa
         }
       }
     };
-    if (nE <= kEcap && hi + nE <= kLcap) commit(std::true_type{});
+    if (nE <= kEcap && (!AF_BL_INPLACE || nEb <= kBcap) && hi + nE <= kLcap) commit(std::true_type{});
     else commit(std::false_type{});
     __syncthreads();
     // No barrier at the step's end: the next step's first reads of what this end writes are behind
